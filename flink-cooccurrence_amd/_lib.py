@@ -1,0 +1,150 @@
+"""ctypes binding of include/cooc.h (the C-ABI of libcooc_hip.so).
+
+This is the Python counterpart of the JNI/Panama stubs in INTEGRATION.md: same entry points,
+same two-phase copy protocol.  Loading fails loudly when the HIP library is missing — the product
+path has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "csrc", "libcooc_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "cooc.h")
+
+COOC_OK = 0
+COOC_ERR_ARG = 1
+COOC_ERR_STATE = 2
+COOC_ERR_HIP = 3
+COOC_ERR_OOM = 4
+COOC_ERR_OVERFLOW = 5
+COOC_FLAG_EXACT_SCORES = 1
+
+i16p = ctypes.POINTER(ctypes.c_int16)
+i32p = ctypes.POINTER(ctypes.c_int32)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+i64p = ctypes.POINTER(ctypes.c_int64)
+f64p = ctypes.POINTER(ctypes.c_double)
+vp = ctypes.c_void_p
+
+
+class CoocConfig(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("n_items", ctypes.c_int32),
+        ("topk", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("window_size_ms", ctypes.c_int64),
+    ]
+
+
+class CoocWindowInfo(ctypes.Structure):
+    _fields_ = [
+        ("ts", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("observed", ctypes.c_int64),
+        ("n_rows", ctypes.c_int32),
+        ("topk", ctypes.c_int32),
+        ("n_topk", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class CoocDeviceResult(ctypes.Structure):
+    _fields_ = [
+        ("n_items", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("observed", ctypes.c_int64),
+        ("row_base", vp),
+        ("row_nnz", vp),
+        ("col", vp),
+        ("cnt", vp),
+        ("rowsum", vp),
+    ]
+
+
+_SIGS = {
+    "cooc_abi_version": (ctypes.c_int, []),
+    "cooc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "cooc_create": (ctypes.c_int, [ctypes.POINTER(CoocConfig), ctypes.POINTER(vp)]),
+    "cooc_destroy": (None, [vp]),
+    "cooc_last_error": (ctypes.c_char_p, [vp]),
+    "cooc_count_device": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
+                                         ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),
+    "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
+    "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),
+    "cooc_finish_window": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(CoocWindowInfo)]),
+    "cooc_copy_window_delta": (ctypes.c_int, [vp, i32p, i64p, i32p, u32p, i16p]),
+    "cooc_copy_window_rowsums": (ctypes.c_int, [vp, i32p, i64p, i32p]),
+    "cooc_copy_window_topk": (ctypes.c_int, [vp, i32p, i32p, i32p, f64p]),
+    "cooc_global_rowsums": (ctypes.c_int, [vp, i64p, i32p]),
+    "cooc_global_observed": (ctypes.c_int, [vp, i64p, i64p]),
+    "cooc_global_row_nnz": (ctypes.c_int, [vp, ctypes.c_int32, i64p]),
+    "cooc_global_row": (ctypes.c_int, [vp, ctypes.c_int32, i32p, u32p, i16p]),
+    "cooc_op_process_elements": (ctypes.c_int, [vp, ctypes.c_int64, i32p, i32p, i64p, i64p]),
+    "cooc_op_process_watermark": (ctypes.c_int, [vp, ctypes.c_int64, i32p, ctypes.POINTER(CoocWindowInfo)]),
+    "cooc_op_counters": (ctypes.c_int, [vp, i64p]),
+    "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
+    "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+}
+
+_lib = None
+
+
+class HipLibraryMissing(RuntimeError):
+    pass
+
+
+def header_symbols() -> list[str]:
+    """Every function include/cooc.h declares (the symbol contract of the library)."""
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"^COOC_API\s+[\w\s\*]*?\b(cooc_\w+)\(", text, re.M)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipLibraryMissing(
+            f"{LIB_PATH} is missing: build it with __graft_entry__.build() (make -C flink-cooccurrence_amd/csrc). "
+            "The co-occurrence core has no CPU fallback."
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class CoocError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[{status}] {msg}")
+        self.status = status
+
+
+class IllegalArgumentException(CoocError, ValueError):
+    pass
+
+
+class IllegalStateException(CoocError):
+    pass
+
+
+def check(status: int, ctx=None):
+    if status == COOC_OK:
+        return
+    L = load()
+    msg = (L.cooc_last_error(ctx) or b"").decode(errors="replace")
+    if not msg:
+        msg = L.cooc_status_string(status).decode()
+    if status == COOC_ERR_ARG:
+        raise IllegalArgumentException(status, msg)
+    if status == COOC_ERR_STATE:
+        raise IllegalStateException(status, msg)
+    raise CoocError(status, msg)

@@ -1,0 +1,268 @@
+"""Host-side mirror of the reference's operator interface over the C-ABI.
+
+The reference (Java, Flink 1.3.2) cannot be built here, so the host side above the C-ABI mirrors its
+operator surface with the same names, argument meaning and error behaviour:
+
+* ``NonSampledUserInteractionCounterOneInputStreamOperator`` —
+  NonSampledUserInteractionCounterOneInputStreamOperator.java:31-178 (constructor ``(windowSize,
+  windowUnit)`` :61, ``processElement`` :84-110, ``onEventTime`` :113-165) fused with the two window
+  aggregators it feeds (ItemRowAggregator.java:15-57, RowSumAggregator.java:15-72) and the rescorer
+  (ItemRowRescorerTwoInputStreamOperator.java:22-246, constructor ``(short topK)`` :51-56).
+  ``process_watermark`` returns the fired windows' outputs: per-window delta rows (the
+  ``Tuple2<Integer, Int2ShortOpenHashMap>`` records), row-sum updates (``Tuple2<Integer,Integer>``)
+  and the top-k queues (``Tuple2<Integer, IntDoublePriorityQueue>``).
+* ``CooccurrenceCore`` — one C-ABI context: the stateless one-window batch (``count``,
+  ``count_device``) and the streaming window API (``submit_batch`` / ``finish_window``).
+
+Every compute call goes through libcooc_hip.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import (CoocConfig, CoocDeviceResult, CoocWindowInfo, check, f64p, i16p, i32p, i64p, u32p)
+
+# Configuration.java:160-182 window units -> milliseconds (Time.of(size, unit).toMilliseconds())
+_UNIT_MS = {"MILLISECONDS": 1, "SECONDS": 1000, "MINUTES": 60_000, "HOURS": 3_600_000, "DAYS": 86_400_000}
+
+
+def window_size_ms(size: int, unit: str = "MILLISECONDS") -> int:
+    u = unit.upper()
+    if u not in _UNIT_MS:
+        raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"Unrecognized window unit {unit}")  # :176-177
+    return int(size) * _UNIT_MS[u]
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+@dataclass
+class BatchResult:
+    """C of one window over empty histories, as a packed CSR over all n_items rows."""
+    row_ptr: np.ndarray   # int64 [M+1]
+    cols: np.ndarray      # int32 [nnz], ascending within a row
+    cnt: np.ndarray       # uint32 [nnz] exact
+    cnt16: np.ndarray     # int16 [nnz]   Int2ShortOpenHashMap view
+    rowsum: np.ndarray    # int64 [M] exact
+    rowsum32: np.ndarray  # int32 [M]     Java int view
+    observed: int         # sum_u n_u (n_u - 1)
+
+
+@dataclass
+class WindowResult:
+    """One fired window's observable outputs (same layout as oracle.WindowOutput)."""
+    ts: int
+    rows: np.ndarray
+    row_ptr: np.ndarray
+    cols: np.ndarray
+    exact: np.ndarray
+    v16: np.ndarray
+    rs_items: np.ndarray
+    rs_exact: np.ndarray
+    rs_v32: np.ndarray
+    observed: int
+    topk_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    topk_sizes: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    topk_values: np.ndarray = field(default_factory=lambda: np.zeros((0, 0), np.int32))
+    topk_scores: np.ndarray = field(default_factory=lambda: np.zeros((0, 0), np.float64))
+
+
+class CooccurrenceCore:
+    """One context of the C-ABI (one Flink subtask)."""
+
+    def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
+                 exact_scores: bool = False):
+        L = _lib.load()
+        cfg = CoocConfig(device, n_items, topk, _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0, window_size_ms)
+        h = ctypes.c_void_p()
+        check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
+        self._h = h
+        self.n_items = n_items
+        self.topk = topk
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().cooc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- stateless one-window batch -------------------------------------------------------------
+    def count_device(self, user_ptr, items, stream=None) -> CoocDeviceResult:
+        """user_ptr: int64 device tensor [U+1] (user_ptr[0] == 0); items: int32 device tensor."""
+        res = CoocDeviceResult()
+        n_users = int(user_ptr.numel()) - 1
+        sp = None if stream is None else ctypes.c_void_p(int(stream))
+        check(_lib.load().cooc_count_device(self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()),
+                                            ctypes.c_void_p(items.data_ptr()), int(items.numel()), sp,
+                                            ctypes.byref(res)), self._h)
+        return res
+
+    def count(self, user_ptr, items) -> BatchResult:
+        up = np.ascontiguousarray(user_ptr, np.int64)
+        it = np.ascontiguousarray(items, np.int32)
+        info = CoocWindowInfo()
+        L = _lib.load()
+        check(L.cooc_count_host(self._h, len(up) - 1, _p(up, i64p), _p(it, i32p), ctypes.byref(info)), self._h)
+        return self.copy_batch(info.nnz, info.observed)
+
+    def copy_batch(self, nnz: int, observed: int) -> BatchResult:
+        M = self.n_items
+        rp = np.zeros(M + 1, np.int64)
+        cols = np.zeros(nnz, np.int32)
+        cnt = np.zeros(nnz, np.uint32)
+        cnt16 = np.zeros(nnz, np.int16)
+        rs = np.zeros(M, np.int64)
+        rs32 = np.zeros(M, np.int32)
+        check(_lib.load().cooc_copy_batch(self._h, _p(rp, i64p), _p(cols, i32p), _p(cnt, u32p), _p(cnt16, i16p),
+                                          _p(rs, i64p), _p(rs32, i32p)), self._h)
+        return BatchResult(rp, cols, cnt, cnt16, rs, rs32, int(observed))
+
+    def set_kernel_timing(self, enable: bool = True) -> None:
+        check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        check(_lib.load().cooc_last_kernel_ms(self._h, ctypes.byref(ms)), self._h)
+        return ms.value
+
+    # ---- streaming windows ----------------------------------------------------------------------
+    def submit_batch(self, window_ts: int, user_ids, user_ptr, items) -> None:
+        uid = np.ascontiguousarray(user_ids, np.int32)
+        up = np.ascontiguousarray(user_ptr, np.int64)
+        it = np.ascontiguousarray(items, np.int32)
+        check(_lib.load().cooc_submit_batch(self._h, window_ts, len(uid), _p(uid, i32p), _p(up, i64p),
+                                            _p(it, i32p)), self._h)
+
+    def finish_window(self, window_ts: int) -> WindowResult:
+        info = CoocWindowInfo()
+        check(_lib.load().cooc_finish_window(self._h, window_ts, ctypes.byref(info)), self._h)
+        return self._window(info)
+
+    def _window(self, info: CoocWindowInfo) -> WindowResult:
+        L = _lib.load()
+        R, nnz = info.n_rows, info.nnz
+        rows = np.zeros(R, np.int32)
+        rp = np.zeros(R + 1, np.int64)
+        cols = np.zeros(nnz, np.int32)
+        cnt = np.zeros(nnz, np.uint32)
+        cnt16 = np.zeros(nnz, np.int16)
+        check(L.cooc_copy_window_delta(self._h, _p(rows, i32p), _p(rp, i64p), _p(cols, i32p), _p(cnt, u32p),
+                                       _p(cnt16, i16p)), self._h)
+        rs_items = np.zeros(R, np.int32)
+        rs = np.zeros(R, np.int64)
+        rs32 = np.zeros(R, np.int32)
+        check(L.cooc_copy_window_rowsums(self._h, _p(rs_items, i32p), _p(rs, i64p), _p(rs32, i32p)), self._h)
+        w = WindowResult(info.ts, rows, rp, cols, cnt.astype(np.int64), cnt16, rs_items, rs, rs32, info.observed)
+        if info.topk > 0:
+            k = info.topk
+            tr = np.zeros(info.n_topk, np.int32)
+            ts = np.zeros(info.n_topk, np.int32)
+            tv = np.zeros((info.n_topk, k), np.int32)
+            tsc = np.zeros((info.n_topk, k), np.float64)
+            if info.n_topk:
+                check(L.cooc_copy_window_topk(self._h, _p(tr, i32p), _p(ts, i32p), _p(tv, i32p), _p(tsc, f64p)),
+                      self._h)
+            w.topk_rows, w.topk_sizes, w.topk_values, w.topk_scores = tr, ts, tv, tsc
+        return w
+
+    def global_rowsums(self):
+        M = self.n_items
+        ex = np.zeros(M, np.int64)
+        v32 = np.zeros(M, np.int32)
+        check(_lib.load().cooc_global_rowsums(self._h, _p(ex, i64p), _p(v32, i32p)), self._h)
+        return ex, v32
+
+    def global_observed(self):
+        ex = ctypes.c_int64()
+        ref = ctypes.c_int64()
+        check(_lib.load().cooc_global_observed(self._h, ctypes.byref(ex), ctypes.byref(ref)), self._h)
+        return ex.value, ref.value
+
+    def global_row(self, item: int):
+        L = _lib.load()
+        n = ctypes.c_int64()
+        check(L.cooc_global_row_nnz(self._h, item, ctypes.byref(n)), self._h)
+        cols = np.zeros(n.value, np.int32)
+        cnt = np.zeros(n.value, np.uint32)
+        cnt16 = np.zeros(n.value, np.int16)
+        check(L.cooc_global_row(self._h, item, _p(cols, i32p), _p(cnt, u32p), _p(cnt16, i16p)), self._h)
+        return cols, cnt, cnt16
+
+    # ---- operator mirror ------------------------------------------------------------------------
+    def op_process_elements(self, users, items, ts) -> int:
+        u = np.ascontiguousarray(users, np.int32)
+        i = np.ascontiguousarray(items, np.int32)
+        t = np.ascontiguousarray(ts, np.int64)
+        late = ctypes.c_int64()
+        check(_lib.load().cooc_op_process_elements(self._h, len(u), _p(u, i32p), _p(i, i32p), _p(t, i64p),
+                                                   ctypes.byref(late)), self._h)
+        return late.value
+
+    def op_process_watermark(self, watermark: int) -> list[WindowResult]:
+        out = []
+        L = _lib.load()
+        while True:
+            fired = ctypes.c_int32()
+            info = CoocWindowInfo()
+            check(L.cooc_op_process_watermark(self._h, watermark, ctypes.byref(fired), ctypes.byref(info)), self._h)
+            if not fired.value:
+                return out
+            out.append(self._window(info))
+
+    def op_counters(self) -> dict:
+        a = np.zeros(5, np.int64)
+        check(_lib.load().cooc_op_counters(self._h, _p(a, i64p)), self._h)
+        return {
+            "UserInteractionCounterLateElements": int(a[0]),
+            "UserInteractionCounterObservedCooccurrences": int(a[1]),
+            "RowSumProcessWindowRowSum": int(a[2]),
+            "ItemRowRescorerRescoredItems": int(a[3]),
+            "rescorer_observed": int(a[4]),
+        }
+
+
+class NonSampledUserInteractionCounterOneInputStreamOperator:
+    """Drop-in for the `--skip-cuts` operator chain (FlinkCooccurrences.java:65-74,135-167).
+
+    ``NonSampledUserInteractionCounterOneInputStreamOperator(windowSize, windowUnit)`` plus the
+    rescorer's ``topK`` (ItemRowRescorerTwoInputStreamOperator(short topK), :51-56) and the item-id
+    universe the device tables are sized for.
+    """
+
+    ITEM_TAG = "itemCooccurrences"  # NonSampled...java:41-42
+    ROW_SUM_TAG = "rowSums"         # NonSampled...java:45-46
+
+    def __init__(self, window_size: int, window_unit: str = "MILLISECONDS", *, n_items: int, top_k: int = 10,
+                 device: int = -1, exact_scores: bool = False):
+        if top_k <= 0:  # ItemRowRescorer...java:52-54
+            raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"{top_k} is <= 0")
+        self.core = CooccurrenceCore(n_items, top_k, window_size_ms(window_size, window_unit), device, exact_scores)
+
+    def process_element(self, user: int, item: int, timestamp: int) -> bool:
+        """Returns True when the record was late and dropped (NonSampled...java:89-91)."""
+        return self.core.op_process_elements([user], [item], [timestamp]) == 1
+
+    def process_elements(self, users, items, timestamps) -> int:
+        return self.core.op_process_elements(users, items, timestamps)
+
+    def process_watermark(self, watermark: int) -> list[WindowResult]:
+        return self.core.op_process_watermark(watermark)
+
+    def accumulators(self) -> dict:
+        return self.core.op_counters()
+
+    def close(self):
+        self.core.close()

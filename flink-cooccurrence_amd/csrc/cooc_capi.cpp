@@ -1,0 +1,180 @@
+// cooc_capi.cpp — the C-ABI of include/cooc.h over the HIP pipeline (cooc_count.hip) and the
+// resident streaming state (cooc_stream.cpp).  Error behaviour mirrors the reference: argument
+// errors (IllegalArgumentException, e.g. ItemRowRescorer...java:52-54) -> COOC_ERR_ARG, state
+// errors (IllegalStateException, e.g. ItemRowRescorer...java:72-79,91-93) -> COOC_ERR_STATE.
+#include "cooc_ctx.h"
+
+#include <cstring>
+#include <vector>
+
+using cooc::Status;
+
+namespace {
+
+int fail(cooc_ctx *ctx, const Status &s) {
+  if (ctx) ctx->last_error = s.msg;
+  return s.code;
+}
+
+int fail(cooc_ctx *ctx, int code, const std::string &msg) { return fail(ctx, Status{code, msg}); }
+
+}  // namespace
+
+extern "C" {
+
+int cooc_abi_version(void) { return COOC_ABI_VERSION; }
+
+const char *cooc_status_string(int status) {
+  switch (status) {
+    case COOC_OK: return "ok";
+    case COOC_ERR_ARG: return "invalid argument";
+    case COOC_ERR_STATE: return "invalid state";
+    case COOC_ERR_HIP: return "HIP runtime error";
+    case COOC_ERR_OOM: return "device out of memory";
+    case COOC_ERR_OVERFLOW: return "uint32 count overflow";
+    default: return "unknown status";
+  }
+}
+
+int cooc_create(const cooc_config *cfg, cooc_ctx **out) {
+  if (!cfg || !out) return COOC_ERR_ARG;
+  *out = nullptr;
+  auto ctx = std::make_unique<cooc_ctx>();
+  Status s = ctx->init(*cfg);
+  if (!s.ok()) {
+    // no context to carry the message: keep it in a thread-local for cooc_last_error(NULL)
+    cooc_ctx::create_error() = s.msg;
+    return s.code;
+  }
+  *out = ctx.release();
+  return COOC_OK;
+}
+
+void cooc_destroy(cooc_ctx *ctx) { delete ctx; }
+
+const char *cooc_last_error(const cooc_ctx *ctx) {
+  return ctx ? ctx->last_error.c_str() : cooc_ctx::create_error().c_str();
+}
+
+int cooc_count_device(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                      int64_t n_interactions, void *hip_stream, cooc_device_result *out) {
+  if (!ctx || !out) return COOC_ERR_ARG;
+  if (n_users < 0 || n_interactions < 0 || (n_users > 0 && (!d_user_ptr || (n_interactions > 0 && !d_items))))
+    return fail(ctx, COOC_ERR_ARG, "bad CSR arguments");
+  Status s = ctx->count_device(n_users, d_user_ptr, d_items, n_interactions,
+                               hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream, out);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
+                    cooc_window_info *info) {
+  if (!ctx || !info) return COOC_ERR_ARG;
+  if (n_users < 0 || (n_users > 0 && !user_ptr)) return fail(ctx, COOC_ERR_ARG, "bad CSR arguments");
+  Status s = ctx->count_host(n_users, user_ptr, items, info);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
+                    int32_t *rowsum32) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->copy_batch(row_ptr, cols, cnt, cnt16, rowsum, rowsum32);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_submit_batch(cooc_ctx *ctx, int64_t window_ts, int32_t n_users, const int32_t *user_ids,
+                      const int64_t *user_ptr, const int32_t *items) {
+  if (!ctx) return COOC_ERR_ARG;
+  if (n_users < 0 || (n_users > 0 && (!user_ids || !user_ptr))) return fail(ctx, COOC_ERR_ARG, "bad batch arguments");
+  Status s = ctx->stream_state.submit(*ctx, window_ts, n_users, user_ids, user_ptr, items);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_info *info) {
+  if (!ctx || !info) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.finish(*ctx, window_ts, info);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,
+                           int16_t *cnt16) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.copy_delta(*ctx, rows, row_ptr, cols, cnt, cnt16);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_copy_window_rowsums(cooc_ctx *ctx, int32_t *items, int64_t *delta, int32_t *delta32) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.copy_rowsums(*ctx, items, delta, delta32);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_copy_window_topk(cooc_ctx *ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.copy_topk(*ctx, rows, sizes, values, scores);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_global_rowsums(cooc_ctx *ctx, int64_t *exact, int32_t *v32) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.global_rowsums(*ctx, exact, v32);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_global_observed(cooc_ctx *ctx, int64_t *exact, int64_t *rescorer) {
+  if (!ctx) return COOC_ERR_ARG;
+  if (exact) *exact = ctx->stream_state.observed_exact;
+  if (rescorer) *rescorer = ctx->stream_state.observed_ref;
+  return COOC_OK;
+}
+
+int cooc_global_row_nnz(cooc_ctx *ctx, int32_t item, int64_t *nnz) {
+  if (!ctx || !nnz) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.global_row_nnz(*ctx, item, nnz);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_global_row(cooc_ctx *ctx, int32_t item, int32_t *cols, uint32_t *cnt, int16_t *cnt16) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->stream_state.global_row(*ctx, item, cols, cnt, cnt16);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_op_process_elements(cooc_ctx *ctx, int64_t n, const int32_t *users, const int32_t *items,
+                             const int64_t *ts, int64_t *n_late) {
+  if (!ctx) return COOC_ERR_ARG;
+  if (n < 0 || (n > 0 && (!users || !items || !ts))) return fail(ctx, COOC_ERR_ARG, "bad element arrays");
+  Status s = ctx->op.process_elements(*ctx, n, users, items, ts, n_late);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_op_process_watermark(cooc_ctx *ctx, int64_t watermark, int32_t *fired, cooc_window_info *info) {
+  if (!ctx || !fired || !info) return COOC_ERR_ARG;
+  Status s = ctx->op.process_watermark(*ctx, watermark, fired, info);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_op_counters(cooc_ctx *ctx, int64_t *counters5) {
+  if (!ctx || !counters5) return COOC_ERR_ARG;
+  counters5[0] = ctx->op.late_elements;
+  counters5[1] = ctx->stream_state.observed_exact;
+  counters5[2] = ctx->stream_state.rowsum_acc;
+  counters5[3] = ctx->stream_state.rescored_items;
+  counters5[4] = ctx->stream_state.observed_ref;
+  return COOC_OK;
+}
+
+int cooc_set_kernel_timing(cooc_ctx *ctx, int32_t enable) {
+  if (!ctx) return COOC_ERR_ARG;
+  ctx->timer.enabled = enable != 0;
+  return COOC_OK;
+}
+
+int cooc_last_kernel_ms(cooc_ctx *ctx, float *accumulate_ms) {
+  if (!ctx || !accumulate_ms) return COOC_ERR_ARG;
+  if (!ctx->timer.enabled) return fail(ctx, COOC_ERR_STATE, "kernel timing is off");
+  hipError_t e = hipEventElapsedTime(accumulate_ms, ctx->timer.acc_begin, ctx->timer.acc_end);
+  if (e != hipSuccess) return fail(ctx, COOC_ERR_HIP, std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
+  return COOC_OK;
+}
+
+}  // extern "C"

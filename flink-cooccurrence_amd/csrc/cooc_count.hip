@@ -1,0 +1,593 @@
+// cooc_count.hip — the hot path: pair expansion + keyed (itemA, itemB) count reduction on gfx950.
+//
+// Reference semantics restated (see cooc_device.h for the contribution form):
+//   NonSampledUserInteractionCounterOneInputStreamOperator.java:113-165   pair emission
+//   ItemRowAggregator.java:26-31                                            per-(itemA, window) row reduce
+//   RowSumAggregator.java:25-27,54-71                                       per-(item, window) row-sum reduce
+//
+// Pipeline for one window (all on one HIP stream):
+//   1. k_build_contribs   one record per (user, position): key = the row item, value = (user, kind)
+//   2. radix sort by row  (hipCUB onesweep, ceil(log2 M) key bits) — the keyBy(item) regrouping
+//   3. k_row_ptr          CSR row pointer of the row-sorted contributions
+//   4. inclusive scan     of each contribution's segment length = its pair work
+//   5. k_plan_rows        per-row work, split into chunks of <= kChunkWork pairs, output capacity
+//   6. k_make_chunks      chunk table, heaviest rows first
+//   7. k_accumulate       ★ persistent: per chunk a dense M-counter LDS row, one ds_add_u32 per pair,
+//                           compacted in column order into the padded CSR (or flushed into a
+//                           staging row when the row is split over chunks)
+//   8. k_finalize_split   compacts staging rows of split rows
+// HBM model per window: the ordered pairs P stream 4 B partner ids (mostly served by MALL/L2:
+// every user list is re-read once per item in it), 12 B per output entry; see DESIGN.md.
+#include <hipcub/hipcub.hpp>
+
+#include "cooc_device.h"
+
+namespace cooc {
+
+namespace {
+
+constexpr int kAccThreads = 1024;
+constexpr int kAccWaves = kAccThreads / 64;
+constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
+constexpr int kMaxLdsCounters = (160 * 1024 - 1024) / 4;  // dense row in LDS (uint32 counters)
+
+template <class T>
+__device__ inline int64_t lower_bound_i64(const T *a, int64_t n, T x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// ---- 1. contributions ---------------------------------------------------------------------------
+// One wave per active user: lanes walk its history.  Key = the item at the position (the row the
+// contribution adds into), value = (active index << 1) | (position is OLD).  Validates item ids.
+__global__ __launch_bounds__(256) void k_build_contribs(int64_t n_active, const int64_t *__restrict__ off,
+                                                        const int32_t *__restrict__ len,
+                                                        const int32_t *__restrict__ old,
+                                                        const int64_t *__restrict__ cbase,
+                                                        const int32_t *__restrict__ arena, int32_t M,
+                                                        uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                        int64_t *__restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  bool bad = false;
+  for (int64_t j = wave; j < n_active; j += n_waves) {
+    const int32_t *h = arena + off[j];
+    const int32_t n = len[j], o = old[j];
+    const int64_t base = cbase[j];
+    for (int32_t p = lane; p < n; p += 64) {
+      int32_t item = h[p];
+      if (item < 0 || item >= M) { bad = true; item = 0; }
+      keys[base + p] = uint32_t(item);
+      vals[base + p] = (uint32_t(j) << 1) | uint32_t(p < o);
+    }
+  }
+  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(err), 1ull);
+}
+
+// ---- 3. row pointer -------------------------------------------------------------------------------
+__global__ void k_row_ptr(const uint32_t *__restrict__ keys, int64_t n, int32_t M, int64_t *__restrict__ row_ptr) {
+  const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (a <= M) row_ptr[a] = lower_bound_i64<uint32_t>(keys, n, uint32_t(a));
+}
+
+struct WorkOp {  // pair work of a contribution = its segment length
+  const int32_t *len;
+  const int32_t *old;
+  __host__ __device__ int64_t operator()(uint32_t v) const {
+    const uint32_t j = v >> 1;
+    return (v & 1u) ? int64_t(len[j] - old[j]) : int64_t(len[j]);
+  }
+};
+
+// ---- 5. per-row plan ------------------------------------------------------------------------------
+__global__ void k_plan_rows(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ epre, int32_t M,
+                            uint64_t *__restrict__ row_work, int32_t *__restrict__ order,
+                            int32_t *__restrict__ row_nch, int64_t *__restrict__ row_cap,
+                            int32_t *__restrict__ row_split) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  const int64_t c0 = row_ptr[a], c1 = row_ptr[a + 1];
+  const int64_t w = epre[c1] - epre[c0];
+  const int32_t nch = c1 > c0 ? int32_t(w > kChunkWork ? (w + kChunkWork - 1) / kChunkWork : 1) : 0;
+  row_work[a] = uint64_t(w);
+  order[a] = a;
+  row_nch[a] = nch;
+  row_cap[a] = c1 > c0 ? (w < M ? w : int64_t(M)) : 0;
+  row_split[a] = nch > 1 ? 1 : 0;
+}
+
+__global__ void k_gather_i32(const int32_t *__restrict__ order, const int32_t *__restrict__ src, int32_t n,
+                             int32_t *__restrict__ dst) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[order[i]];
+}
+
+__global__ void k_split_rows(const int32_t *__restrict__ row_split, const int32_t *__restrict__ split_slot,
+                             int32_t M, int32_t *__restrict__ split_row) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < M && row_split[a]) split_row[split_slot[a]] = a;
+}
+
+__global__ void k_totals(const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_base,
+                         const int32_t *__restrict__ split_slot, const int64_t *__restrict__ epre, int32_t M,
+                         int64_t n_contrib, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue) {
+  tot->n_chunks = ord_cbase[M];
+  tot->cap_total = row_base[M];
+  tot->n_split = split_slot[M];
+  tot->work_total = epre[n_contrib];
+  tot->nnz_total = 0;
+  queue[0] = 0;
+  queue[1] = 0;
+}
+
+// ---- 6. chunk table -------------------------------------------------------------------------------
+__global__ void k_make_chunks(const int32_t *__restrict__ order, const int32_t *__restrict__ ord_nch,
+                              const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_ptr,
+                              const int64_t *__restrict__ epre, const int32_t *__restrict__ split_slot, int32_t M,
+                              Chunk *__restrict__ chunks) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= M) return;
+  const int32_t nch = ord_nch[r];
+  if (nch == 0) return;
+  const int32_t a = order[r];
+  const int64_t c0 = row_ptr[a], c1 = row_ptr[a + 1];
+  const int64_t w0 = epre[c0];
+  const int32_t slot = nch > 1 ? split_slot[a] : -1;
+  int64_t b = c0;
+  for (int32_t j = 0; j < nch; j++) {
+    const int64_t e = (j == nch - 1) ? c1 : c0 + lower_bound_i64<int64_t>(epre + c0, c1 - c0, w0 + (j + 1) * kChunkWork);
+    chunks[ord_cbase[r] + j] = Chunk{a, slot, b, e, 0};
+    b = e;
+  }
+}
+
+// Block-wide sum of a uint64 (kAccThreads threads).
+__device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t *s_red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  for (int w = 0; w < kAccWaves; w++) t += s_red[w];
+  __syncthreads();
+  return t;
+}
+
+// Column-order compaction of a dense row (LDS or global) into (col, cnt) at out_base; zeroes the
+// source.  Returns the entry count (block-uniform) and the sum of counts.
+template <class Src>
+__device__ inline uint32_t compact_row(Src *row, int32_t M, int32_t *__restrict__ col_out,
+                                       uint32_t *__restrict__ cnt_out, int64_t out_base, uint64_t *sum,
+                                       uint32_t *s_wave) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t base = 0;
+  uint64_t my_sum = 0;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t t0 = 0; t0 < M; t0 += kAccThreads) {
+    const int32_t b = t0 + tid;
+    uint32_t v = 0;
+    if (b < M) {
+      v = row[b];
+      if (v) row[b] = 0;
+    }
+    const uint64_t m = __ballot(v != 0);
+    if (lane == 0) s_wave[wave] = uint32_t(__popcll(m));
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kAccWaves; w++) {
+      const uint32_t x = s_wave[w];
+      woff += (w < wave) ? x : 0u;
+      tot += x;
+    }
+    if (v) {
+      const int64_t pos = out_base + base + woff + uint32_t(__popcll(m & lt_mask));
+      col_out[pos] = b;
+      cnt_out[pos] = v;
+      my_sum += v;
+    }
+    base += tot;
+    __syncthreads();
+  }
+  *sum = my_sum;
+  return base;
+}
+
+// ---- 7. ★ the hot kernel --------------------------------------------------------------------------
+// Persistent: one 1024-thread workgroup per CU (the M-counter LDS row needs up to 159 KiB), chunks
+// dequeued heaviest-first from a device counter.  Waves take contributions round-robin; a
+// contribution's user list is streamed with coalesced 4 B loads (64 lanes, 4 loads in flight per
+// lane) and every partner id becomes one no-return ds_add_u32 on the row's counter.
+__global__ __launch_bounds__(kAccThreads) void k_accumulate(
+    const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
+    const uint32_t *__restrict__ cvals, const int64_t *__restrict__ aoff, const int32_t *__restrict__ alen,
+    const int32_t *__restrict__ aold, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
+    int32_t M, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, int32_t *__restrict__ col_out,
+    uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging, int64_t *__restrict__ rowsum,
+    int64_t *__restrict__ err) {
+  extern __shared__ uint32_t acc[];
+  __shared__ int32_t s_chunk;
+  __shared__ uint32_t s_self;
+  __shared__ uint32_t s_wave[kAccWaves];
+  __shared__ uint64_t s_red[kAccWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n_chunks = tot->n_chunks;
+  for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
+  for (;;) {
+    if (tid == 0) {
+      s_chunk = atomicAdd(queue, 1);
+      s_self = 0;
+    }
+    __syncthreads();
+    const int32_t ch = s_chunk;
+    if (ch >= n_chunks) break;
+    const Chunk c = chunks[ch];
+    uint32_t selfs = 0;
+    for (int64_t k = c.begin + wave; k < c.end; k += kAccWaves) {
+      const uint32_t v = cvals[k];
+      const uint32_t j = v >> 1;
+      const int32_t *h = arena + aoff[j];
+      const int32_t n = alen[j];
+      const int32_t start = (v & 1u) ? aold[j] : 0;
+      selfs += (v & 1u) ^ 1u;
+      for (int32_t i = start + lane; i < n; i += 256) {
+        const int32_t b0 = h[i];
+        const int32_t b1 = (i + 64 < n) ? h[i + 64] : -1;
+        const int32_t b2 = (i + 128 < n) ? h[i + 128] : -1;
+        const int32_t b3 = (i + 192 < n) ? h[i + 192] : -1;
+        atomicAdd(&acc[b0], 1u);
+        if (b1 >= 0) atomicAdd(&acc[b1], 1u);
+        if (b2 >= 0) atomicAdd(&acc[b2], 1u);
+        if (b3 >= 0) atomicAdd(&acc[b3], 1u);
+      }
+    }
+    if (lane == 0 && selfs) atomicAdd(&s_self, selfs);
+    __syncthreads();
+    const uint32_t self_total = s_self;
+    const int64_t chunk_rowsum = (epre[c.end] - epre[c.begin]) - int64_t(self_total);
+    if (tid == 0) {
+      acc[c.row] -= self_total;  // the -1 at x_p for every new position (p != q)
+      atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
+    }
+    __syncthreads();
+    if (c.split < 0) {
+      uint64_t sum;
+      const uint32_t nnz = compact_row(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
+      const uint64_t total = block_sum_u64(sum, s_red);
+      if (tid == 0) {
+        row_nnz[c.row] = int32_t(nnz);
+        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+      }
+    } else {
+      uint32_t *srow = staging + int64_t(c.split) * M;
+      for (int32_t b = tid; b < M; b += kAccThreads) {
+        const uint32_t v = acc[b];
+        if (v) {
+          atomicAdd(srow + b, v);
+          acc[b] = 0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- 8. split rows: compact the staging rows ------------------------------------------------------
+__global__ __launch_bounds__(kAccThreads) void k_finalize_split(
+    const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M,
+    uint32_t *__restrict__ staging, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, const int64_t *__restrict__ rowsum,
+    int64_t *__restrict__ err) {
+  __shared__ uint32_t s_wave[kAccWaves];
+  __shared__ uint64_t s_red[kAccWaves];
+  const int64_t n_split = tot->n_split;
+  for (int64_t s = blockIdx.x; s < n_split; s += gridDim.x) {
+    const int32_t a = split_row[s];
+    uint64_t sum;
+    const uint32_t nnz = compact_row(staging + s * M, M, col_out, cnt_out, row_base[a], &sum, s_wave);
+    const uint64_t total = block_sum_u64(sum, s_red);
+    if (threadIdx.x == 0) {
+      row_nnz[a] = int32_t(nnz);
+      if (total != uint64_t(rowsum[a])) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+    }
+  }
+}
+
+__global__ void k_nnz_total(const int32_t *__restrict__ row_nnz, int32_t M, PlanTotals *__restrict__ tot) {
+  __shared__ int64_t s[256];
+  int64_t v = 0;
+  for (int32_t a = threadIdx.x; a < M; a += 256) v += row_nnz[a];
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot->nnz_total = s[0];
+}
+
+// Pack: padded CSR -> contiguous CSR (one wave per row).
+__global__ void k_pack(const int64_t *__restrict__ row_base, const int64_t *__restrict__ pk_row_ptr,
+                       const int32_t *__restrict__ col, const uint32_t *__restrict__ cnt, int32_t M,
+                       int32_t *__restrict__ pk_col, uint32_t *__restrict__ pk_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = wave; a < M; a += n_waves) {
+    const int64_t src = row_base[a], dst = pk_row_ptr[a], n = pk_row_ptr[a + 1] - dst;
+    for (int64_t i = lane; i < n; i += 64) {
+      pk_col[dst + i] = col[src + i];
+      pk_cnt[dst + i] = cnt[src + i];
+    }
+  }
+}
+
+__global__ void k_iota_users(int64_t n, const int64_t *__restrict__ user_ptr, int64_t *__restrict__ off,
+                             int32_t *__restrict__ len, int32_t *__restrict__ old) {
+  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) {
+    off[j] = user_ptr[j];
+    len[j] = int32_t(user_ptr[j + 1] - user_ptr[j]);
+    old[j] = 0;
+  }
+}
+
+inline unsigned blocks_for(int64_t n, int t) { return unsigned((n + t - 1) / t); }
+
+int key_bits(int32_t M) {
+  int b = 1;
+  while ((int64_t(1) << b) < M) b++;
+  return b;
+}
+
+}  // namespace
+
+Status DevBuf::reserve(size_t bytes) {
+  if (bytes <= cap) return Status::Ok();
+  release();
+  size_t want = bytes + bytes / 4 + 256;
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    p = nullptr;
+    cap = 0;
+    return Status{4, "hipMalloc(" + std::to_string(want) + " B) failed: " + hipGetErrorString(e)};
+  }
+  cap = want;
+  return Status::Ok();
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+}
+
+Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr, int64_t *off, int32_t *len,
+                         int32_t *old) {
+  if (n_users > 0) k_iota_users<<<blocks_for(n_users, 256), 256, 0, s>>>(n_users, user_ptr, off, len, old);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status Counter::init(int32_t n_items) {
+  if (n_items <= 0) return Status{1, "n_items must be positive"};
+  if (n_items > kMaxLdsCounters)
+    return Status{1, "n_items " + std::to_string(n_items) + " exceeds the single-tile LDS row (" +
+                         std::to_string(kMaxLdsCounters) + " items); column tiling is not built yet"};
+  M_ = n_items;
+  COOC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_tot_), sizeof(PlanTotals), hipHostMallocDefault));
+  const size_t lds = size_t(M_) * 4;
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  return Status::Ok();
+}
+
+void Counter::release() {
+  DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
+                   &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
+                   &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
+                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_};
+  for (DevBuf *b : all) b->release();
+  if (h_tot_) (void)hipHostFree(h_tot_);
+  h_tot_ = nullptr;
+}
+
+Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
+  const int32_t M = M_;
+  const int64_t n = au.n_contrib;
+  if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
+  // ---- workspace
+  COOC_TRY(keys_in_.reserve(sizeof(uint32_t) * (n + 1)));
+  COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n + 1)));
+  COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n + 1)));
+  COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n + 1)));
+  COOC_TRY(epre_.reserve(sizeof(int64_t) * (n + 1)));
+  COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(order_.reserve(sizeof(int32_t) * M * 2));
+  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(row_cap_.reserve(sizeof(int64_t) * M));
+  COOC_TRY(row_split_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (M + 1)));
+  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * (M + 1)));
+  COOC_TRY(split_row_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
+  COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
+  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
+
+  uint32_t *keys_in = keys_in_.as<uint32_t>(), *vals_in = vals_in_.as<uint32_t>();
+  uint32_t *keys = keys_out_.as<uint32_t>(), *vals = vals_out_.as<uint32_t>();
+  int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
+  PlanTotals *tot = tot_.as<PlanTotals>();
+
+  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
+  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * M, s));
+  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * M, s));
+  COOC_HIP_TRY(hipMemsetAsync(epre, 0, sizeof(int64_t), s));
+
+  // 1. contributions
+  if (au.n_active > 0) {
+    const int64_t waves = au.n_active < 65536 ? au.n_active : 65536;
+    k_build_contribs<<<blocks_for(waves * 64, 256), 256, 0, s>>>(au.n_active, au.off, au.len, au.old, au.cbase,
+                                                                  au.arena, M, keys_in, vals_in,
+                                                                  reinterpret_cast<int64_t *>(&tot->err));
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152)
+  size_t tmp_bytes = 0;
+  const int nb = key_bits(M);
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
+  size_t scan_bytes = 0;
+  hipcub::TransformInputIterator<int64_t, WorkOp, const uint32_t *> work_it(vals, WorkOp{au.len, au.old});
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, work_it, epre + 1, int(n), s));
+  tmp_bytes = std::max(tmp_bytes, scan_bytes);
+  size_t sort2_bytes = 0;
+  uint64_t *okeys = order_keys_.as<uint64_t>();
+  int32_t *order = order_.as<int32_t>();
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort2_bytes, row_work_.as<uint64_t>(), okeys,
+                                                            order + M, order, M, 0, 64, s));
+  tmp_bytes = std::max(tmp_bytes, sort2_bytes);
+  size_t scan2_bytes = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan2_bytes, row_cap_.as<int64_t>(),
+                                                row_base_.as<int64_t>() + 1, M, s));
+  tmp_bytes = std::max(tmp_bytes, scan2_bytes);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan2_bytes, row_nch_.as<int32_t>(),
+                                                ord_cbase_.as<int32_t>() + 1, M, s));
+  tmp_bytes = std::max(tmp_bytes, scan2_bytes);
+  COOC_TRY(sort_tmp_.reserve(tmp_bytes));
+
+  if (n > 0) {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
+    // 4. pair work prefix
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, work_it, epre + 1, int(n), s));
+  }
+  // 3. row pointer
+  k_row_ptr<<<blocks_for(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
+  // 5. per-row plan
+  k_plan_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_work_.as<uint64_t>(), order + M,
+                                                 row_nch_.as<int32_t>(), row_cap_.as<int64_t>(),
+                                                 row_split_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint64_t>(), okeys,
+                                                              order + M, order, M, 0, 64, s));
+  }
+  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
+  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(),
+                                                  ord_cbase_.as<int32_t>() + 1, M, s));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_cap_.as<int64_t>(),
+                                                  row_base_.as<int64_t>() + 1, M, s));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
+                                                  split_slot_.as<int32_t>() + 1, M, s));
+  }
+  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
+                                                  split_row_.as<int32_t>());
+  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), row_base_.as<int64_t>(), split_slot_.as<int32_t>(), epre, M, n,
+                           tot, queue_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+
+  // ---- output + chunk buffers sized by the plan
+  const int64_t n_chunks = h_tot_->n_chunks, cap = h_tot_->cap_total, n_split = h_tot_->n_split;
+  COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
+  COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
+  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
+  if (n_split > 0) {
+    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
+    COOC_TRY(staging_.reserve(need));
+    COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
+  }
+  k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
+                                                   epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
+  COOC_HIP_TRY(hipGetLastError());
+
+  // 7. ★ accumulate
+  int dev = 0, n_cu = 256;
+  COOC_HIP_TRY(hipGetDevice(&dev));
+  COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t grid = std::min<int64_t>(n_chunks, n_cu);
+  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+  if (grid > 0) {
+    k_accumulate<<<unsigned(grid), kAccThreads, size_t(M) * 4, s>>>(
+        chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), vals, au.off, au.len, au.old, au.arena, epre, M,
+        row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
+        staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+  // 8. split rows
+  if (n_split > 0) {
+    const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu));
+    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), M, staging_.as<uint32_t>(),
+                                                          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
+                                                          col_.as<int32_t>(), cnt_.as<uint32_t>(),
+                                                          rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  k_nnz_total<<<1, 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
+  COOC_HIP_TRY(hipGetLastError());
+
+  out->row_base = row_base_.as<int64_t>();
+  out->row_nnz = row_nnz_.as<int32_t>();
+  out->col = col_.as<int32_t>();
+  out->cnt = cnt_.as<uint32_t>();
+  out->rowsum = rowsum_.as<int64_t>();
+  out->work = h_tot_->work_total;
+  out->observed = h_tot_->work_total - au.n_new;
+  out->nnz = -1;  // known after the stream drains: Counter::totals().nnz_total
+  return Status::Ok();
+}
+
+Status Counter::read_totals(PlanTotals *t) {
+  COOC_HIP_TRY(hipMemcpy(t, tot_.p, sizeof(PlanTotals), hipMemcpyDeviceToHost));
+  return Status::Ok();
+}
+
+Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t **cnt) {
+  const int32_t M = M_;
+  COOC_TRY(pk_row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot_.p, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  const int64_t nnz = h_tot_->nnz_total;
+  COOC_TRY(pk_col_.reserve(sizeof(int32_t) * (nnz + 1)));
+  COOC_TRY(pk_cnt_.reserve(sizeof(uint32_t) * (nnz + 1)));
+  size_t b = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, row_nnz_.as<int32_t>(), pk_row_ptr_.as<int64_t>() + 1, M, s));
+  COOC_TRY(sort_tmp_.reserve(b));
+  b = sort_tmp_.cap;
+  COOC_HIP_TRY(hipMemsetAsync(pk_row_ptr_.p, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_nnz_.as<int32_t>(), pk_row_ptr_.as<int64_t>() + 1,
+                                                M, s));
+  k_pack<<<blocks_for(int64_t(M) * 64, 256) < 8192 ? blocks_for(int64_t(M) * 64, 256) : 8192, 256, 0, s>>>(
+      row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(), M,
+      pk_col_.as<int32_t>(), pk_cnt_.as<uint32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  *row_ptr = pk_row_ptr_.as<int64_t>();
+  *col = pk_col_.as<int32_t>();
+  *cnt = pk_cnt_.as<uint32_t>();
+  return Status::Ok();
+}
+
+}  // namespace cooc

@@ -1,0 +1,148 @@
+// cooc_ctx.cpp — context lifecycle and the stateless one-window batch entry points.
+#include "cooc_ctx.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+using cooc::Status;
+
+std::string &cooc_ctx::create_error() {
+  static thread_local std::string e;
+  return e;
+}
+
+Status cooc_ctx::init(const cooc_config &c) {
+  cfg = c;
+  if (c.n_items <= 0) return Status{COOC_ERR_ARG, "n_items must be > 0"};
+  if (c.topk < 0 || c.topk > 32767)  // topK is a Java short (Configuration.java:153, ItemRowRescorer...java:31)
+    return Status{COOC_ERR_ARG, std::to_string(c.topk) + " is not a valid topK"};
+  if (c.window_size_ms <= 0) return Status{COOC_ERR_ARG, "window size must be > 0"};
+  int n_dev = 0;
+  hipError_t e = hipGetDeviceCount(&n_dev);
+  if (e != hipSuccess || n_dev == 0) {
+    (void)hipGetLastError();
+    return Status{COOC_ERR_HIP, "no HIP device available (the co-occurrence core has no CPU fallback)"};
+  }
+  if (c.device >= n_dev) return Status{COOC_ERR_ARG, "device ordinal out of range"};
+  if (c.device >= 0) COOC_HIP_TRY(hipSetDevice(c.device));
+  COOC_HIP_TRY(hipGetDevice(&device));
+  COOC_HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  COOC_HIP_TRY(hipEventCreate(&timer.acc_begin));
+  COOC_HIP_TRY(hipEventCreate(&timer.acc_end));
+  return counter.init(c.n_items);
+}
+
+cooc_ctx::~cooc_ctx() {
+  (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  stream_state.release();
+  counter.release();
+  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old};
+  for (auto *b : bufs) b->release();
+  if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
+  if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                              int64_t n_interactions, hipStream_t s, cooc_device_result *out) {
+  COOC_HIP_TRY(hipSetDevice(device));
+  have_batch = false;
+  const int64_t n_act = std::max<int64_t>(n_users, 1);
+  COOC_TRY(b_off.reserve(sizeof(int64_t) * n_act));
+  COOC_TRY(b_len.reserve(sizeof(int32_t) * n_act));
+  COOC_TRY(b_old.reserve(sizeof(int32_t) * n_act));
+  COOC_TRY(cooc::launch_iota_users(s, n_users, d_user_ptr, b_off.as<int64_t>(), b_len.as<int32_t>(),
+                                   b_old.as<int32_t>()));
+  cooc::ActiveUsers au;
+  au.n_active = n_users;
+  au.off = b_off.as<int64_t>();
+  au.len = b_len.as<int32_t>();
+  au.old = b_old.as<int32_t>();
+  au.cbase = d_user_ptr;  // contributions are the interactions themselves (user_ptr[0] == 0)
+  au.n_contrib = n_interactions;
+  au.n_new = n_interactions;
+  au.arena = d_items;
+  cooc::CountResult r;
+  COOC_TRY(counter.run(au, s, &r, timer.enabled ? &timer : nullptr));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  // totals (nnz, overflow flag) are written by the last kernels of the run
+  int64_t nnz = 0, err = 0;
+  {
+    cooc::PlanTotals h;
+    COOC_TRY(counter.read_totals(&h));
+    nnz = h.nnz_total;
+    err = h.err;
+  }
+  if (err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  out->n_items = cfg.n_items;
+  out->nnz = nnz;
+  out->observed = r.observed;
+  out->row_base = r.row_base;
+  out->row_nnz = r.row_nnz;
+  out->col = r.col;
+  out->cnt = r.cnt;
+  out->rowsum = r.rowsum;
+  have_batch = true;
+  batch_observed = r.observed;
+  batch_nnz = nnz;
+  batch_stream = s;
+  return Status::Ok();
+}
+
+Status cooc_ctx::count_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_window_info *info) {
+  COOC_HIP_TRY(hipSetDevice(device));
+  if (user_ptr && n_users > 0 && user_ptr[0] != 0) return Status{COOC_ERR_ARG, "user_ptr[0] must be 0"};
+  for (int64_t u = 0; u < n_users; u++)
+    if (user_ptr[u + 1] < user_ptr[u]) return Status{COOC_ERR_ARG, "user_ptr must be non-decreasing"};
+  const int64_t n = n_users > 0 ? user_ptr[n_users] : 0;
+  if (n > 0 && !items) return Status{COOC_ERR_ARG, "items is NULL"};
+  COOC_TRY(b_user_ptr.reserve(sizeof(int64_t) * (n_users + 1)));
+  COOC_TRY(b_items.reserve(sizeof(int32_t) * (n + 1)));
+  if (n_users > 0)
+    COOC_HIP_TRY(hipMemcpyAsync(b_user_ptr.p, user_ptr, sizeof(int64_t) * (n_users + 1), hipMemcpyHostToDevice, stream));
+  if (n > 0) COOC_HIP_TRY(hipMemcpyAsync(b_items.p, items, sizeof(int32_t) * n, hipMemcpyHostToDevice, stream));
+  cooc_device_result r;
+  COOC_TRY(count_device(n_users, b_user_ptr.as<int64_t>(), b_items.as<int32_t>(), n, stream, &r));
+  std::vector<int32_t> nnz_rows(cfg.n_items);
+  COOC_HIP_TRY(hipMemcpy(nnz_rows.data(), r.row_nnz, sizeof(int32_t) * cfg.n_items, hipMemcpyDeviceToHost));
+  std::memset(info, 0, sizeof(*info));
+  info->nnz = r.nnz;
+  info->observed = r.observed;
+  info->n_rows = int32_t(std::count_if(nnz_rows.begin(), nnz_rows.end(), [](int32_t x) { return x > 0; }));
+  return Status::Ok();
+}
+
+Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
+                            int32_t *rowsum32) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  const int32_t M = cfg.n_items;
+  int64_t *d_rp;
+  int32_t *d_col;
+  uint32_t *d_cnt;
+  COOC_TRY(counter.pack(batch_stream, &d_rp, &d_col, &d_cnt));
+  COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  if (row_ptr) COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
+  if (cols && batch_nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
+  if ((cnt || cnt16) && batch_nnz) {
+    std::vector<uint32_t> tmp;
+    uint32_t *dst = cnt;
+    if (!dst) {
+      tmp.resize(batch_nnz);
+      dst = tmp.data();
+    }
+    COOC_HIP_TRY(hipMemcpy(dst, d_cnt, sizeof(uint32_t) * batch_nnz, hipMemcpyDeviceToHost));
+    if (cnt16)  // Int2ShortOpenHashMap value: the count modulo 2^16 as a signed short
+      for (int64_t i = 0; i < batch_nnz; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
+  }
+  if (rowsum || rowsum32) {
+    std::vector<int64_t> tmp(M);
+    COOC_HIP_TRY(hipMemcpy(tmp.data(), counter.last_rowsum(), sizeof(int64_t) * M, hipMemcpyDeviceToHost));
+    if (rowsum) std::memcpy(rowsum, tmp.data(), sizeof(int64_t) * M);
+    if (rowsum32)  // Java int accumulation (RowSumAggregator.java:25-27, Int2IntOpenHashMap.addTo)
+      for (int32_t a = 0; a < M; a++) rowsum32[a] = int32_t(uint32_t(uint64_t(tmp[a])));
+  }
+  return Status::Ok();
+}

@@ -1,0 +1,115 @@
+// cooc_ctx.h — the context behind the C-ABI handle: one per Flink subtask.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cooc.h"
+#include "cooc_device.h"
+
+struct cooc_ctx;
+
+namespace cooc {
+
+// Resident streaming state: per-user histories (device arena), global rows (dense uint32
+// [n_items x n_items] in HBM), global row sums, the rescorer's observed total, and the outputs of
+// the last finished window.  Restates NonSampled...java:129-161 (history), ItemRowRescorer...java:
+// 33-41,144-241 (global state, merge, rescoring).
+class StreamState {
+ public:
+  Status submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int32_t *user_ids, const int64_t *user_ptr,
+                const int32_t *items);
+  Status finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info);
+  Status copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+  Status copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32);
+  Status copy_topk(cooc_ctx &ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores);
+  Status global_rowsums(cooc_ctx &ctx, int64_t *exact, int32_t *v32);
+  Status global_row_nnz(cooc_ctx &ctx, int32_t item, int64_t *nnz);
+  Status global_row(cooc_ctx &ctx, int32_t item, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+  void release();
+
+  int64_t observed_exact = 0;  // UserInteractionCounterObservedCooccurrences (NonSampled...java:80,153)
+  int64_t observed_ref = 0;    // ItemRowRescorer observedCooccurrences: long += int delta (:37,154)
+  int64_t rowsum_acc = 0;      // RowSumProcessWindowRowSum (RowSumAggregator.java:50,67)
+  int64_t rescored_items = 0;  // ItemRowRescorerRescoredItems (ItemRowRescorer...java:60,169)
+
+ private:
+  Status ensure_global(cooc_ctx &ctx);
+  Status grow_arena(cooc_ctx &ctx, int64_t need);
+
+  // host metadata of the per-user histories
+  std::unordered_map<int32_t, int32_t> slot_of_;
+  std::vector<int64_t> h_off_;
+  std::vector<int32_t> h_len_, h_cap_;
+  int64_t arena_used_ = 0;
+  DevBuf arena_;
+  // staged window
+  bool staged_ = false;
+  int64_t staged_ts_ = 0;
+  std::unordered_map<int32_t, int32_t> staged_idx_;  // slot -> index into staged_items_
+  std::vector<int32_t> staged_slots_;
+  std::vector<std::vector<int32_t>> staged_items_;
+  // device uploads of one window
+  DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
+  // global state
+  bool global_ready_ = false;
+  DevBuf d_global_, d_grs_, d_touched_, d_scan_tmp_, d_scal_, d_topk_val_, d_topk_score_, d_topk_size_;
+  // last window
+  bool have_window_ = false;
+  cooc_window_info last_{};
+  int32_t n_touched_ = 0;
+};
+
+// NonSampledUserInteractionCounterOneInputStreamOperator mirror: late-element drop, tumbling
+// window assignment, per-window buffering in arrival order, watermark-driven firing
+// (NonSampled...java:84-165).
+class Operator {
+ public:
+  Status process_elements(cooc_ctx &ctx, int64_t n, const int32_t *users, const int32_t *items, const int64_t *ts,
+                          int64_t *n_late);
+  Status process_watermark(cooc_ctx &ctx, int64_t watermark, int32_t *fired, cooc_window_info *info);
+
+  int64_t watermark = INT64_MIN;  // timerService.currentWatermark()
+  int64_t late_elements = 0;      // UserInteractionCounterLateElements
+
+ private:
+  struct Pending {
+    std::vector<int32_t> users, items;
+  };
+  std::map<int64_t, Pending> pending_;  // window.maxTimestamp() -> buffered interactions
+};
+
+}  // namespace cooc
+
+struct cooc_ctx {
+  cooc::Status init(const cooc_config &cfg);
+  ~cooc_ctx();
+
+  cooc::Status count_device(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
+                            hipStream_t s, cooc_device_result *out);
+  cooc::Status count_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_window_info *info);
+  cooc::Status copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
+                          int32_t *rowsum32);
+
+  static std::string &create_error();
+
+  cooc_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  cooc::Counter counter;
+  cooc::KernelTimer timer;
+  cooc::StreamState stream_state;
+  cooc::Operator op;
+
+  // stateless batch buffers
+  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old;
+  bool have_batch = false;
+  int64_t batch_observed = 0;
+  int64_t batch_nnz = 0;
+  hipStream_t batch_stream = nullptr;
+};

@@ -1,0 +1,139 @@
+// cooc_device.h — internal C++ interface between the C-ABI (cooc_capi.cpp) and the HIP kernels.
+//
+// The device pipeline reduces "contributions" into per-row dense LDS accumulators.  A
+// contribution is (row a, segment of one user's history in the device arena): the reference's
+// NonSampled...java:113-165 expansion of one window is exactly
+//   for every user u expanded in the window, with resident history length `old` and `len` items
+//   after appending the window's items (old + new, arrival order):
+//     position p >= old (a NEW interaction x_p):  row x_p += the whole list  [0, len), then -1 at x_p
+//     position p <  old (an OLD interaction x_p): row x_p += the new part     [old, len)
+// which covers every ordered position pair (p != q) whose later position is new — the pairs the
+// reference emits in that window (ITEM records (x, h, +1) and (o, x, +1), :138-151).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace cooc {
+
+struct Status {
+  int code = 0;  // cooc_status
+  std::string msg;
+  bool ok() const { return code == 0; }
+  static Status Ok() { return {}; }
+};
+
+#define COOC_HIP_TRY(expr)                                                                      \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return ::cooc::Status{3, std::string(#expr) + ": " + hipGetErrorString(e_)};              \
+  } while (0)
+
+#define COOC_TRY(expr)            \
+  do {                            \
+    ::cooc::Status s_ = (expr);   \
+    if (!s_.ok()) return s_;      \
+  } while (0)
+
+// Grow-only device buffer (the workspace of one context).  Never shrinks, so steady-state
+// windows perform no hipMalloc.
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  Status reserve(size_t bytes);
+  void release();
+  template <class T>
+  T *as() const { return static_cast<T *>(p); }
+};
+
+// The users expanded in one window, all device pointers.
+struct ActiveUsers {
+  int64_t n_active = 0;
+  const int64_t *off = nullptr;    // [n_active] arena offset of the user's history
+  const int32_t *len = nullptr;    // [n_active] history length after the window (old + new)
+  const int32_t *old = nullptr;    // [n_active] history length before the window
+  const int64_t *cbase = nullptr;  // [n_active + 1] exclusive prefix of len (contribution slots)
+  int64_t n_contrib = 0;           // == cbase[n_active] (host copy)
+  int64_t n_new = 0;               // interactions of the window == sum(len - old) (host copy)
+  const int32_t *arena = nullptr;  // item ids of all histories
+};
+
+// One row's share of the work (heavy rows are split over several chunks).
+struct Chunk {
+  int32_t row;
+  int32_t split;  // staging slot of a split row, -1 when the row is one chunk
+  int64_t begin;  // contribution range [begin, end) in row-sorted order
+  int64_t end;
+  int64_t pad;
+};
+
+// Scalars of one run (device-side, copied to a pinned host mirror once per run).
+struct PlanTotals {
+  int64_t n_chunks;
+  int64_t cap_total;  // padded output entries
+  int64_t n_split;
+  int64_t work_total; // sum over contributions of segment length (ordered pairs + self terms)
+  int64_t nnz_total;  // filled after the run
+  int64_t err;        // bit 0: item id out of range, bit 1: uint32 count overflow
+  int64_t pad[2];
+};
+
+// Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
+struct CountResult {
+  int64_t *row_base = nullptr;
+  int32_t *row_nnz = nullptr;
+  int32_t *col = nullptr;
+  uint32_t *cnt = nullptr;
+  int64_t *rowsum = nullptr;
+  int64_t nnz = 0;
+  int64_t observed = 0;  // ordered pairs of the run
+  int64_t work = 0;
+};
+
+// Kernel timing hooks for the benchmark (HIP events recorded on the run's stream).
+struct KernelTimer {
+  hipEvent_t acc_begin = nullptr, acc_end = nullptr;
+  bool enabled = false;
+};
+
+class Counter {
+ public:
+  Status init(int32_t n_items);
+  void release();
+  ~Counter() { release(); }
+
+  // Expand + reduce the given contributions; returns the padded CSR.  Synchronises `stream`
+  // once (to size the output).
+  Status run(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
+
+  // Pack the padded CSR of the last run into contiguous CSR (device), for copy-out.
+  Status pack(hipStream_t stream, int64_t **row_ptr, int32_t **col, uint32_t **cnt);
+
+  // Copy the device totals of the last run (the stream must have drained).
+  Status read_totals(PlanTotals *t);
+  const int64_t *last_rowsum() const { return rowsum_.as<int64_t>(); }
+  const int32_t *last_row_nnz() const { return row_nnz_.as<int32_t>(); }
+  const int64_t *last_row_base() const { return row_base_.as<int64_t>(); }
+  const int32_t *last_col() const { return col_.as<int32_t>(); }
+  const uint32_t *last_cnt() const { return cnt_.as<uint32_t>(); }
+  int32_t n_items() const { return M_; }
+
+ private:
+  int32_t M_ = 0;
+  // workspace
+  DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
+  DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
+  DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
+  DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_;
+  PlanTotals *h_tot_ = nullptr;  // pinned
+};
+
+// Launch wrappers for the streaming state (cooc_stream.hip).
+Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr, int64_t *off, int32_t *len,
+                         int32_t *old);
+
+}  // namespace cooc

@@ -1,0 +1,409 @@
+// cooc_stream.cpp — host side of the resident streaming state and of the operator mirror.
+//
+// StreamState restates, per tumbling window, NonSampledUserInteractionCounterOneInputStreamOperator
+// .onEventTime (:113-165: expand every buffered interaction against the user's history, then
+// append it), the two window aggregators (ItemRowAggregator.java:26-56, RowSumAggregator.java:
+// 25-71) and ItemRowRescorerTwoInputStreamOperator.processWatermark (:116-241).  The expansion and
+// reductions run on the device (cooc_count.hip); this file only keeps per-user metadata, stages
+// the window's interactions and moves results.
+#include <algorithm>
+#include <cstring>
+
+#include "cooc_ctx.h"
+#include "cooc_stream_kernels.h"
+
+namespace cooc {
+
+namespace {
+
+// Flink TumblingEventTimeWindows.assignWindows with offset 0 [3P, Flink 1.3.2]:
+// start = ts - (ts - offset + size) % size (Java remainder), maxTimestamp = start + size - 1.
+int64_t window_max_ts(int64_t ts, int64_t size) {
+  const int64_t start = ts - (ts + size) % size;
+  return start + size - 1;
+}
+
+template <class T>
+Status upload(DevBuf &b, const std::vector<T> &v, hipStream_t s) {
+  COOC_TRY(b.reserve(sizeof(T) * (v.size() + 1)));
+  if (!v.empty()) COOC_HIP_TRY(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s));
+  return Status::Ok();
+}
+
+}  // namespace
+
+void StreamState::release() {
+  DevBuf *all[] = {&arena_,      &d_act_off_,      &d_act_len_,     &d_act_old_,   &d_cbase_,
+                   &d_new_items_, &d_new_dst_ptr_, &d_new_dst_,     &d_reloc_,     &d_global_,
+                   &d_grs_,       &d_touched_,     &d_scan_tmp_,    &d_scal_,      &d_topk_val_,
+                   &d_topk_score_, &d_topk_size_};
+  for (DevBuf *b : all) b->release();
+  global_ready_ = false;
+}
+
+Status StreamState::submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int32_t *user_ids,
+                           const int64_t *user_ptr, const int32_t *items) {
+  if (staged_ && ts != staged_ts_)
+    return Status{COOC_ERR_STATE, "window " + std::to_string(staged_ts_) + " is staged; finish it before submitting " +
+                                      std::to_string(ts)};
+  const int32_t M = ctx.cfg.n_items;
+  for (int32_t u = 0; u < n_users; u++) {
+    if (user_ptr[u + 1] < user_ptr[u]) return Status{COOC_ERR_ARG, "user_ptr must be non-decreasing"};
+    for (int64_t i = user_ptr[u]; i < user_ptr[u + 1]; i++)
+      if (items[i] < 0 || items[i] >= M)
+        return Status{COOC_ERR_ARG, "item id " + std::to_string(items[i]) + " outside [0, n_items)"};
+  }
+  for (int32_t u = 0; u < n_users; u++) {
+    const int32_t uid = user_ids[u];
+    auto it = slot_of_.find(uid);
+    int32_t slot;
+    if (it == slot_of_.end()) {  // userHistoryState.value() == null -> new IntArrayList(), :130-132
+      slot = int32_t(h_off_.size());
+      slot_of_.emplace(uid, slot);
+      h_off_.push_back(0);
+      h_len_.push_back(0);
+      h_cap_.push_back(0);
+    } else {
+      slot = it->second;
+    }
+    auto st = staged_idx_.find(slot);
+    int32_t j;
+    if (st == staged_idx_.end()) {
+      j = int32_t(staged_slots_.size());
+      staged_idx_.emplace(slot, j);
+      staged_slots_.push_back(slot);
+      staged_items_.emplace_back();
+    } else {
+      j = st->second;
+    }
+    auto &dst = staged_items_[j];
+    dst.insert(dst.end(), items + user_ptr[u], items + user_ptr[u + 1]);
+  }
+  staged_ = true;
+  staged_ts_ = ts;
+  return Status::Ok();
+}
+
+Status StreamState::grow_arena(cooc_ctx &ctx, int64_t need) {
+  if (int64_t(arena_.cap / sizeof(int32_t)) >= need) return Status::Ok();
+  DevBuf bigger;
+  COOC_TRY(bigger.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(need, 2 * int64_t(arena_.cap / 4)))));
+  if (arena_.p && arena_used_ > 0) {
+    // arena_used_ already includes the new reservations; copy the whole old capacity
+    COOC_HIP_TRY(hipMemcpyAsync(bigger.p, arena_.p, arena_.cap, hipMemcpyDeviceToDevice, ctx.stream));
+    COOC_HIP_TRY(hipStreamSynchronize(ctx.stream));
+  }
+  arena_.release();
+  arena_ = bigger;
+  bigger.p = nullptr;
+  bigger.cap = 0;
+  return Status::Ok();
+}
+
+Status StreamState::ensure_global(cooc_ctx &ctx) {
+  if (global_ready_) return Status::Ok();
+  const int64_t M = ctx.cfg.n_items;
+  const size_t g_bytes = sizeof(uint32_t) * size_t(M) * size_t(M);
+  size_t free_b = 0, total_b = 0;
+  COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  if (g_bytes > free_b / 10 * 8)
+    return Status{COOC_ERR_OOM, "dense global rows need " + std::to_string(g_bytes) +
+                                    " B of HBM (n_items^2 x 4); sparse global rows are not built yet"};
+  COOC_TRY(d_global_.reserve(g_bytes));
+  COOC_TRY(d_grs_.reserve(sizeof(int64_t) * M));
+  COOC_TRY(d_scal_.reserve(sizeof(int64_t) * 8));
+  COOC_HIP_TRY(hipMemsetAsync(d_global_.p, 0, g_bytes, ctx.stream));
+  COOC_HIP_TRY(hipMemsetAsync(d_grs_.p, 0, sizeof(int64_t) * M, ctx.stream));
+  COOC_HIP_TRY(hipMemsetAsync(d_scal_.p, 0, sizeof(int64_t) * 8, ctx.stream));
+  global_ready_ = true;
+  return Status::Ok();
+}
+
+Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  if (staged_ && ts != staged_ts_)
+    return Status{COOC_ERR_STATE, "finish_window(" + std::to_string(ts) + ") but window " +
+                                      std::to_string(staged_ts_) + " is staged"};
+  hipStream_t s = ctx.stream;
+  const int32_t M = ctx.cfg.n_items;
+  const int64_t n_act = int64_t(staged_slots_.size());
+
+  // ---- host plan: history capacity (relocation on growth), append destinations, contributions
+  std::vector<int64_t> act_off(n_act), cbase(n_act + 1, 0), new_ptr(n_act + 1, 0), new_dst(n_act), reloc;
+  std::vector<int32_t> act_len(n_act), act_old(n_act), new_items;
+  int64_t observed_window = 0;
+  for (int64_t j = 0; j < n_act; j++) {
+    const int32_t slot = staged_slots_[j];
+    const int64_t old = h_len_[slot], w = int64_t(staged_items_[j].size());
+    const int64_t need = old + w;
+    if (need > int64_t(INT32_MAX)) return Status{COOC_ERR_ARG, "user history longer than 2^31"};
+    if (need > h_cap_[slot]) {
+      const int64_t cap = std::max<int64_t>(16, std::max<int64_t>(2 * int64_t(h_cap_[slot]), need));
+      const int64_t off = arena_used_;
+      arena_used_ += cap;
+      if (old > 0) {
+        reloc.push_back(h_off_[slot]);
+        reloc.push_back(off);
+        reloc.push_back(old);
+      }
+      h_off_[slot] = off;
+      h_cap_[slot] = int32_t(std::min<int64_t>(cap, INT32_MAX));
+    }
+    act_off[j] = h_off_[slot];
+    act_len[j] = int32_t(need);
+    act_old[j] = int32_t(old);
+    cbase[j + 1] = cbase[j] + need;
+    new_dst[j] = h_off_[slot] + old;
+    new_ptr[j + 1] = new_ptr[j] + w;
+    new_items.insert(new_items.end(), staged_items_[j].begin(), staged_items_[j].end());
+    observed_window += need * (need - 1) - old * (old - 1);  // sum over new positions of 2*|history|
+    h_len_[slot] = int32_t(need);
+  }
+  COOC_TRY(grow_arena(ctx, std::max<int64_t>(arena_used_, 1024)));
+  COOC_TRY(upload(d_reloc_, reloc, s));
+  COOC_TRY(upload(d_new_items_, new_items, s));
+  COOC_TRY(upload(d_new_dst_ptr_, new_ptr, s));
+  COOC_TRY(upload(d_new_dst_, new_dst, s));
+  COOC_TRY(upload(d_act_off_, act_off, s));
+  COOC_TRY(upload(d_act_len_, act_len, s));
+  COOC_TRY(upload(d_act_old_, act_old, s));
+  COOC_TRY(upload(d_cbase_, cbase, s));
+  COOC_TRY(launch_relocate(s, int64_t(reloc.size() / 3), d_reloc_.as<int64_t>(), arena_.as<int32_t>()));
+  COOC_TRY(launch_append(s, n_act, d_new_dst_ptr_.as<int64_t>(), d_new_dst_.as<int64_t>(),
+                         d_new_items_.as<int32_t>(), arena_.as<int32_t>()));
+
+  // ---- expansion + keyed reduce of the window (the hot path)
+  ActiveUsers au;
+  au.n_active = n_act;
+  au.off = d_act_off_.as<int64_t>();
+  au.len = d_act_len_.as<int32_t>();
+  au.old = d_act_old_.as<int32_t>();
+  au.cbase = d_cbase_.as<int64_t>();
+  au.n_contrib = cbase[n_act];
+  au.n_new = new_ptr[n_act];
+  au.arena = arena_.as<int32_t>();
+  CountResult r;
+  COOC_TRY(ctx.counter.run(au, s, &r));
+
+  // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
+  COOC_TRY(ensure_global(ctx));
+  int64_t *scal = d_scal_.as<int64_t>();
+  COOC_TRY(launch_merge_global(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, d_global_.as<uint32_t>(),
+                               d_grs_.as<int64_t>(), scal, observed_window));
+  COOC_TRY(d_touched_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(launch_touched(s, M, r.row_nnz, d_touched_.as<int32_t>(), scal, d_scan_tmp_));
+  const int32_t topk = ctx.cfg.topk;
+  if (topk > 0) {
+    COOC_TRY(d_topk_size_.reserve(sizeof(int32_t) * M));
+    COOC_TRY(d_topk_val_.reserve(sizeof(int32_t) * size_t(M) * topk));
+    COOC_TRY(d_topk_score_.reserve(sizeof(double) * size_t(M) * topk));
+    COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
+                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_topk_size_.as<int32_t>(),
+                            d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+  }
+  int64_t h_scal[8];
+  COOC_HIP_TRY(hipMemcpyAsync(h_scal, scal, sizeof(h_scal), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  PlanTotals t;
+  COOC_TRY(ctx.counter.read_totals(&t));
+  if (t.err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+
+  n_touched_ = int32_t(h_scal[0]);
+  observed_exact += observed_window;
+  observed_ref = h_scal[2];
+  rowsum_acc += h_scal[1];
+  rescored_items += n_touched_;
+
+  std::memset(&last_, 0, sizeof(last_));
+  last_.ts = ts;
+  last_.nnz = t.nnz_total;
+  last_.observed = r.observed;
+  last_.n_rows = n_touched_;
+  last_.topk = topk;
+  last_.n_topk = topk > 0 ? n_touched_ : 0;
+  *info = last_;
+  have_window_ = true;
+
+  staged_ = false;
+  staged_idx_.clear();
+  staged_slots_.clear();
+  staged_items_.clear();
+  return Status::Ok();
+}
+
+Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,
+                               int16_t *cnt16) {
+  if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  const int32_t M = ctx.cfg.n_items;
+  int64_t *d_rp;
+  int32_t *d_col;
+  uint32_t *d_cnt;
+  COOC_TRY(ctx.counter.pack(ctx.stream, &d_rp, &d_col, &d_cnt));
+  COOC_HIP_TRY(hipStreamSynchronize(ctx.stream));
+  const int64_t nnz = last_.nnz;
+  if (rows || row_ptr) {
+    std::vector<int64_t> rp(M + 1);
+    COOC_HIP_TRY(hipMemcpy(rp.data(), d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
+    int32_t k = 0;
+    for (int32_t a = 0; a < M; a++) {
+      if (rp[a + 1] == rp[a]) continue;
+      if (rows) rows[k] = a;
+      if (row_ptr) row_ptr[k] = rp[a];
+      k++;
+    }
+    if (row_ptr) row_ptr[k] = rp[M];
+  }
+  if (cols && nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+  if ((cnt || cnt16) && nnz) {
+    std::vector<uint32_t> tmp;
+    uint32_t *dst = cnt;
+    if (!dst) {
+      tmp.resize(nnz);
+      dst = tmp.data();
+    }
+    COOC_HIP_TRY(hipMemcpy(dst, d_cnt, sizeof(uint32_t) * nnz, hipMemcpyDeviceToHost));
+    if (cnt16)  // ItemRowAggregator's Int2ShortOpenHashMap value (short addTo wraps)
+      for (int64_t i = 0; i < nnz; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
+  }
+  return Status::Ok();
+}
+
+Status StreamState::copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32) {
+  if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  const int32_t M = ctx.cfg.n_items;
+  std::vector<int32_t> nnz(M);
+  std::vector<int64_t> rs(M);
+  COOC_HIP_TRY(hipMemcpy(nnz.data(), ctx.counter.last_row_nnz(), sizeof(int32_t) * M, hipMemcpyDeviceToHost));
+  COOC_HIP_TRY(hipMemcpy(rs.data(), ctx.counter.last_rowsum(), sizeof(int64_t) * M, hipMemcpyDeviceToHost));
+  int32_t k = 0;
+  for (int32_t a = 0; a < M; a++) {
+    if (nnz[a] == 0) continue;
+    if (items) items[k] = a;
+    if (delta) delta[k] = rs[a];
+    if (delta32) delta32[k] = int32_t(uint32_t(uint64_t(rs[a])));  // Java int accumulation
+    k++;
+  }
+  return Status::Ok();
+}
+
+Status StreamState::copy_topk(cooc_ctx &ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores) {
+  if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
+  if (ctx.cfg.topk <= 0) return Status{COOC_ERR_STATE, "rescoring is disabled (topk == 0)"};
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  const size_t n = size_t(n_touched_), k = size_t(ctx.cfg.topk);
+  if (n == 0) return Status::Ok();
+  if (rows) COOC_HIP_TRY(hipMemcpy(rows, d_touched_.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (sizes) COOC_HIP_TRY(hipMemcpy(sizes, d_topk_size_.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (values) COOC_HIP_TRY(hipMemcpy(values, d_topk_val_.p, sizeof(int32_t) * n * k, hipMemcpyDeviceToHost));
+  if (scores) COOC_HIP_TRY(hipMemcpy(scores, d_topk_score_.p, sizeof(double) * n * k, hipMemcpyDeviceToHost));
+  return Status::Ok();
+}
+
+Status StreamState::global_rowsums(cooc_ctx &ctx, int64_t *exact, int32_t *v32) {
+  const int32_t M = ctx.cfg.n_items;
+  std::vector<int64_t> rs(M, 0);
+  if (global_ready_) {
+    COOC_HIP_TRY(hipSetDevice(ctx.device));
+    COOC_HIP_TRY(hipMemcpy(rs.data(), d_grs_.p, sizeof(int64_t) * M, hipMemcpyDeviceToHost));
+  }
+  if (exact) std::memcpy(exact, rs.data(), sizeof(int64_t) * M);
+  if (v32)  // globalItemRowSums (Int2IntOpenHashMap, int32 wrap)
+    for (int32_t a = 0; a < M; a++) v32[a] = int32_t(uint32_t(uint64_t(rs[a])));
+  return Status::Ok();
+}
+
+Status StreamState::global_row_nnz(cooc_ctx &ctx, int32_t item, int64_t *nnz) {
+  const int32_t M = ctx.cfg.n_items;
+  if (item < 0 || item >= M) return Status{COOC_ERR_ARG, "item outside [0, n_items)"};
+  *nnz = 0;
+  if (!global_ready_) return Status::Ok();
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  std::vector<uint32_t> row(M);
+  COOC_HIP_TRY(hipMemcpy(row.data(), d_global_.as<uint32_t>() + int64_t(item) * M, sizeof(uint32_t) * M,
+                         hipMemcpyDeviceToHost));
+  *nnz = std::count_if(row.begin(), row.end(), [](uint32_t v) { return v != 0; });
+  return Status::Ok();
+}
+
+Status StreamState::global_row(cooc_ctx &ctx, int32_t item, int32_t *cols, uint32_t *cnt, int16_t *cnt16) {
+  const int32_t M = ctx.cfg.n_items;
+  if (item < 0 || item >= M) return Status{COOC_ERR_ARG, "item outside [0, n_items)"};
+  if (!global_ready_) return Status::Ok();
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  std::vector<uint32_t> row(M);
+  COOC_HIP_TRY(hipMemcpy(row.data(), d_global_.as<uint32_t>() + int64_t(item) * M, sizeof(uint32_t) * M,
+                         hipMemcpyDeviceToHost));
+  int64_t k = 0;
+  for (int32_t b = 0; b < M; b++) {
+    if (!row[b]) continue;  // a key exists iff it was ever touched (all increments are +1)
+    if (cols) cols[k] = b;
+    if (cnt) cnt[k] = row[b];
+    if (cnt16) cnt16[k] = int16_t(uint16_t(row[b]));
+    k++;
+  }
+  return Status::Ok();
+}
+
+// ---- NonSampledUserInteractionCounterOneInputStreamOperator mirror -------------------------------
+Status Operator::process_elements(cooc_ctx &ctx, int64_t n, const int32_t *users, const int32_t *items,
+                                  const int64_t *ts, int64_t *n_late) {
+  const int32_t M = ctx.cfg.n_items;
+  int64_t late = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (ts[i] <= watermark) {  // :89-91
+      late++;
+      continue;
+    }
+    if (items[i] < 0 || items[i] >= M)
+      return Status{COOC_ERR_ARG, "item id " + std::to_string(items[i]) + " outside [0, n_items)"};
+    Pending &p = pending_[window_max_ts(ts[i], ctx.cfg.window_size_ms)];  // :93-100
+    p.users.push_back(users[i]);
+    p.items.push_back(items[i]);
+  }
+  late_elements += late;
+  if (n_late) *n_late = late;
+  return Status::Ok();
+}
+
+Status Operator::process_watermark(cooc_ctx &ctx, int64_t wm, int32_t *fired, cooc_window_info *info) {
+  if (wm > watermark) watermark = wm;
+  *fired = 0;
+  auto it = pending_.begin();
+  if (it == pending_.end() || it->first > watermark) return Status::Ok();
+  // onEventTime for every user of the window: group the buffered interactions by user, keeping
+  // each user's arrival order (windowState list order, :118).
+  const int64_t max_ts = it->first;
+  Pending &p = it->second;
+  std::unordered_map<int32_t, int32_t> idx;
+  std::vector<int32_t> uids;
+  std::vector<int64_t> counts;
+  std::vector<int32_t> which(p.users.size());
+  for (size_t i = 0; i < p.users.size(); i++) {
+    auto f = idx.find(p.users[i]);
+    int32_t j;
+    if (f == idx.end()) {
+      j = int32_t(uids.size());
+      idx.emplace(p.users[i], j);
+      uids.push_back(p.users[i]);
+      counts.push_back(0);
+    } else {
+      j = f->second;
+    }
+    which[i] = j;
+    counts[j]++;
+  }
+  std::vector<int64_t> ptr(uids.size() + 1, 0);
+  for (size_t j = 0; j < uids.size(); j++) ptr[j + 1] = ptr[j] + counts[j];
+  std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+  std::vector<int32_t> grouped(p.items.size());
+  for (size_t i = 0; i < p.items.size(); i++) grouped[fill[which[i]]++] = p.items[i];
+  COOC_TRY(ctx.stream_state.submit(ctx, max_ts, int32_t(uids.size()), uids.data(), ptr.data(), grouped.data()));
+  pending_.erase(it);
+  COOC_TRY(ctx.stream_state.finish(ctx, max_ts, info));
+  *fired = 1;
+  return Status::Ok();
+}
+
+}  // namespace cooc

@@ -1,0 +1,239 @@
+// cooc_stream.hip — kernels of the resident streaming state.
+//
+//   k_relocate / k_append   per-user history arena (NonSampled...java:129-161: userHistory.add)
+//   k_merge_global          global rows += window delta rows (ItemRowRescorer...java:171-177),
+//                           global row sums += row-sum deltas and the rescorer's observed total
+//                           += the int view of every delta (:144-156)
+//   k_rescore               LLR of every entry of every touched row + top-k heap
+//                           (ItemRowRescorer...java:195-241, LogLikelihood.java:41-61,
+//                           IntDoublePriorityQueue.java:132-205), rows iterated in column order
+//
+// Compiled with -ffp-contract=off: the LLR must keep Java's unfused operation order.
+#include <hipcub/hipcub.hpp>
+
+#include "cooc_stream_kernels.h"
+
+namespace cooc {
+namespace {
+
+inline unsigned blocks_for(int64_t n, int t) { return unsigned((n + t - 1) / t); }
+
+__global__ void k_relocate(int64_t n, const int64_t *__restrict__ reloc, int32_t *__restrict__ arena) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = wave; r < n; r += n_waves) {
+    const int64_t src = reloc[3 * r], dst = reloc[3 * r + 1], len = reloc[3 * r + 2];
+    for (int64_t i = lane; i < len; i += 64) arena[dst + i] = arena[src + i];
+  }
+}
+
+__global__ void k_append(int64_t n, const int64_t *__restrict__ new_ptr, const int64_t *__restrict__ new_dst,
+                         const int32_t *__restrict__ new_items, int32_t *__restrict__ arena) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = wave; j < n; j += n_waves) {
+    const int64_t s = new_ptr[j], e = new_ptr[j + 1], d = new_dst[j];
+    for (int64_t i = s + lane; i < e; i += 64) arena[d + (i - s)] = new_items[i];
+  }
+}
+
+// One wave per row with a non-empty delta.
+__global__ void k_merge_global(int32_t M, const int64_t *__restrict__ row_base, const int32_t *__restrict__ row_nnz,
+                               const int32_t *__restrict__ col, const uint32_t *__restrict__ cnt,
+                               const int64_t *__restrict__ rowsum_delta, uint32_t *__restrict__ G,
+                               int64_t *__restrict__ grs, int64_t *__restrict__ scal) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = wave; a < M; a += n_waves) {
+    const int32_t n = row_nnz[a];
+    if (n == 0) continue;
+    const int64_t b = row_base[a];
+    uint32_t *g = G + a * int64_t(M);
+    for (int32_t i = lane; i < n; i += 64) g[col[b + i]] += cnt[b + i];  // unique (a, col) per window
+    if (lane == 0) {
+      const int64_t d = rowsum_delta[a];
+      grs[a] += d;
+      // RowSumAggregator's int value of this window's update, ItemRowRescorer...java:154
+      atomicAdd(reinterpret_cast<unsigned long long *>(scal + 1),
+                (unsigned long long)int64_t(int32_t(uint32_t(uint64_t(d)))));
+    }
+  }
+}
+
+__global__ void k_finish_scalars(int64_t *__restrict__ scal, int64_t observed_window) {
+  scal[2] += scal[1];
+  scal[3] += observed_window;
+}
+
+struct IsTouched {
+  const int32_t *row_nnz;
+  __host__ __device__ bool operator()(int32_t a) const { return row_nnz[a] > 0; }
+};
+
+// ---- LogLikelihood.java:41-61 (Java operation order, no contraction) -------------------------
+__device__ inline double xlogx(int64_t x) {
+#pragma clang fp contract(off)
+  return x == 0 ? 0.0 : double(x) * log(double(x));
+}
+
+__device__ inline double llr(int64_t k11, int64_t k12, int64_t k21, int64_t k22) {
+#pragma clang fp contract(off)
+  const int64_t k11k12 = k11 + k12;
+  const int64_t k21k22 = k21 + k22;
+  const double all = xlogx(k11k12 + k21k22);
+  const double row = all - xlogx(k11k12) - xlogx(k21k22);
+  const double column = all - xlogx(k11 + k21) - xlogx(k12 + k22);
+  const double matrix = all - xlogx(k11) - xlogx(k12) - xlogx(k21) - xlogx(k22);
+  if (row + column < matrix) return 0.0;
+  return 2.0 * (row + column - matrix);
+}
+
+// ---- IntDoublePriorityQueue.java:132-205, every lane of the wave runs it on the same LDS heap ----
+__device__ inline void heap_add(int32_t *hv, double *hs, int32_t &size, int32_t value, double score) {
+  size++;
+  int32_t i = size;
+  int32_t j = i >> 1;
+  while (j > 0 && score < hs[j]) {
+    hv[i] = hv[j];
+    hs[i] = hs[j];
+    i = j;
+    j = j >> 1;
+  }
+  hv[i] = value;
+  hs[i] = score;
+}
+
+__device__ inline void heap_update(int32_t *hv, double *hs, int32_t size, int32_t value, double score) {
+  int32_t i = 1, j = 2, k = 3;
+  if (k <= size && hs[k] < hs[j]) j = k;
+  while (j <= size && hs[j] < score) {
+    hv[i] = hv[j];
+    hs[i] = hs[j];
+    i = j;
+    j = i << 1;
+    k = j + 1;
+    if (k <= size && hs[k] < hs[j]) j = k;
+  }
+  hv[i] = value;
+  hs[i] = score;
+}
+
+// One wave per touched row; the wave scores 64 consecutive columns at a time (ascending column =
+// the iteration order contract) and feeds the lanes that can enter the heap to it in lane order,
+// which is exactly the sequential loop of ItemRowRescorer...java:199-223.
+__global__ void k_rescore(const int32_t *__restrict__ touched, const int64_t *__restrict__ scal, int32_t M,
+                          const uint32_t *__restrict__ G, const int64_t *__restrict__ grs, int32_t exact,
+                          int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
+                          double *__restrict__ out_score) {
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+  double *hs = smem + int64_t(wave) * (topk + 1);
+  int32_t *hv = reinterpret_cast<int32_t *>(smem + int64_t(waves) * (topk + 1)) + int64_t(wave) * (topk + 1);
+  const int64_t n_touched = scal[0];
+  const int64_t observed = exact ? scal[3] : scal[2];
+  for (int64_t t = int64_t(blockIdx.x) * waves + wave; t < n_touched; t += int64_t(gridDim.x) * waves) {
+    const int32_t a = touched[t];
+    const int64_t rs_a = exact ? grs[a] : int64_t(int32_t(uint32_t(uint64_t(grs[a]))));
+    const uint32_t *g = G + int64_t(a) * M;
+    int32_t size = 0;
+    double least = 0.0;
+    for (int32_t c0 = 0; c0 < M; c0 += 64) {
+      const int32_t c = c0 + lane;
+      const uint32_t v = c < M ? g[c] : 0u;
+      double score = 0.0;
+      if (v != 0u) {
+        // ItemRowRescorer...java:203-205,230-240
+        const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+        const int64_t rs_b = exact ? grs[c] : int64_t(int32_t(uint32_t(uint64_t(grs[c]))));
+        const int64_t k12 = rs_a - k11;
+        const int64_t k21 = rs_b - k11;
+        const int64_t k22 = observed + k11 - k12 - k21;
+        score = llr(k11, k12, k21, k22);
+      }
+      uint64_t m = __ballot(v != 0u && (size < topk || score > least));
+      while (m) {
+        const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+        m &= m - 1;
+        const double sc = __shfl(score, l, 64);
+        if (size < topk) {
+          heap_add(hv, hs, size, c0 + l, sc);
+        } else if (sc > hs[1]) {
+          heap_update(hv, hs, size, c0 + l, sc);
+        }
+        least = hs[1];
+      }
+    }
+    out_size[t] = size;
+    for (int32_t i = lane; i < size; i += 64) {
+      out_val[t * topk + i] = hv[i + 1];
+      out_score[t * topk + i] = hs[i + 1];
+    }
+  }
+}
+
+}  // namespace
+
+Status launch_relocate(hipStream_t s, int64_t n, const int64_t *reloc, int32_t *arena) {
+  if (n > 0) k_relocate<<<std::min<unsigned>(blocks_for(n * 64, 256), 4096), 256, 0, s>>>(n, reloc, arena);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_append(hipStream_t s, int64_t n, const int64_t *new_ptr, const int64_t *new_dst, const int32_t *items,
+                     int32_t *arena) {
+  if (n > 0) k_append<<<std::min<unsigned>(blocks_for(n * 64, 256), 4096), 256, 0, s>>>(n, new_ptr, new_dst, items, arena);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
+                           const int32_t *col, const uint32_t *cnt, const int64_t *rowsum_delta, uint32_t *G,
+                           int64_t *grs, int64_t *scal, int64_t observed_window) {
+  COOC_HIP_TRY(hipMemsetAsync(scal + 1, 0, sizeof(int64_t), s));
+  k_merge_global<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
+      M, row_base, row_nnz, col, cnt, rowsum_delta, G, grs, scal);
+  k_finish_scalars<<<1, 1, 0, s>>>(scal, observed_window);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_touched(hipStream_t s, int32_t M, const int32_t *row_nnz, int32_t *touched, int64_t *n_touched,
+                      DevBuf &tmp) {
+  hipcub::CountingInputIterator<int32_t> it(0);
+  size_t bytes = 0;
+  COOC_HIP_TRY(hipcub::DeviceSelect::If(nullptr, bytes, it, touched, n_touched, M, IsTouched{row_nnz}, s));
+  COOC_TRY(tmp.reserve(bytes));
+  bytes = tmp.cap;
+  COOC_HIP_TRY(hipcub::DeviceSelect::If(tmp.p, bytes, it, touched, n_touched, M, IsTouched{row_nnz}, s));
+  return Status::Ok();
+}
+
+int rescore_waves_per_block(int32_t topk) { return topk <= 1024 ? 4 : 1; }
+
+size_t rescore_lds_bytes(int32_t topk) {
+  return size_t(rescore_waves_per_block(topk)) * size_t(topk + 1) * (sizeof(double) + sizeof(int32_t));
+}
+
+Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
+                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
+                      int32_t *out_val, double *out_score) {
+  const int waves = rescore_waves_per_block(topk);
+  const size_t lds = rescore_lds_bytes(topk);
+  if (lds > 64 * 1024)
+    COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  int dev = 0, n_cu = 256;
+  COOC_HIP_TRY(hipGetDevice(&dev));
+  COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t want = (int64_t(max_rows) + waves - 1) / waves;
+  const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
+  k_rescore<<<grid, 64 * waves, lds, s>>>(touched, scal, M, G, grs, exact ? 1 : 0, topk, out_size, out_val,
+                                         out_score);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+}  // namespace cooc

@@ -1,0 +1,23 @@
+// cooc_stream_kernels.h — launch wrappers of cooc_stream.hip (resident streaming state).
+#pragma once
+
+#include "cooc_device.h"
+
+namespace cooc {
+
+Status launch_relocate(hipStream_t s, int64_t n, const int64_t *reloc, int32_t *arena);
+Status launch_append(hipStream_t s, int64_t n, const int64_t *new_ptr, const int64_t *new_dst, const int32_t *items,
+                     int32_t *arena);
+// scal: [0] touched rows, [1] sum of the window's int row-sum deltas, [2] rescorer observed
+// (cumulative), [3] exact observed (cumulative).
+Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
+                           const int32_t *col, const uint32_t *cnt, const int64_t *rowsum_delta, uint32_t *G,
+                           int64_t *grs, int64_t *scal, int64_t observed_window);
+Status launch_touched(hipStream_t s, int32_t M, const int32_t *row_nnz, int32_t *touched, int64_t *n_touched,
+                      DevBuf &tmp);
+size_t rescore_lds_bytes(int32_t topk);
+Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
+                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
+                      int32_t *out_val, double *out_score);
+
+}  // namespace cooc

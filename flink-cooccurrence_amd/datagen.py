@@ -1,0 +1,166 @@
+"""Seeded synthetic interaction logs for BASELINE.json's configs.
+
+All generators use numpy PCG64 and return a CSR of per-user histories in arrival order:
+``user_ptr`` int64[U+1], ``items`` int32[N] and, for streaming configs, ``ts`` int64[N] (event time
+in ms, the `user,item,timestamp` schema of Configuration.java:59 / FlinkCooccurrences.java:207-217).
+There is no network: these stand in for MovieLens / click logs of the same shape.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _zipf_cdf(M: int, s: float) -> np.ndarray:
+    w = 1.0 / np.power(np.arange(1, M + 1, dtype=np.float64), s)
+    c = np.cumsum(w)
+    return c / c[-1]
+
+
+def _draw(rng, cdf: np.ndarray, n: int) -> np.ndarray:
+    return np.minimum(np.searchsorted(cdf, rng.random(n), side="right"), len(cdf) - 1).astype(np.int32)
+
+
+def ordered_pairs(user_ptr: np.ndarray) -> int:
+    """P = sum_u n_u (n_u - 1): the reference's ObservedCooccurrences unit (NonSampled...java:153)."""
+    n = np.diff(np.asarray(user_ptr, np.int64))
+    return int(np.sum(n * (n - 1)))
+
+
+def zipf_with_replacement(rng, lens: np.ndarray, M: int, s: float) -> np.ndarray:
+    return _draw(rng, _zipf_cdf(M, s), int(lens.sum()))
+
+
+def zipf_without_replacement(rng, lens: np.ndarray, M: int, s: float) -> np.ndarray:
+    """Distinct items per user, drawn from Zipf(s) by rejection of duplicates (rating-log shape).
+
+    Rounds only touch the users that still lack items; a user that overshoots keeps a random
+    subset of its distinct draws."""
+    cdf = _zipf_cdf(M, s)
+    U = len(lens)
+    lens = np.asarray(lens, np.int64)
+    if np.any(lens > M):
+        raise ValueError("a user cannot rate more distinct items than exist")
+    done = []
+    carry = np.zeros(0, np.int64)          # sorted keys (user * M + item) of unfinished users
+    act = np.arange(U, dtype=np.int64)     # unfinished users
+    have = np.zeros(U, np.int64)
+    rnd = 0
+    while len(act):
+        need = lens[act] - have[act]
+        draw = (need * (1.3 + 0.7 * rnd) + 8).astype(np.int64)
+        users = np.repeat(act, draw)
+        keys = np.unique(np.concatenate([carry, users * M + _draw(rng, cdf, len(users))]))
+        owner = keys // M
+        # trim overshoot: a user with more distinct draws than lens[u] keeps a random subset
+        cnt = np.bincount(owner, minlength=U)
+        over = cnt[owner] > lens[owner]
+        if over.any():
+            ok, ko = keys[~over], keys[over]
+            oo = ko // M
+            order = np.argsort((oo << 24) | rng.integers(0, 1 << 24, len(ko)), kind="stable")
+            ko, oo = ko[order], oo[order]
+            first = np.searchsorted(oo, oo, side="left")
+            ko = ko[(np.arange(len(ko)) - first) < lens[oo]]
+            keys = np.sort(np.concatenate([ok, ko]))
+            owner = keys // M
+        cnt = np.bincount(owner, minlength=U)
+        have[act] = cnt[act]
+        complete = cnt[owner] >= lens[owner]
+        done.append(keys[complete])
+        carry = np.sort(keys[~complete])
+        act = act[have[act] < lens[act]]
+        rnd += 1
+    keys = np.concatenate(done) if done else np.zeros(0, np.int64)
+    owner = keys // M
+    # arrival order inside each user: random permutation
+    order = np.argsort((owner << 24) | rng.integers(0, 1 << 24, len(keys)))
+    return (keys[order] % M).astype(np.int32)
+
+
+def config_c1(seed: int = 1, U: int = 10_000, M: int = 1_000, mean: float = 20.0, window_ms: int = 1000):
+    """C1, the reference MiniCluster config: click log, Poisson(20) items/user, Zipf(1.0) with
+    replacement, strictly ascending ms timestamps over a random interleave of users, 1 s windows."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = np.maximum(rng.poisson(mean, U), 1).astype(np.int64)
+    items = zipf_with_replacement(rng, lens, M, 1.0)
+    user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    # arrival: a random interleave of the users' streams, one interaction per ms.  Slot k of the
+    # arrival sequence belongs to user seq_owner[k]; user u's i-th interaction (CSR order) takes u's
+    # i-th slot, so grouping the slots by user (stable) lists the CSR timestamps in order.
+    owner = np.repeat(np.arange(U, dtype=np.int64), lens)
+    seq_owner = owner[rng.permutation(len(owner))]
+    ts_csr = np.argsort(seq_owner, kind="stable").astype(np.int64)
+    return dict(user_ptr=user_ptr, items=items, ts=ts_csr, n_items=M, window_ms=window_ms,
+                name="C1 click log 10k users x 1k items", seed=seed)
+
+
+def lognormal_lengths(rng, U: int, N: int, floor: int, cap: int, sigma: float = 1.0) -> np.ndarray:
+    """n_u = max(floor, lognormal) rescaled so that sum n_u == N exactly, each in [floor, cap]."""
+    x = rng.lognormal(0.0, sigma, U)
+    lens = np.maximum(floor, np.round(x * (N / x.sum()))).astype(np.int64)
+    for _ in range(64):
+        lens = np.clip(np.round(floor + (lens - floor) * ((N - floor * U) / max(1, (lens - floor).sum()))), floor,
+                       cap).astype(np.int64)
+        if abs(int(lens.sum()) - N) < U:
+            break
+    diff = N - int(lens.sum())
+    while diff != 0:
+        step = 1 if diff > 0 else -1
+        ok = np.nonzero((lens + step >= floor) & (lens + step <= cap))[0]
+        pick = rng.choice(ok, size=min(abs(diff), len(ok)), replace=False)
+        lens[pick] += step
+        diff = N - int(lens.sum())
+    return lens
+
+
+def config_c2(seed: int = 2, U: int = 138_493, M: int = 26_744, N: int = 20_000_263, s: float = 0.9,
+              floor: int = 20, cap: int = 5_000):
+    """C2, MovieLens-20M-shaped: n_u = max(20, lognormal) rescaled to exactly N; Zipf(0.9) items
+    without replacement per user (ratings are unique); one window."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = lognormal_lengths(rng, U, N, floor, min(cap, M))
+    items = zipf_without_replacement(rng, lens, M, s)
+    user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return dict(user_ptr=user_ptr, items=items, ts=None, n_items=M, window_ms=None,
+                name="C2 MovieLens-20M-shaped 138,493 users x 26,744 items, 20,000,263 interactions", seed=seed)
+
+
+def spread_over_windows(rng, user_ptr: np.ndarray, n_windows: int, window_ms: int) -> np.ndarray:
+    """C4: event times spread over n_windows tumbling windows, ascending within each user."""
+    n = int(user_ptr[-1])
+    ts = rng.integers(0, n_windows * window_ms, n).astype(np.int64)
+    lens = np.diff(user_ptr)
+    owner = np.repeat(np.arange(len(lens)), lens)
+    order = np.lexsort((ts, owner))
+    return ts[order]
+
+
+def config_c4(seed: int = 4, n_windows: int = 100, window_ms: int = 1000, **c2_kwargs):
+    """C4, streaming: the C2 log with timestamps spread over 100 tumbling 1 s windows."""
+    d = config_c2(**c2_kwargs)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    d["ts"] = spread_over_windows(rng, d["user_ptr"], n_windows, window_ms)
+    d["window_ms"] = window_ms
+    d["name"] = f"C4 streaming: C2 over {n_windows} x {window_ms} ms windows"
+    return d
+
+
+def small_log(seed: int, U: int, M: int, mean_len: float, s: float = 1.0, replacement: bool = True):
+    """Small seeded logs for parity tests."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = np.maximum(rng.poisson(mean_len, U), 1).astype(np.int64)
+    if replacement:
+        items = zipf_with_replacement(rng, lens, M, s)
+    else:
+        lens = np.minimum(lens, M)
+        items = zipf_without_replacement(rng, lens, M, s)
+    user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return user_ptr, items
+
+
+def to_records(user_ptr: np.ndarray, items: np.ndarray, ts: np.ndarray, user_ids: np.ndarray | None = None):
+    """CSR + per-interaction timestamps -> arrival-ordered (user, item, ts) records."""
+    lens = np.diff(user_ptr)
+    users = np.repeat(np.arange(len(lens), dtype=np.int32) if user_ids is None else user_ids, lens)
+    order = np.argsort(ts, kind="stable")
+    return users[order].astype(np.int32), items[order].astype(np.int32), ts[order].astype(np.int64)

@@ -1,0 +1,179 @@
+/*
+ * cooc.h — C-ABI of the MI355X co-occurrence core (pair expansion + keyed (itemA,itemB) count
+ * reduction, the non-sampled path of uce/flink-cooccurrence).
+ *
+ * Boundary.  The entry points replace, for the `--skip-cuts` job graph of
+ * FlinkCooccurrences.java:65-74,135-167, everything between the keyBy(user) edge and the sink:
+ *
+ *   reference (file:line, under src/main/java/com/github/uce/flinkcooccurrences/)   replaced by
+ *   ------------------------------------------------------------------------------  -------------------------------
+ *   NonSampledUserInteractionCounterOneInputStreamOperator.processElement :84-110   cooc_op_process_elements
+ *   NonSampledUserInteractionCounterOneInputStreamOperator.onEventTime    :113-165  cooc_op_process_watermark /
+ *     (+ ItemCooccurrences record & Kryo codec, ItemCooccurrences.java:14-149)        cooc_submit_batch +
+ *   ItemRowAggregator.ItemCooccurrenceRowAggregateFunction.add            :26-31      cooc_finish_window
+ *   ItemRowAggregator.ItemCooccurrenceRowWindowFunction.process           :50-56    cooc_copy_window_delta
+ *   RowSumAggregator.RowSumAggregateFunction.add / RowSumProcessWindow    :25-71    cooc_copy_window_rowsums
+ *   ItemRowRescorerTwoInputStreamOperator.processWatermark..scoreItem     :116-241  cooc_copy_window_topk
+ *   LogLikelihood.logLikelihoodRatio                                       :41-57    (inside the rescoring kernel)
+ *   IntDoublePriorityQueue add/update/iterator                             :132-242  (heap layout of topk output)
+ *   UserInteractionCounterObservedCooccurrences / LateElements /
+ *   RowSumProcessWindowRowSum / ItemRowRescorerRescoredItems accumulators            cooc_op_counters
+ *
+ * plus one stateless entry point over a device-resident CSR of user histories
+ * (cooc_count_device): one tumbling window over empty histories, the unit the benchmark times.
+ *
+ * Conventions:
+ *  - Every function returns an int status (COOC_OK = 0); the message of the last failure on a
+ *    context is cooc_last_error(ctx).  The Java wrapper rethrows IllegalStateException /
+ *    IllegalArgumentException where the reference throws them.
+ *  - The library never retains caller pointers after a call returns.  Results are either copied
+ *    into caller buffers (two-phase: sizes from cooc_window_info, then cooc_copy_*), or handed
+ *    out as BORROWED device views that stay valid until the next call on the same context.
+ *  - One context per Flink subtask; a context is not thread-safe, distinct contexts are.
+ *  - Item ids must lie in [0, cfg.n_items); user ids are arbitrary int32 (keyed state).
+ *  - Counts are exact (uint32, overflow is detected and reported as COOC_ERR_OVERFLOW); the
+ *    reference's own int16 (Int2ShortOpenHashMap) and int32 (Int2IntOpenHashMap / IntValue) wrapped
+ *    views are produced by the copy functions ("ref_compat").
+ *  - There is no CPU fallback: without a usable HIP device every compute entry point fails with
+ *    COOC_ERR_HIP.
+ */
+#ifndef COOC_H_
+#define COOC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COOC_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define COOC_API __attribute__((visibility("default")))
+#else
+#define COOC_API
+#endif
+
+enum cooc_status {
+  COOC_OK = 0,
+  COOC_ERR_ARG = 1,      /* IllegalArgumentException in the reference */
+  COOC_ERR_STATE = 2,    /* IllegalStateException in the reference */
+  COOC_ERR_HIP = 3,      /* HIP runtime / no device */
+  COOC_ERR_OOM = 4,      /* device allocation failed */
+  COOC_ERR_OVERFLOW = 5  /* an exact uint32 count overflowed */
+};
+
+/* Rescoring flavour for cooc_config.flags. */
+#define COOC_FLAG_EXACT_SCORES 1 /* LLR on exact counts instead of the reference's wrapped int16/int32 */
+
+typedef struct cooc_ctx cooc_ctx;
+
+typedef struct cooc_config {
+  int32_t device;         /* HIP device ordinal; -1 = the current device */
+  int32_t n_items;        /* item-id universe: ids in [0, n_items) */
+  int32_t topk;           /* ItemRowRescorer topK (ItemRowRescorer...java:51-56, Configuration.java:153);
+                             0 disables rescoring */
+  int32_t flags;          /* COOC_FLAG_* */
+  int64_t window_size_ms; /* TumblingEventTimeWindows.of(Time.of(windowSize, windowUnit)),
+                             NonSampled...java:61-62, in milliseconds */
+} cooc_config;
+
+/* Sizes of one fired window's outputs (two-phase copy protocol). */
+typedef struct cooc_window_info {
+  int64_t ts;             /* window.maxTimestamp(): timestamp of every output record, NonSampled...java:115 */
+  int64_t nnz;            /* entries over all delta rows */
+  int64_t observed;       /* exact ordered pairs of the window: sum of 2*|history| (NonSampled...java:153) */
+  int32_t n_rows;         /* items with a delta row (= items with a row-sum update) */
+  int32_t topk;           /* columns of the top-k output (cfg.topk) */
+  int32_t n_topk;         /* rescored rows (n_rows when topk > 0, else 0) */
+  int32_t reserved;
+} cooc_window_info;
+
+/* Borrowed device views of a cooc_count_device result (valid until the next call on ctx). */
+typedef struct cooc_device_result {
+  int64_t n_items;
+  int64_t nnz;            /* total entries */
+  int64_t observed;       /* exact ordered pairs sum_u n_u (n_u - 1) */
+  const int64_t *row_base;  /* [n_items]: first entry of row a in col/cnt (rows padded, not packed) */
+  const int32_t *row_nnz;   /* [n_items]: entries of row a */
+  const int32_t *col;       /* ascending within a row */
+  const uint32_t *cnt;      /* exact counts */
+  const int64_t *rowsum;    /* [n_items]: exact row sums sum_b C[a,b] */
+} cooc_device_result;
+
+/* ---- lifecycle ------------------------------------------------------------------------------ */
+COOC_API int cooc_abi_version(void);
+COOC_API const char *cooc_status_string(int status);
+COOC_API int cooc_create(const cooc_config *cfg, cooc_ctx **out);
+COOC_API void cooc_destroy(cooc_ctx *ctx);
+COOC_API const char *cooc_last_error(const cooc_ctx *ctx);
+
+/* ---- stateless one-window batch over a device CSR (the benchmarked unit) ----------------------
+ * d_user_ptr: int64[n_users+1] offsets into d_items (device memory); d_items: int32[n_interactions]
+ * in per-user arrival order.  hip_stream: a hipStream_t (NULL = the context's own stream).
+ * Computes C = sum over users of the ordered position pairs (p != q) -> (x_p, x_q), i.e. exactly
+ * what NonSampled...java:113-165 emits for users whose histories start empty, reduced by
+ * ItemRowAggregator/RowSumAggregator.  Does not touch the context's streaming state. */
+COOC_API int cooc_count_device(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                      int64_t n_interactions, void *hip_stream, cooc_device_result *out);
+/* Same from host buffers; afterwards cooc_copy_batch copies the packed CSR out. */
+COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
+                    cooc_window_info *info);
+/* Packed CSR over ALL n_items rows: row_ptr int64[n_items+1]; cols/cnt/cnt16 [nnz];
+ * rowsum int64[n_items], rowsum32 int32[n_items].  Any pointer may be NULL. */
+COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
+                    int32_t *rowsum32);
+
+/* ---- streaming (resident per-user histories, global rows, row sums) ------------------------
+ * cooc_submit_batch stages the interactions of one tumbling window: n_users users with their
+ * new items in arrival order (user_ptr int64[n_users+1] into items).  Several submits to the same
+ * window append.  cooc_finish_window expands every staged user against its resident history,
+ * reduces the window's delta rows and row sums, merges them into the global state and, if
+ * topk > 0, rescores every touched row (ItemRowRescorer...java:144-228). */
+COOC_API int cooc_submit_batch(cooc_ctx *ctx, int64_t window_ts, int32_t n_users, const int32_t *user_ids,
+                      const int64_t *user_ptr, const int32_t *items);
+COOC_API int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_info *info);
+
+/* Delta rows of the last finished window (ItemCooccurrenceRowWindowFunction output):
+ * rows int32[n_rows] ascending, row_ptr int64[n_rows+1], cols/cnt/cnt16 [nnz].  NULLs skipped. */
+COOC_API int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,
+                           int16_t *cnt16);
+/* Row-sum updates of the last window, one per delta row (same order as rows): exact int64 and the
+ * reference's int view (RowSumAggregator.java:25-27; the reference drops an update whose int
+ * value is 0, RowSumAggregator.java:66 -- the caller applies that filter on delta32). */
+COOC_API int cooc_copy_window_rowsums(cooc_ctx *ctx, int32_t *items, int64_t *delta, int32_t *delta32);
+/* Top-k of every rescored row: rows int32[n_topk], sizes int32[n_topk],
+ * values int32[n_topk*topk], scores double[n_topk*topk] in IntDoublePriorityQueue heap order
+ * (positions 1..size, least score first: IntDoublePriorityQueue.java:215-242). */
+COOC_API int cooc_copy_window_topk(cooc_ctx *ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores);
+
+/* Global state snapshots. */
+COOC_API int cooc_global_rowsums(cooc_ctx *ctx, int64_t *exact, int32_t *v32);          /* [n_items] each */
+COOC_API int cooc_global_observed(cooc_ctx *ctx, int64_t *exact, int64_t *rescorer);   /* rescorer: sum of int deltas */
+COOC_API int cooc_global_row_nnz(cooc_ctx *ctx, int32_t item, int64_t *nnz);
+COOC_API int cooc_global_row(cooc_ctx *ctx, int32_t item, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+
+/* ---- operator mirror: NonSampledUserInteractionCounterOneInputStreamOperator + aggregators ----
+ * cooc_op_process_elements: Tuple3(user,item,ts) records in arrival order; records with
+ * ts <= current watermark are dropped and counted (NonSampled...java:89-91).
+ * cooc_op_process_watermark: advances the watermark and fires AT MOST ONE pending window with
+ * maxTimestamp <= watermark (the earliest); sets *fired = 1 and fills *info if one fired (its
+ * outputs are then readable with cooc_copy_window_*), *fired = 0 when nothing is due.  Callers
+ * loop until *fired == 0, which mirrors the Flink timer service firing timers in timestamp order. */
+COOC_API int cooc_op_process_elements(cooc_ctx *ctx, int64_t n, const int32_t *users, const int32_t *items,
+                             const int64_t *ts, int64_t *n_late);
+COOC_API int cooc_op_process_watermark(cooc_ctx *ctx, int64_t watermark, int32_t *fired, cooc_window_info *info);
+/* counters[0] UserInteractionCounterLateElements, [1] UserInteractionCounterObservedCooccurrences,
+ * [2] RowSumProcessWindowRowSum, [3] ItemRowRescorerRescoredItems, [4] rescorer observed. */
+COOC_API int cooc_op_counters(cooc_ctx *ctx, int64_t *counters5);
+
+/* ---- diagnostics (not part of the reference surface) ------------------------------------------
+ * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the
+ * stream it is launched on; read back after a call that ran it. */
+COOC_API int cooc_set_kernel_timing(cooc_ctx *ctx, int32_t enable);
+COOC_API int cooc_last_kernel_ms(cooc_ctx *ctx, float *accumulate_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COOC_H_ */

@@ -1,0 +1,364 @@
+"""Oracle for the co-occurrence hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module.  The product path (``flink-cooccurrence_amd``) never imports it and fails loudly
+when its HIP library is missing; it has no CPU fallback.
+
+Three independent restatements of the reference's non-sampled path:
+
+1. ``OracleStream`` — ctypes wrapper of ``cooc_oracle.c``: the record-by-record restatement of
+   NonSampledUserInteractionCounterOneInputStreamOperator.java:84-165, ItemRowAggregator.java:26-56,
+   RowSumAggregator.java:25-71, ItemRowRescorerTwoInputStreamOperator.java:116-241,
+   LogLikelihood.java:41-61 and IntDoublePriorityQueue.java:132-205.
+2. ``closed_form`` — numpy/scipy ``C = A^T A - diag(colsum A)`` with A the user x item
+   multiplicity matrix, row sums ``sum_u m_ua (n_u - 1)`` and observed ``sum_u n_u (n_u - 1)``
+   (SURVEY.md §0.3).  Independent of (1): agreement of the two pins the literal expansion.
+3. ``literal_python`` — pure-Python transliteration of NonSampled...java:129-161 for tiny logs.
+
+Parity status: LLR and the heap are pinned by the reference's own KATs
+(LogLikelihoodTest.java:14-16, IntDoublePriorityQueueTest.java:12-98).  No reference fixture pins
+pair counts / row sums / windows and the Java reference cannot run here, so count parity is
+"parity unpinned" by the reference; hand-derived micro-logs (tests/golden/micro_logs.json) and
+the agreement of (1), (2) and (3) are what pin it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libcooc_oracle.so")
+_lib = None
+
+i32p = ctypes.POINTER(ctypes.c_int32)
+i64p = ctypes.POINTER(ctypes.c_int64)
+i16p = ctypes.POINTER(ctypes.c_int16)
+f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build() -> str:
+    """Compile the C restatement (make in oracle/)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+        os.path.join(_HERE, "cooc_oracle.c")
+    ):
+        build()
+    L = ctypes.CDLL(_LIB_PATH)
+    vp = ctypes.c_void_p
+    sig = {
+        "oc_llr": (ctypes.c_double, [ctypes.c_int64] * 4),
+        "oc_score_item": (ctypes.c_double, [ctypes.c_int16, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]),
+        "oc_pq_create": (vp, [ctypes.c_int32]),
+        "oc_pq_destroy": (None, [vp]),
+        "oc_pq_size": (ctypes.c_int32, [vp]),
+        "oc_pq_least_value": (ctypes.c_int32, [vp]),
+        "oc_pq_least_score": (ctypes.c_double, [vp]),
+        "oc_pq_reset": (None, [vp]),
+        "oc_pq_add": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_double]),
+        "oc_pq_update": (None, [vp, ctypes.c_int32, ctypes.c_double]),
+        "oc_pq_entries": (None, [vp, i32p, f64p]),
+        "oc_java_random_doubles": (None, [ctypes.c_int64, ctypes.c_int32, f64p]),
+        "oc_java_random_next_int32": (None, [ctypes.c_int64, ctypes.c_int32, i32p]),
+        "oc_java_random_ints": (None, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, i32p]),
+        "oc_create": (vp, [ctypes.c_int64, ctypes.c_int32]),
+        "oc_destroy": (None, [vp]),
+        "oc_window_max_ts": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+        "oc_process_element": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
+        "oc_process_elements": (ctypes.c_int64, [vp, ctypes.c_int64, i32p, i32p, i64p]),
+        "oc_process_watermark": (ctypes.c_int32, [vp, ctypes.c_int64]),
+        "oc_n_windows": (ctypes.c_int32, [vp]),
+        "oc_window_ts": (ctypes.c_int64, [vp, ctypes.c_int32]),
+        "oc_window_n_rows": (ctypes.c_int32, [vp, ctypes.c_int32]),
+        "oc_window_nnz": (ctypes.c_int64, [vp, ctypes.c_int32]),
+        "oc_window_observed": (ctypes.c_int64, [vp, ctypes.c_int32]),
+        "oc_window_n_rowsums": (ctypes.c_int32, [vp, ctypes.c_int32]),
+        "oc_window_n_topk": (ctypes.c_int32, [vp, ctypes.c_int32]),
+        "oc_window_delta": (None, [vp, ctypes.c_int32, i32p, i64p, i32p, i64p, i16p]),
+        "oc_window_rowsums": (None, [vp, ctypes.c_int32, i32p, i64p, i32p]),
+        "oc_window_topk": (None, [vp, ctypes.c_int32, i32p, i32p, i32p, f64p]),
+        "oc_counters": (None, [vp, i64p]),
+        "oc_global_n_rows": (ctypes.c_int32, [vp]),
+        "oc_global_nnz": (ctypes.c_int64, [vp]),
+        "oc_global_rows": (None, [vp, i32p, i64p, i32p, i64p, i16p]),
+        "oc_global_n_rowsums": (ctypes.c_int32, [vp]),
+        "oc_global_rowsums": (None, [vp, i32p, i32p, i64p]),
+        "oc_batch_dense": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, i64p, i64p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+# ---------------------------------------------------------------------------------------------
+# LogLikelihood / IntDoublePriorityQueue / java.util.Random restatements
+# ---------------------------------------------------------------------------------------------
+def llr(k11: int, k12: int, k21: int, k22: int) -> float:
+    """LogLikelihood.logLikelihoodRatio, LogLikelihood.java:41-57."""
+    return lib().oc_llr(k11, k12, k21, k22)
+
+
+def score_item(k11_i16: int, item_row_sum: int, other_row_sum: int, observed: int) -> float:
+    """ItemRowRescorerTwoInputStreamOperator.scoreItem, :230-241."""
+    return lib().oc_score_item(k11_i16, item_row_sum, other_row_sum, observed)
+
+
+class PriorityQueue:
+    """IntDoublePriorityQueue.java restated in C (1-based Lucene min-heap)."""
+
+    def __init__(self, max_size: int):
+        if max_size < 1:
+            raise ValueError("maxSize not positive")  # IntDoublePriorityQueue.java:70-72
+        self._q = lib().oc_pq_create(max_size)
+        self.max_size = max_size
+
+    def __del__(self):
+        if getattr(self, "_q", None):
+            lib().oc_pq_destroy(self._q)
+            self._q = None
+
+    def size(self) -> int:
+        return lib().oc_pq_size(self._q)
+
+    def least_value(self) -> int:
+        return lib().oc_pq_least_value(self._q)
+
+    def least_score(self) -> float:
+        return lib().oc_pq_least_score(self._q)
+
+    def reset(self) -> None:
+        lib().oc_pq_reset(self._q)
+
+    def add(self, value: int, score: float) -> None:
+        if lib().oc_pq_add(self._q, value, score) != 0:
+            raise IndexError("ArrayIndexOutOfBoundsException")  # Java's behaviour at :133-134
+
+    def update(self, value: int, score: float) -> None:
+        lib().oc_pq_update(self._q, value, score)
+
+    def entries(self):
+        n = self.size()
+        v = np.zeros(n, np.int32)
+        s = np.zeros(n, np.float64)
+        lib().oc_pq_entries(self._q, _p(v, i32p), _p(s, f64p))
+        return list(zip(v.tolist(), s.tolist()))
+
+
+def java_random_doubles(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.float64)
+    lib().oc_java_random_doubles(seed, n, _p(out, f64p))
+    return out
+
+
+def java_random_next_int32(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.int32)
+    lib().oc_java_random_next_int32(seed, n, _p(out, i32p))
+    return out
+
+
+def java_random_ints(seed: int, bound: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.int32)
+    lib().oc_java_random_ints(seed, bound, n, _p(out, i32p))
+    return out
+
+
+def window_max_ts(ts: int, size: int) -> int:
+    return lib().oc_window_max_ts(ts, size)
+
+
+# ---------------------------------------------------------------------------------------------
+# Streaming restatement: processElement / processWatermark and every fired window's outputs
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class WindowOutput:
+    ts: int
+    rows: np.ndarray       # int32 [R] ascending item ids with a delta row
+    row_ptr: np.ndarray    # int64 [R+1]
+    cols: np.ndarray       # int32 [nnz] ascending within a row
+    exact: np.ndarray      # int64 [nnz]
+    v16: np.ndarray        # int16 [nnz]  (Int2ShortOpenHashMap values)
+    rs_items: np.ndarray   # int32 items with non-zero exact row-sum delta
+    rs_exact: np.ndarray   # int64
+    rs_v32: np.ndarray     # int32 (RowSumAggregator int accumulation)
+    observed: int          # ObservedCooccurrences accumulator delta
+    topk_rows: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    topk_sizes: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    topk_values: np.ndarray = field(default_factory=lambda: np.zeros((0, 0), np.int32))
+    topk_scores: np.ndarray = field(default_factory=lambda: np.zeros((0, 0), np.float64))
+
+
+class OracleStream:
+    """Record-by-record restatement of the skip-cuts job from the keyBy(user) edge onwards."""
+
+    def __init__(self, window_size_ms: int, topk: int = 0):
+        self._s = lib().oc_create(window_size_ms, topk)
+        if not self._s:
+            raise ValueError("bad window size / topk")
+        self.topk = topk
+        self._read = 0
+
+    def __del__(self):
+        if getattr(self, "_s", None):
+            lib().oc_destroy(self._s)
+            self._s = None
+
+    def process_element(self, user: int, item: int, ts: int) -> bool:
+        """Returns True when the element was late and dropped (NonSampled...java:89-91)."""
+        return bool(lib().oc_process_element(self._s, user, item, ts))
+
+    def process_elements(self, users, items, ts) -> int:
+        u = np.ascontiguousarray(users, np.int32)
+        i = np.ascontiguousarray(items, np.int32)
+        t = np.ascontiguousarray(ts, np.int64)
+        return lib().oc_process_elements(self._s, len(u), _p(u, i32p), _p(i, i32p), _p(t, i64p))
+
+    def process_watermark(self, wm: int) -> list[WindowOutput]:
+        lib().oc_process_watermark(self._s, wm)
+        return self._drain()
+
+    def _drain(self) -> list[WindowOutput]:
+        L = lib()
+        out = []
+        n = L.oc_n_windows(self._s)
+        for w in range(self._read, n):
+            R = L.oc_window_n_rows(self._s, w)
+            nnz = L.oc_window_nnz(self._s, w)
+            rows = np.zeros(R, np.int32)
+            row_ptr = np.zeros(R + 1, np.int64)
+            cols = np.zeros(nnz, np.int32)
+            exact = np.zeros(nnz, np.int64)
+            v16 = np.zeros(nnz, np.int16)
+            L.oc_window_delta(self._s, w, _p(rows, i32p), _p(row_ptr, i64p), _p(cols, i32p), _p(exact, i64p),
+                              _p(v16, i16p))
+            nr = L.oc_window_n_rowsums(self._s, w)
+            rs_items = np.zeros(nr, np.int32)
+            rs_exact = np.zeros(nr, np.int64)
+            rs_v32 = np.zeros(nr, np.int32)
+            L.oc_window_rowsums(self._s, w, _p(rs_items, i32p), _p(rs_exact, i64p), _p(rs_v32, i32p))
+            wo = WindowOutput(L.oc_window_ts(self._s, w), rows, row_ptr, cols, exact, v16, rs_items, rs_exact,
+                              rs_v32, L.oc_window_observed(self._s, w))
+            nt = L.oc_window_n_topk(self._s, w)
+            if self.topk > 0:
+                tr = np.zeros(nt, np.int32)
+                ts_ = np.zeros(nt, np.int32)
+                tv = np.zeros((nt, self.topk), np.int32)
+                tsc = np.zeros((nt, self.topk), np.float64)
+                L.oc_window_topk(self._s, w, _p(tr, i32p), _p(ts_, i32p), _p(tv, i32p), _p(tsc, f64p))
+                wo.topk_rows, wo.topk_sizes, wo.topk_values, wo.topk_scores = tr, ts_, tv, tsc
+            out.append(wo)
+        self._read = n
+        return out
+
+    def counters(self) -> dict:
+        a = np.zeros(5, np.int64)
+        lib().oc_counters(self._s, _p(a, i64p))
+        return {
+            "UserInteractionCounterLateElements": int(a[0]),
+            "UserInteractionCounterObservedCooccurrences": int(a[1]),
+            "RowSumProcessWindowRowSum": int(a[2]),
+            "ItemRowRescorerRescoredItems": int(a[3]),
+            "rescorer_observed": int(a[4]),
+        }
+
+    def global_rows(self):
+        L = lib()
+        R = L.oc_global_n_rows(self._s)
+        nnz = L.oc_global_nnz(self._s)
+        rows = np.zeros(R, np.int32)
+        row_ptr = np.zeros(R + 1, np.int64)
+        cols = np.zeros(nnz, np.int32)
+        exact = np.zeros(nnz, np.int64)
+        v16 = np.zeros(nnz, np.int16)
+        L.oc_global_rows(self._s, _p(rows, i32p), _p(row_ptr, i64p), _p(cols, i32p), _p(exact, i64p), _p(v16, i16p))
+        return rows, row_ptr, cols, exact, v16
+
+    def global_rowsums(self):
+        L = lib()
+        n = L.oc_global_n_rowsums(self._s)
+        items = np.zeros(n, np.int32)
+        v32 = np.zeros(n, np.int32)
+        exact = np.zeros(n, np.int64)
+        L.oc_global_rowsums(self._s, _p(items, i32p), _p(v32, i32p), _p(exact, i64p))
+        return items, v32, exact
+
+
+# ---------------------------------------------------------------------------------------------
+# One-window batch forms (the stateless device entry point's contract)
+# ---------------------------------------------------------------------------------------------
+def batch_dense(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
+    """Literal expansion (C) of one window over empty histories -> dense int64 counts."""
+    user_ptr = np.ascontiguousarray(user_ptr, np.int64)
+    items = np.ascontiguousarray(items, np.int32)
+    counts = np.zeros((n_items, n_items), np.int64)
+    rowsums = np.zeros(n_items, np.int64)
+    obs = lib().oc_batch_dense(len(user_ptr) - 1, _p(user_ptr, i64p), _p(items, i32p), n_items,
+                               _p(counts, i64p), _p(rowsums, i64p))
+    return counts, rowsums, int(obs)
+
+
+def closed_form(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
+    """C = A^T A - diag(colsum A) as a sorted CSR (scipy), row sums and observed."""
+    import scipy.sparse as sp
+
+    user_ptr = np.asarray(user_ptr, np.int64)
+    items = np.asarray(items, np.int64)
+    U = len(user_ptr) - 1
+    lens = np.diff(user_ptr)
+    users = np.repeat(np.arange(U, dtype=np.int64), lens)
+    A = sp.csr_matrix((np.ones(len(items), np.int64), (users, items)), shape=(U, n_items))
+    A.sum_duplicates()
+    colsum = np.asarray(A.sum(axis=0)).ravel().astype(np.int64)
+    C = (A.T @ A).tocsr()
+    C = C - sp.diags(colsum, format="csr")
+    C.eliminate_zeros()
+    C.sort_indices()
+    rowsums = np.zeros(n_items, np.int64)
+    np.add.at(rowsums, items, np.repeat(lens - 1, lens))
+    observed = int(np.sum(lens * (lens - 1)))
+    return C.indptr.astype(np.int64), C.indices.astype(np.int32), C.data.astype(np.int64), rowsums, observed
+
+
+def literal_python(histories: list[list[int]]):
+    """Pure-Python NonSampled...java:129-161 over per-user item lists (tiny inputs only)."""
+    counts: dict[tuple[int, int], int] = {}
+    rowsums: dict[int, int] = {}
+    observed = 0
+    for items in histories:
+        history: list[int] = []
+        for item in items:
+            size = len(history)
+            if size > 0:
+                for o in history:
+                    counts[(item, o)] = counts.get((item, o), 0) + 1
+                rowsums[item] = rowsums.get(item, 0) + size
+                for o in history:
+                    counts[(o, item)] = counts.get((o, item), 0) + 1
+                    rowsums[o] = rowsums.get(o, 0) + 1
+                observed += 2 * size
+            history.append(item)
+    return counts, rowsums, observed
+
+
+def to_i16(x):
+    return np.asarray(x, np.int64).astype(np.uint16).view(np.int16)
+
+
+def to_i32(x):
+    return np.asarray(x, np.int64).astype(np.uint32).view(np.int32)

@@ -1,0 +1,125 @@
+"""Shared test helpers: golden micro-logs, window comparison (oracle vs HIP path)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+INT64_MAX = (1 << 63) - 1
+
+
+def micro_logs():
+    with open(os.path.join(GOLDEN, "micro_logs.json")) as f:
+        return json.load(f)["logs"]
+
+
+def micro_events(log):
+    """-> list of ('e', user, item, ts) / ('w', watermark) in arrival order."""
+    if "events" in log:
+        return [tuple(e) for e in log["events"]]
+    g = log["generator"]
+    ev = []
+    if g["kind"] == "pairs":
+        for u in range(g["users"]):
+            for it in g["items"]:
+                ev.append(("e", u, it, 500))
+    elif g["kind"] == "repeat":
+        for u in range(g["users"]):
+            ev.extend([("e", u, g["item"], 500)] * g["times"])
+    ev.append(("w", INT64_MAX))
+    return ev
+
+
+def micro_csr(log):
+    """One-window micro-log -> (user_ptr, items) CSR in arrival order."""
+    by_user: dict[int, list[int]] = {}
+    for e in micro_events(log):
+        if e[0] == "e":
+            by_user.setdefault(e[1], []).append(e[2])
+    users = sorted(by_user)
+    lens = [len(by_user[u]) for u in users]
+    user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    items = np.array([i for u in users for i in by_user[u]], np.int32)
+    return user_ptr, items
+
+
+def run_events(events, process_element, process_watermark, batch=True):
+    """Feed events to an operator; returns the list of fired windows."""
+    out = []
+    pend = []
+
+    def flush():
+        if pend:
+            u, i, t = zip(*pend)
+            process_element(np.array(u, np.int32), np.array(i, np.int32), np.array(t, np.int64))
+            pend.clear()
+
+    for e in events:
+        if e[0] == "e":
+            pend.append(e[1:])
+        else:
+            flush()
+            out.extend(process_watermark(e[1]))
+    flush()
+    return out
+
+
+def window_rows(w) -> dict:
+    """{row: {col: exact}} of a fired window (oracle.WindowOutput or core.WindowResult)."""
+    rows = {}
+    for r, a in enumerate(w.rows.tolist()):
+        s, e = int(w.row_ptr[r]), int(w.row_ptr[r + 1])
+        rows[a] = dict(zip(w.cols[s:e].tolist(), w.exact[s:e].tolist()))
+    return rows
+
+
+def window_rows16(w) -> dict:
+    rows = {}
+    for r, a in enumerate(w.rows.tolist()):
+        s, e = int(w.row_ptr[r]), int(w.row_ptr[r + 1])
+        rows[a] = dict(zip(w.cols[s:e].tolist(), w.v16[s:e].tolist()))
+    return rows
+
+
+def as_int_keys(d):
+    return {int(k): (as_int_keys(v) if isinstance(v, dict) else v) for k, v in d.items()}
+
+
+def assert_windows_equal(got, want, topk_rtol=1e-6):
+    """Bit-exact delta rows / row sums / observed; top-k by the tolerance contract of SURVEY §8(a)."""
+    assert got.ts == want.ts
+    assert np.array_equal(got.rows, want.rows), "delta row set differs"
+    assert np.array_equal(got.row_ptr, want.row_ptr), "delta row lengths differ"
+    assert np.array_equal(got.cols, want.cols), "delta columns differ"
+    assert np.array_equal(np.asarray(got.exact, np.int64), np.asarray(want.exact, np.int64)), "exact counts differ"
+    assert np.array_equal(got.v16, want.v16), "int16 view differs"
+    assert np.array_equal(got.rs_items, want.rs_items)
+    assert np.array_equal(got.rs_exact, want.rs_exact)
+    assert np.array_equal(got.rs_v32, want.rs_v32)
+    assert got.observed == want.observed
+    if len(want.topk_rows) or len(got.topk_rows):
+        assert_topk_equal(got, want, topk_rtol)
+
+
+def assert_topk_equal(got, want, rtol=1e-6):
+    assert np.array_equal(got.topk_rows, want.topk_rows)
+    assert np.array_equal(got.topk_sizes, want.topk_sizes)
+    for r in range(len(want.topk_rows)):
+        n = int(want.topk_sizes[r])
+        gs, ws = got.topk_scores[r, :n], want.topk_scores[r, :n]
+        gv, wv = got.topk_values[r, :n], want.topk_values[r, :n]
+        # The heap layouts agree exactly whenever every score agrees bit for bit (same iteration
+        # order, same comparisons).  Scores may differ by a few ulp (device vs glibc log), so compare
+        # the score multisets with a tolerance and the item sets strictly above the k-th score.
+        nan_g, nan_w = np.isnan(gs), np.isnan(ws)
+        assert np.array_equal(np.sort(nan_g), np.sort(nan_w)), "NaN scores differ"
+        g_sorted = np.sort(gs[~nan_g])
+        w_sorted = np.sort(ws[~nan_w])
+        tol = np.maximum(rtol * np.abs(w_sorted), 1e-9)
+        assert np.all(np.abs(g_sorted - w_sorted) <= tol), f"row {want.topk_rows[r]}: scores differ"
+        if n and not nan_w.any():
+            kth = w_sorted[0]
+            margin = max(rtol * abs(kth), 1e-9)
+            assert set(gv[gs > kth + margin].tolist()) == set(wv[ws > kth + margin].tolist())

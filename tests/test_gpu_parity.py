@@ -1,0 +1,268 @@
+"""Parity of the HIP path (through the C-ABI) against the oracle.  Needs an MI355X.
+
+Bar: bit-exact for every count, row sum, key set and wrapped view; LLR scores within the
+condition-aware tolerance of SURVEY.md §8(a) (rtol 1e-6 here, tighter than the reference's own 0.1
+KAT tolerance), top-k item sets equal strictly above the k-th score.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from tests._helpers import (INT64_MAX, as_int_keys, assert_windows_equal, micro_csr, micro_events, micro_logs,
+                            run_events, window_rows, window_rows16)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _batch_vs_closed_form(pkg, oracle, up, it, M):
+    with pkg.CooccurrenceCore(n_items=M) as core:
+        got = core.count(up, it)
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert got.observed == observed
+    assert np.array_equal(got.row_ptr, rp), "row lengths / key sets differ"
+    assert np.array_equal(got.cols, cols)
+    assert np.array_equal(got.cnt.astype(np.int64), data)
+    assert np.array_equal(got.cnt16, oracle.to_i16(data))
+    assert np.array_equal(got.rowsum, rowsums)
+    assert np.array_equal(got.rowsum32, oracle.to_i32(rowsums))
+    return got
+
+
+@pytest.mark.parametrize("seed,U,M,mean,repl", [
+    (1, 500, 97, 12.0, True),
+    (2, 3000, 1000, 20.0, True),      # C1 shape, scaled
+    (3, 2000, 4096, 40.0, False),     # rating-log shape
+    (4, 300, 40704, 60.0, True),      # the largest single-tile LDS row
+])
+def test_batch_random_logs(pkg, oracle, torch_cuda, seed, U, M, mean, repl):
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(seed, U, M, mean, replacement=repl)
+    _batch_vs_closed_form(pkg, oracle, up, it, M)
+
+
+def test_batch_matches_literal_expansion(pkg, oracle, torch_cuda):
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(5, 400, 64, 10.0)
+    got = _batch_vs_closed_form(pkg, oracle, up, it, 64)
+    dense, rs, obs = oracle.batch_dense(up, it, 64)
+    C = sp.csr_matrix((got.cnt.astype(np.int64), got.cols, got.row_ptr), shape=(64, 64)).toarray()
+    assert np.array_equal(C, dense) and np.array_equal(got.rowsum, rs) and got.observed == obs
+
+
+@pytest.mark.parametrize("case", ["empty", "empty_users", "singletons", "one_item_universe", "max_id", "one_user"])
+def test_batch_edge_cases(pkg, oracle, torch_cuda, case):
+    M = 50
+    if case == "empty":
+        up, it = np.zeros(1, np.int64), np.zeros(0, np.int32)
+    elif case == "empty_users":
+        up, it = np.array([0, 0, 3, 3, 5, 5], np.int64), np.array([1, 2, 3, 4, 4], np.int32)
+    elif case == "singletons":
+        up, it = np.arange(11, dtype=np.int64), np.arange(10, dtype=np.int32)
+    elif case == "one_item_universe":
+        M = 1
+        up, it = np.array([0, 3, 4, 8], np.int64), np.zeros(8, np.int32)
+    elif case == "max_id":
+        up, it = np.array([0, 4], np.int64), np.array([M - 1, 0, M - 1, 7], np.int32)
+    else:
+        up, it = np.array([0, 30], np.int64), np.arange(30, dtype=np.int32) % 7
+    _batch_vs_closed_form(pkg, oracle, up, it, M)
+
+
+def test_batch_split_heavy_rows(pkg, oracle, torch_cuda):
+    """Rows whose pair work exceeds one chunk (2^22) are split over workgroups and merged."""
+    rng = np.random.default_rng(9)
+    U, L, M = 2600, 1700, 5000
+    it = np.concatenate([np.concatenate([[0, 1], rng.choice(np.arange(2, M), L - 2, replace=False)])
+                         for _ in range(U)]).astype(np.int32)
+    up = (np.arange(U + 1) * L).astype(np.int64)
+    got = _batch_vs_closed_form(pkg, oracle, up, it, M)
+    assert got.rowsum[0] == U * (L - 1) > (1 << 22)
+
+
+@pytest.mark.parametrize("log", micro_logs(), ids=lambda l: l["name"])
+def test_micro_logs_batch(pkg, oracle, torch_cuda, log):
+    if len(log["windows"]) != 1:
+        pytest.skip("multi-window log: covered by the streaming test")
+    up, it = micro_csr(log)
+    M = int(it.max()) + 1
+    got = _batch_vs_closed_form(pkg, oracle, up, it, M)
+    w = log["windows"][0]
+    rows = {a: dict(zip(got.cols[got.row_ptr[a]:got.row_ptr[a + 1]].tolist(),
+                        got.cnt[got.row_ptr[a]:got.row_ptr[a + 1]].astype(np.int64).tolist()))
+            for a in range(M) if got.row_ptr[a + 1] > got.row_ptr[a]}
+    assert rows == as_int_keys(w["rows"])
+    if "rows16" in w:
+        r16 = {a: dict(zip(got.cols[got.row_ptr[a]:got.row_ptr[a + 1]].tolist(),
+                           got.cnt16[got.row_ptr[a]:got.row_ptr[a + 1]].tolist()))
+               for a in range(M) if got.row_ptr[a + 1] > got.row_ptr[a]}
+        assert r16 == as_int_keys(w["rows16"])
+    if "rowsums32" in w:
+        for a, v in as_int_keys(w["rowsums32"]).items():
+            assert got.rowsum32[a] == v
+    assert got.observed == w["observed"]
+
+
+@pytest.mark.parametrize("log", [l for l in micro_logs() if not l.get("closed_form_only")], ids=lambda l: l["name"])
+def test_micro_logs_operator(pkg, oracle, torch_cuda, log):
+    """The operator mirror (processElement / watermark firing / late drop) on the micro-logs."""
+    ev = micro_events(log)
+    M = 1 + max(e[2] for e in ev if e[0] == "e")
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(log["window_ms"], n_items=M, top_k=3)
+    got = run_events(ev, op.process_elements, op.process_watermark)
+    ref = oracle.OracleStream(log["window_ms"], topk=3)
+    want = run_events(ev, ref.process_elements, ref.process_watermark)
+    assert len(got) == len(want) == len(log["windows"])
+    for g, w, gold in zip(got, want, log["windows"]):
+        assert_windows_equal(g, w)
+        assert window_rows(g) == as_int_keys(gold["rows"])
+        if "rows16" in gold:
+            assert window_rows16(g) == as_int_keys(gold["rows16"])
+    acc, racc = op.accumulators(), ref.counters()
+    assert acc == racc
+    op.close()
+
+
+def test_bad_item_id_is_illegal_argument(pkg, torch_cuda):
+    with pkg.CooccurrenceCore(n_items=10) as core:
+        with pytest.raises(pkg.IllegalArgumentException):
+            core.count(np.array([0, 2], np.int64), np.array([3, 10], np.int32))
+        # the context stays usable
+        got = core.count(np.array([0, 2], np.int64), np.array([3, 4], np.int32))
+        assert got.observed == 2
+
+
+def test_count_device_padded_layout(pkg, oracle, torch_cuda):
+    import ctypes
+
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(21, 1000, 300, 15.0)
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=300, device=0) as core:
+        core.set_kernel_timing(True)
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        assert core.last_kernel_ms() > 0
+        rp, cols, data, rowsums, observed = oracle.closed_form(up, it, 300)
+        assert res.observed == observed and res.nnz == len(cols)
+        got = core.copy_batch(res.nnz, res.observed)
+        assert np.array_equal(got.cols, cols)
+        # borrowed device views: row_nnz matches the packed row lengths
+        nnz = np.zeros(300, np.int32)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy(nnz.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(res.row_nnz), ctypes.c_size_t(1200),
+                      ctypes.c_int(2))
+        assert np.array_equal(nnz, np.diff(rp))
+
+
+def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda):
+    """C1-shaped click log over 1 s windows: every window's delta rows, row sums, observed, the
+    rescorer's top-k, and the final global state."""
+    from flink_cooccurrence_amd import datagen
+
+    d = datagen.config_c1(seed=1, U=2000, M=300, mean=20.0)
+    users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=300, top_k=10)
+    ref = oracle.OracleStream(1000, topk=10)
+    got, want = [], []
+    for lo in range(0, len(users), 7000):  # watermarks between chunks, like periodic watermarks
+        sl = slice(lo, lo + 7000)
+        op.process_elements(users[sl], items[sl], ts[sl])
+        ref.process_elements(users[sl], items[sl], ts[sl])
+        wm = int(ts[sl][-1]) - 1
+        got += op.process_watermark(wm)
+        want += ref.process_watermark(wm)
+    got += op.process_watermark(INT64_MAX)
+    want += ref.process_watermark(INT64_MAX)
+    assert len(got) == len(want) > 10
+    for g, w in zip(got, want):
+        assert_windows_equal(g, w)
+    assert op.accumulators() == ref.counters()
+    rows, rp, cols, exact, v16 = ref.global_rows()
+    for r, a in enumerate(rows[:50]):
+        c, n, n16 = op.core.global_row(int(a))
+        assert np.array_equal(c, cols[rp[r]:rp[r + 1]])
+        assert np.array_equal(n.astype(np.int64), exact[rp[r]:rp[r + 1]])
+        assert np.array_equal(n16, v16[rp[r]:rp[r + 1]])
+    gi, gv32, gex = ref.global_rowsums()
+    ex, v32 = op.core.global_rowsums()
+    assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
+    op.close()
+
+
+def test_streaming_exact_scores_flag(pkg, oracle, torch_cuda):
+    """COOC_FLAG_EXACT_SCORES: LLR on exact counts (differs from the reference only after wrap)."""
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1000, n_items=20, top_k=2, exact_scores=True)
+    u = np.repeat(np.arange(40, dtype=np.int32), 3)
+    it = np.tile(np.array([1, 2, 3], np.int32), 40)
+    op.process_elements(u, it, np.full(len(u), 5, np.int64))
+    (w,) = op.process_watermark(INT64_MAX)
+    # exact observed = 40 users * 6 pairs; row 1 = {2: 40, 3: 40}
+    assert w.observed == 240
+    assert np.all(np.isfinite(w.topk_scores[:, :2]))
+    op.close()
+
+
+def test_submit_order_errors(pkg, torch_cuda):
+    with pkg.CooccurrenceCore(n_items=10, topk=2) as core:
+        core.submit_batch(999, [1], [0, 2], [1, 2])
+        with pytest.raises(pkg.IllegalStateException):
+            core.submit_batch(1999, [1], [0, 1], [3])
+        with pytest.raises(pkg.IllegalStateException):
+            core.finish_window(1999)
+        w = core.finish_window(999)
+        assert w.observed == 2
+
+
+def test_c2_scale_properties(pkg, oracle, torch_cuda):
+    """BASELINE configs[1] at full size: size-independent properties of the result."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    d = datagen.config_c2()
+    up, it, M = d["user_ptr"], d["items"], d["n_items"]
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        got = core.copy_batch(res.nnz, res.observed)
+    P = datagen.ordered_pairs(up)
+    assert got.observed == P
+    cnt = got.cnt.astype(np.int64)
+    assert cnt.sum() == P  # every ordered pair counted once
+    rows = np.repeat(np.arange(M), np.diff(got.row_ptr))
+    assert np.array_equal(np.bincount(rows, weights=cnt, minlength=M).astype(np.int64), got.rowsum)
+    # closed-form row sums: sum_u m_ua (n_u - 1)
+    lens = np.diff(up)
+    rs = np.bincount(it, weights=np.repeat(lens - 1, lens), minlength=M).astype(np.int64)
+    assert np.array_equal(rs, got.rowsum)
+    # columns strictly ascending within every row
+    d_cols = np.diff(got.cols.astype(np.int64))
+    starts = got.row_ptr[1:-1]
+    ok = np.ones(len(d_cols), bool)
+    ok[starts[(starts > 0) & (starts < len(got.cols))] - 1] = False
+    assert np.all(d_cols[ok] > 0)
+    # symmetry C == C^T through weighted checksums (no self pairs: ratings are unique)
+    w1 = np.bincount(rows, weights=got.cols.astype(np.float64) * cnt, minlength=M)
+    w2 = np.bincount(got.cols, weights=rows.astype(np.float64) * cnt, minlength=M)
+    colsum = np.bincount(got.cols, weights=cnt, minlength=M).astype(np.int64)
+    assert np.array_equal(colsum, got.rowsum)
+    assert np.allclose(w1.sum(), w2.sum())
+    # an exact sample of rows against the closed form on the users touching them
+    for a in [0, 1, 17, 5000, M - 1]:
+        has = np.add.reduceat((it == a).astype(np.int64), up[:-1]) > 0
+        row = np.bincount(it[np.repeat(has, lens)], minlength=M).astype(np.int64)
+        row[a] -= int(has.sum())
+        s, e = got.row_ptr[a], got.row_ptr[a + 1]
+        assert np.array_equal(got.cols[s:e], np.nonzero(row)[0])
+        assert np.array_equal(cnt[s:e], row[row != 0])

@@ -1,0 +1,101 @@
+"""The oracle against the hand-derived micro-logs and its independent restatements (CPU)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from tests._helpers import (INT64_MAX, as_int_keys, micro_csr, micro_events, micro_logs, run_events, window_rows,
+                            window_rows16)
+
+
+@pytest.mark.parametrize("log", micro_logs(), ids=lambda l: l["name"])
+def test_micro_logs(oracle, log):
+    if log.get("closed_form_only"):
+        up, it = micro_csr(log)
+        M = int(it.max()) + 1
+        rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+        w = log["windows"][0]
+        C = sp.csr_matrix((data, cols, rp), shape=(M, M))
+        for a, row in as_int_keys(w["rows"]).items():
+            for b, v in row.items():
+                assert C[a, b] == v
+                assert oracle.to_i16(v) == as_int_keys(w["rows16"])[a][b]
+        for a, v in as_int_keys(w["rowsums"]).items():
+            assert rowsums[a] == v
+            assert oracle.to_i32(v) == as_int_keys(w["rowsums32"])[a]
+        assert observed == w["observed"]
+        return
+    s = oracle.OracleStream(log["window_ms"], topk=3)
+    fired = run_events(micro_events(log), s.process_elements, s.process_watermark)
+    assert len(fired) == len(log["windows"])
+    for got, want in zip(fired, log["windows"]):
+        assert got.ts == want["ts"]
+        assert window_rows(got) == as_int_keys(want["rows"])
+        if "rows16" in want:
+            assert window_rows16(got) == as_int_keys(want["rows16"])
+        assert dict(zip(got.rs_items.tolist(), got.rs_exact.tolist())) == as_int_keys(want["rowsums"])
+        assert got.observed == want["observed"]
+    c = s.counters()
+    assert c["UserInteractionCounterLateElements"] == log["late"]
+    if "global_rows" in log:
+        rows, rp, cols, exact, _ = s.global_rows()
+        g = {int(a): dict(zip(cols[rp[r]:rp[r + 1]].tolist(), exact[rp[r]:rp[r + 1]].tolist()))
+             for r, a in enumerate(rows)}
+        assert g == as_int_keys(log["global_rows"])
+        items, v32, ex = s.global_rowsums()
+        assert dict(zip(items.tolist(), ex.tolist())) == as_int_keys(log["global_rowsums"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_three_restatements_agree(oracle, seed):
+    rng = np.random.default_rng(seed)
+    U, M = 60, 15
+    lens = rng.integers(1, 10, U)
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    it = rng.integers(0, M, up[-1]).astype(np.int32)
+    dense, rs, obs = oracle.batch_dense(up, it, M)
+    rp, cols, data, rs2, obs2 = oracle.closed_form(up, it, M)
+    assert np.array_equal(sp.csr_matrix((data, cols, rp), shape=(M, M)).toarray(), dense)
+    assert np.array_equal(rs, rs2) and obs == obs2
+    counts, rsd, obs3 = oracle.literal_python([it[up[u]:up[u + 1]].tolist() for u in range(U)])
+    D = np.zeros((M, M), np.int64)
+    for (a, b), v in counts.items():
+        D[a, b] = v
+    assert np.array_equal(D, dense) and obs3 == obs
+
+
+def test_streaming_windows_sum_to_closed_form(oracle):
+    """Per-window deltas summed over windows == C of the whole log; global rows == that sum."""
+    rng = np.random.default_rng(11)
+    U, M, n = 40, 25, 900
+    users = rng.integers(0, U, n).astype(np.int32)
+    items = rng.integers(0, M, n).astype(np.int32)
+    ts = np.sort(rng.integers(0, 10_000, n)).astype(np.int64)
+    s = oracle.OracleStream(1000, topk=5)
+    s.process_elements(users, items, ts)
+    wins = s.process_watermark(INT64_MAX)
+    assert [w.ts for w in wins] == sorted({int(oracle.window_max_ts(t, 1000)) for t in ts})
+    tot = np.zeros((M, M), np.int64)
+    for w in wins:
+        for r, a in enumerate(w.rows):
+            tot[a, w.cols[w.row_ptr[r]:w.row_ptr[r + 1]]] += w.exact[w.row_ptr[r]:w.row_ptr[r + 1]]
+    order = np.lexsort((np.arange(n), users))  # per-user arrival order
+    lens = np.bincount(users, minlength=U)
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    rp, cols, data, rs, obs = oracle.closed_form(up, items[order], M)
+    assert np.array_equal(tot, sp.csr_matrix((data, cols, rp), shape=(M, M)).toarray())
+    rows, grp, gcols, gex, g16 = s.global_rows()
+    G = np.zeros((M, M), np.int64)
+    for r, a in enumerate(rows):
+        G[a, gcols[grp[r]:grp[r + 1]]] = gex[grp[r]:grp[r + 1]]
+    assert np.array_equal(G, tot)
+    c = s.counters()
+    assert c["UserInteractionCounterObservedCooccurrences"] == obs == c["rescorer_observed"]
+    assert c["ItemRowRescorerRescoredItems"] == sum(len(w.rows) for w in wins)
+
+
+def test_window_assignment_matches_flink(oracle):
+    # TumblingEventTimeWindows offset 0: [k*size, (k+1)*size), maxTimestamp = end - 1
+    assert oracle.window_max_ts(0, 1000) == 999
+    assert oracle.window_max_ts(999, 1000) == 999
+    assert oracle.window_max_ts(1000, 1000) == 1999
+    assert oracle.window_max_ts(-1, 1000) == -1
