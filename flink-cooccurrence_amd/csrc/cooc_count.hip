@@ -29,7 +29,8 @@ namespace {
 constexpr int kAccThreads = 1024;
 constexpr int kAccWaves = kAccThreads / 64;
 constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
-constexpr int kMaxLdsCounters = (160 * 1024 - 1024) / 4;  // dense row in LDS (uint32 counters)
+constexpr int kMaxLdsCounters = 40704;            // dense row in LDS (uint32 counters)
+constexpr int kLdsBudget = 160 * 1024 - 256;      // dynamic LDS left after the kernels' static LDS
 
 template <class T>
 __device__ inline int64_t lower_bound_i64(const T *a, int64_t n, T x) {
@@ -277,6 +278,132 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate(
   }
 }
 
+// Segment start of every row-sorted contribution (arena offset of its first partner id), with
+// bit 63 set for a NEW position (the -1 self correction applies to it).
+__global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ aoff,
+                            const int32_t *__restrict__ aold, int64_t *__restrict__ seg) {
+  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const uint32_t v = cvals[c];
+  const uint32_t j = v >> 1;
+  const int64_t off = aoff[j];
+  seg[c] = (v & 1u) ? off + aold[j] : (off | (int64_t(1) << 63));
+}
+
+// ★ v2: the chunk's contributions are flattened into one virtual pair range.  Up to `db`
+// segment descriptors (virtual start, arena start) are staged in LDS per batch; the 16 waves split
+// the batch's range into equal contiguous pieces and walk it 64 lanes wide, so every lane stays
+// busy whatever the user-list lengths, and no wave waits on a per-user descriptor chain.
+__global__ __launch_bounds__(kAccThreads) void k_accumulate2(
+    const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
+    const int64_t *__restrict__ seg, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
+    int32_t M, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
+    int64_t *__restrict__ rowsum, int64_t *__restrict__ err) {
+  extern __shared__ int64_t lds64[];
+  int64_t *s_seg = lds64;                                            // [db] arena start - virtual start
+  uint32_t *s_vst = reinterpret_cast<uint32_t *>(lds64 + db);        // [db + 1] virtual starts
+  uint32_t *acc = s_vst + db + 1;                                    // [M]
+  __shared__ int32_t s_chunk;
+  __shared__ uint32_t s_self;
+  __shared__ uint32_t s_wave[kAccWaves];
+  __shared__ uint64_t s_red[kAccWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n_chunks = tot->n_chunks;
+  for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
+  for (;;) {
+    if (tid == 0) {
+      s_chunk = atomicAdd(queue, 1);
+      s_self = 0;
+    }
+    __syncthreads();
+    const int32_t ch = s_chunk;
+    if (ch >= n_chunks) break;
+    const Chunk c = chunks[ch];
+    for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
+      const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
+      const int64_t e0 = epre[b0];
+      uint32_t selfs = 0;
+      for (int32_t i = tid; i <= nb; i += kAccThreads) {
+        const uint32_t vs = uint32_t(epre[b0 + i] - e0);
+        s_vst[i] = vs;
+        if (i < nb) {
+          const int64_t sg = seg[b0 + i];
+          selfs += uint32_t(sg < 0);
+          s_seg[i] = (sg & ~(int64_t(1) << 63)) - int64_t(vs);
+        }
+      }
+      const uint64_t bal = __ballot(selfs != 0u);
+      if (lane == 0 && bal) atomicAdd(&s_self, uint32_t(__popcll(bal)));
+      __syncthreads();
+      const uint32_t total = s_vst[nb];
+      const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
+      const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
+      uint32_t v = lo + lane;
+      if (v < hi) {
+        // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
+        int32_t l = 0, r = nb;
+        while (r - l > 1) {
+          const int32_t m = (l + r) >> 1;
+          if (s_vst[m] <= v) l = m; else r = m;
+        }
+        int32_t cur = l;
+        uint32_t next = s_vst[cur + 1];
+        int64_t base = s_seg[cur];
+        for (; v < hi; v += 256) {
+          int64_t a[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t vk = v + 64u * k;
+            a[k] = -1;
+            if (vk < hi) {
+              while (vk >= next) {
+                cur++;
+                next = s_vst[cur + 1];
+                base = s_seg[cur];
+              }
+              a[k] = base + vk;
+            }
+          }
+          int32_t it[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) it[k] = a[k] >= 0 ? arena[a[k]] : -1;
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (it[k] >= 0) atomicAdd(&acc[it[k]], 1u);
+        }
+      }
+      __syncthreads();
+    }
+    const uint32_t self_total = s_self;
+    const int64_t chunk_rowsum = (epre[c.end] - epre[c.begin]) - int64_t(self_total);
+    if (tid == 0) {
+      acc[c.row] -= self_total;
+      atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
+    }
+    __syncthreads();
+    if (c.split < 0) {
+      uint64_t sum;
+      const uint32_t nnz = compact_row(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
+      const uint64_t total = block_sum_u64(sum, s_red);
+      if (tid == 0) {
+        row_nnz[c.row] = int32_t(nnz);
+        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+      }
+    } else {
+      uint32_t *srow = staging + int64_t(c.split) * M;
+      for (int32_t b = tid; b < M; b += kAccThreads) {
+        const uint32_t v = acc[b];
+        if (v) {
+          atomicAdd(srow + b, v);
+          acc[b] = 0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---- 8. split rows: compact the staging rows ------------------------------------------------------
 __global__ __launch_bounds__(kAccThreads) void k_finalize_split(
     const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M,
@@ -385,6 +512,15 @@ Status Counter::init(int32_t n_items) {
   const size_t lds = size_t(M_) * 4;
   COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  // v2: descriptors share the LDS with the row; as many as fit, 64..1024
+  db_ = int((kLdsBudget - lds - 4) / 12);
+  db_ = std::min(1024, db_ - db_ % 64);
+  if (db_ < 64) return Status{1, "n_items too large for the LDS row plus descriptors"};
+  const size_t lds2 = size_t(db_) * 12 + 4 + lds;
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate2),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  const char *v = getenv("COOC_ACC_VARIANT");
+  variant_ = (v && v[0] == '1') ? 1 : 2;
   return Status::Ok();
 }
 
@@ -392,7 +528,7 @@ void Counter::release() {
   DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
-                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_};
+                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
@@ -408,6 +544,7 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n + 1)));
+  if (variant_ == 2) COOC_TRY(seg_.reserve(sizeof(int64_t) * (n + 1)));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
   COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
   COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
@@ -472,6 +609,10 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
     // 4. pair work prefix
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, work_it, epre + 1, int(n), s));
+    if (variant_ == 2) {
+      k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
+      COOC_HIP_TRY(hipGetLastError());
+    }
   }
   // 3. row pointer
   k_row_ptr<<<blocks_for(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
@@ -529,9 +670,15 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   const int64_t grid = std::min<int64_t>(n_chunks, n_cu);
   if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  if (grid > 0) {
+  if (grid > 0 && variant_ == 1) {
     k_accumulate<<<unsigned(grid), kAccThreads, size_t(M) * 4, s>>>(
         chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), vals, au.off, au.len, au.old, au.arena, epre, M,
+        row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
+        staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
+    COOC_HIP_TRY(hipGetLastError());
+  } else if (grid > 0) {
+    k_accumulate2<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
+        chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), au.arena, epre, M, db_,
         row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
         staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
     COOC_HIP_TRY(hipGetLastError());

@@ -123,12 +123,14 @@ class Counter {
 
  private:
   int32_t M_ = 0;
+  int db_ = 0;       // segment descriptors staged per batch (accumulate v2)
+  int variant_ = 2;  // COOC_ACC_VARIANT=1 selects the per-contribution wave kernel (A/B)
   // workspace
   DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
   DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
-  DevBuf pk_row_ptr_, pk_col_, pk_cnt_;
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_;
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 
