@@ -199,6 +199,48 @@ __device__ inline uint32_t compact_row(Src *row, int32_t M, int32_t *__restrict_
   return base;
 }
 
+// Two-pass compaction: every wave owns a contiguous column range; pass 1 counts its nonzeros,
+// one block scan gives each wave its output offset, pass 2 writes (col, cnt) in column order.
+// Two barriers per row instead of two per 1024-column tile.
+__device__ inline uint32_t compact_row_ranges(uint32_t *row, int32_t M, int32_t *__restrict__ col_out,
+                                              uint32_t *__restrict__ cnt_out, int64_t out_base, uint64_t *sum,
+                                              uint32_t *s_wave) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t per = ((M + kAccWaves - 1) / kAccWaves + 63) & ~63;
+  const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
+  uint32_t cnt = 0;
+  for (int32_t b = lo + lane; b < hi; b += 64) cnt += uint32_t(__popcll(__ballot(row[b] != 0u)));
+  // lanes that skipped the last partial iteration still hold the same count (ballot is wave-wide)
+  cnt = __shfl(cnt, 0, 64);
+  if (lane == 0) s_wave[wave] = cnt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kAccWaves; w++) {
+    const uint32_t x = s_wave[w];
+    off += (w < wave) ? x : 0u;
+    tot += x;
+  }
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint64_t my_sum = 0;
+  for (int32_t b0 = lo; b0 < hi; b0 += 64) {
+    const int32_t b = b0 + lane;
+    const uint32_t v = b < hi ? row[b] : 0u;
+    const uint64_t m = __ballot(v != 0u);
+    if (v) {
+      const int64_t pos = out_base + off + uint32_t(__popcll(m & lt_mask));
+      col_out[pos] = b;
+      cnt_out[pos] = v;
+      row[b] = 0;
+      my_sum += v;
+    }
+    off += uint32_t(__popcll(m));
+  }
+  __syncthreads();
+  *sum = my_sum;
+  return tot;
+}
+
 // ---- 7. ★ the hot kernel --------------------------------------------------------------------------
 // Persistent: one 1024-thread workgroup per CU (the M-counter LDS row needs up to 159 KiB), chunks
 // dequeued heaviest-first from a device counter.  Waves take contributions round-robin; a
@@ -294,6 +336,7 @@ __global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const
 // segment descriptors (virtual start, arena start) are staged in LDS per batch; the 16 waves split
 // the batch's range into equal contiguous pieces and walk it 64 lanes wide, so every lane stays
 // busy whatever the user-list lengths, and no wave waits on a per-user descriptor chain.
+template <int U>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const int64_t *__restrict__ seg, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
@@ -350,10 +393,10 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
         int32_t cur = l;
         uint32_t next = s_vst[cur + 1];
         int64_t base = s_seg[cur];
-        for (; v < hi; v += 256) {
-          int64_t a[4];
+        for (; v < hi; v += 64u * U) {
+          int64_t a[U];
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
+          for (int k = 0; k < U; k++) {
             const uint32_t vk = v + 64u * k;
             a[k] = -1;
             if (vk < hi) {
@@ -365,11 +408,11 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
               a[k] = base + vk;
             }
           }
-          int32_t it[4];
+          int32_t it[U];
 #pragma unroll
-          for (int k = 0; k < 4; k++) it[k] = a[k] >= 0 ? arena[a[k]] : -1;
+          for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? arena[a[k]] : -1;
 #pragma unroll
-          for (int k = 0; k < 4; k++)
+          for (int k = 0; k < U; k++)
             if (it[k] >= 0) atomicAdd(&acc[it[k]], 1u);
         }
       }
@@ -384,7 +427,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     __syncthreads();
     if (c.split < 0) {
       uint64_t sum;
-      const uint32_t nnz = compact_row(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
+      const uint32_t nnz = compact_row_ranges(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
         row_nnz[c.row] = int32_t(nnz);
@@ -513,14 +556,19 @@ Status Counter::init(int32_t n_items) {
   COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   // v2: descriptors share the LDS with the row; as many as fit, 64..1024
-  db_ = int((kLdsBudget - lds - 4) / 12);
-  db_ = std::min(1024, db_ - db_ % 64);
-  if (db_ < 64) return Status{1, "n_items too large for the LDS row plus descriptors"};
+  db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
+  if (db_ < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
   const size_t lds2 = size_t(db_) * 12 + 4 + lds;
-  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate2),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<4>),
+                        reinterpret_cast<const void *>(k_accumulate2<8>),
+                        reinterpret_cast<const void *>(k_accumulate2<16>),
+                        reinterpret_cast<const void *>(k_accumulate2<32>)})
+    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
   const char *v = getenv("COOC_ACC_VARIANT");
   variant_ = (v && v[0] == '1') ? 1 : 2;
+  const char *u = getenv("COOC_ACC_UNROLL");
+  unroll_ = u ? atoi(u) : 16;
+  if (unroll_ != 4 && unroll_ != 8 && unroll_ != 32) unroll_ = 16;
   return Status::Ok();
 }
 
@@ -677,7 +725,10 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
         staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
     COOC_HIP_TRY(hipGetLastError());
   } else if (grid > 0) {
-    k_accumulate2<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
+    auto kern = unroll_ == 32 ? k_accumulate2<32>
+                : unroll_ == 8 ? k_accumulate2<8>
+                : unroll_ == 4 ? k_accumulate2<4> : k_accumulate2<16>;
+    kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
         chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), au.arena, epre, M, db_,
         row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
         staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));

@@ -125,6 +125,7 @@ class Counter {
   int32_t M_ = 0;
   int db_ = 0;       // segment descriptors staged per batch (accumulate v2)
   int variant_ = 2;  // COOC_ACC_VARIANT=1 selects the per-contribution wave kernel (A/B)
+  int unroll_ = 16;  // COOC_ACC_UNROLL: partner loads in flight per lane (4, 8, 16, 32)
   // workspace
   DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
