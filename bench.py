@@ -57,6 +57,11 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, budget_pairs: int = 80
                       f"one window, {dt:.1f} s"}
 
 
+def core_last_nnz(core) -> int:
+    """Distinct keys of this rank's local (pre-exchange) result."""
+    return int(core.partition_plan(1)[0])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +87,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    from flink_cooccurrence_amd import sharding
 
     d = datagen.config_c2(seed=2 + rank)
     up_h, it_h, M = d["user_ptr"], d["items"], d["n_items"]
@@ -93,23 +99,34 @@ def main():
 
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
     core.set_kernel_timing(True)
-    res = None
+
+    def step():
+        if world == 1:
+            return core.count_device(up, it)  # returns after the stream drained (errors are checked)
+        # users sharded over ranks; partial rows all-to-all'd to owner(a) = a mod world and merged
+        return sharding.count_sharded(core, up, it)
+
     for _ in range(args.warmup):
-        res = core.count_device(up, it)
+        step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms = []
+    res = None
     for _ in range(args.steps):
-        res = core.count_device(up, it)  # returns after the stream drained (errors are checked)
+        res = step()
         kernel_ms.append(core.last_kernel_ms())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    assert res.observed == P, "pair count mismatch"
-    D = int(res.nnz)
+    if world == 1:
+        assert res.observed == P, "pair count mismatch"
+        D = int(res.nnz)
+    else:
+        assert res.local_observed == P, "pair count mismatch"
+        D = int(core_last_nnz(core))
 
     stats = torch.tensor([elapsed, float(P), float(algorithmic_bytes(P, N, U, D))], dtype=torch.float64, device=dev)
     if world > 1:
@@ -151,11 +168,14 @@ def main():
             "workload": "C2 MovieLens-20M-shaped: 138,493 users x 26,744 items, 20,000,263 interactions, "
                         "Zipf(0.9) without replacement, one window, numpy PCG64 seed 2 (+rank)",
             "users_per_gpu": U, "items": M, "interactions_per_gpu": N, "ordered_pairs_per_gpu": P,
-            "distinct_keys_per_gpu": D, "parallelism": f"users sharded, dp{world}",
+            "distinct_keys_per_gpu": D,
+            "parallelism": f"users sharded over {world} GPU(s)" + (
+                "; partial rows all-to-all'd to owner(a) = a mod N over RCCL and merged; row sums all-reduced"
+                if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_accumulate",
+            "kernel": "k_accumulate2",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
@@ -168,6 +188,9 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if world > 1:
+        out["config"]["exchange"] = {"entries_sent_rank0": res.sent_entries, "entries_recv_rank0": res.recv_entries,
+                                     "bytes_per_entry": 8, "global_ordered_pairs_per_step": res.observed}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(up_h, it_h)
     if rank == 0:

@@ -87,6 +87,11 @@ _SIGS = {
     "cooc_op_process_elements": (ctypes.c_int, [vp, ctypes.c_int64, i32p, i32p, i64p, i64p]),
     "cooc_op_process_watermark": (ctypes.c_int, [vp, ctypes.c_int64, i32p, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_op_counters": (ctypes.c_int, [vp, i64p]),
+    "cooc_partition_plan": (ctypes.c_int, [vp, ctypes.c_int32, i64p]),
+    "cooc_partition_pack": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
+    "cooc_copy_rowsum_device": (ctypes.c_int, [vp, vp, vp]),
+    "cooc_merge_partitions": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
+                                             ctypes.POINTER(CoocDeviceResult)]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }

@@ -130,6 +130,33 @@ class CooccurrenceCore:
                                           _p(rs, i64p), _p(rs32, i32p)), self._h)
         return BatchResult(rp, cols, cnt, cnt16, rs, rs32, int(observed))
 
+    # ---- sharding layer (owner-partitioned exchange of partial rows) -----------------------------
+    def partition_plan(self, n_parts: int) -> np.ndarray:
+        out = np.zeros(n_parts, np.int64)
+        check(_lib.load().cooc_partition_plan(self._h, n_parts, _p(out, i64p)), self._h)
+        return out
+
+    def partition_pack(self, n_parts: int, row_nnz, entries, stream=None) -> None:
+        """row_nnz: int32 device tensor [n_items]; entries: int64 device tensor [sum of the plan]."""
+        check(_lib.load().cooc_partition_pack(self._h, n_parts, ctypes.c_void_p(row_nnz.data_ptr()),
+                                              ctypes.c_void_p(entries.data_ptr()) if entries.numel() else None,
+                                              None if stream is None else ctypes.c_void_p(int(stream))), self._h)
+
+    def copy_rowsum_device(self, rowsum, stream=None) -> None:
+        check(_lib.load().cooc_copy_rowsum_device(self._h, ctypes.c_void_p(rowsum.data_ptr()),
+                                                  None if stream is None else ctypes.c_void_p(int(stream))),
+              self._h)
+
+    def merge_partitions(self, n_parts: int, part: int, recv_row_nnz, recv_entries, rowsum_global=None,
+                         stream=None) -> CoocDeviceResult:
+        res = CoocDeviceResult()
+        check(_lib.load().cooc_merge_partitions(
+            self._h, n_parts, part, ctypes.c_void_p(recv_row_nnz.data_ptr()),
+            ctypes.c_void_p(recv_entries.data_ptr()) if recv_entries.numel() else None,
+            None if rowsum_global is None else ctypes.c_void_p(rowsum_global.data_ptr()),
+            None if stream is None else ctypes.c_void_p(int(stream)), ctypes.byref(res)), self._h)
+        return res
+
     def set_kernel_timing(self, enable: bool = True) -> None:
         check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)
 

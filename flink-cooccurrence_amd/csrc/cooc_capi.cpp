@@ -163,6 +163,58 @@ int cooc_op_counters(cooc_ctx *ctx, int64_t *counters5) {
   return COOC_OK;
 }
 
+static hipStream_t stream_of(cooc_ctx *ctx, void *s) { return s ? static_cast<hipStream_t>(s) : ctx->stream; }
+
+int cooc_partition_plan(cooc_ctx *ctx, int32_t n_parts, int64_t *h_entries) {
+  if (!ctx || !h_entries) return COOC_ERR_ARG;
+  if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result to partition");
+  Status s = hipSetDevice(ctx->device) == hipSuccess
+                 ? ctx->sharder.plan(ctx->batch_result, ctx->cfg.n_items, n_parts, ctx->batch_stream, h_entries)
+                 : Status{COOC_ERR_HIP, "hipSetDevice"};
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_partition_pack(cooc_ctx *ctx, int32_t n_parts, int32_t *d_row_nnz, uint64_t *d_entries, void *hip_stream) {
+  if (!ctx) return COOC_ERR_ARG;
+  if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result to partition");
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream_of(ctx, hip_stream);
+  if (s != ctx->batch_stream) (void)hipStreamSynchronize(ctx->batch_stream);
+  Status st = ctx->sharder.pack(ctx->batch_result, ctx->cfg.n_items, n_parts, s, d_row_nnz, d_entries);
+  return st.ok() ? COOC_OK : fail(ctx, st);
+}
+
+int cooc_copy_rowsum_device(cooc_ctx *ctx, int64_t *d_rowsum, void *hip_stream) {
+  if (!ctx || !d_rowsum) return COOC_ERR_ARG;
+  if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result");
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipMemcpyAsync(d_rowsum, ctx->batch_result.rowsum, sizeof(int64_t) * ctx->cfg.n_items,
+                                hipMemcpyDeviceToDevice, stream_of(ctx, hip_stream));
+  if (e != hipSuccess) return fail(ctx, COOC_ERR_HIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+  return COOC_OK;
+}
+
+int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t *d_recv_row_nnz,
+                          const uint64_t *d_recv_entries, const int64_t *d_rowsum_global, void *hip_stream,
+                          cooc_device_result *out) {
+  if (!ctx || !out || !d_recv_row_nnz) return COOC_ERR_ARG;
+  if (n_parts < 1) return fail(ctx, COOC_ERR_ARG, "n_parts must be >= 1");
+  (void)hipSetDevice(ctx->device);
+  cooc::MergeResult m;
+  Status s = ctx->sharder.merge(ctx->cfg.n_items, n_parts, part, d_recv_row_nnz, d_recv_entries, d_rowsum_global,
+                                stream_of(ctx, hip_stream), &m);
+  if (!s.ok()) return fail(ctx, s);
+  out->n_items = m.n_rows;
+  out->nnz = -1;
+  out->observed = -1;
+  out->row_base = m.row_base;
+  out->row_nnz = m.row_nnz;
+  out->col = m.col;
+  out->cnt = m.cnt;
+  out->rowsum = m.rowsum;
+  return COOC_OK;
+}
+
 int cooc_set_kernel_timing(cooc_ctx *ctx, int32_t enable) {
   if (!ctx) return COOC_ERR_ARG;
   ctx->timer.enabled = enable != 0;

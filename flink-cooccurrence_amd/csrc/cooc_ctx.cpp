@@ -37,6 +37,7 @@ cooc_ctx::~cooc_ctx() {
   (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
   stream_state.release();
+  sharder.release();
   counter.release();
   cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old};
   for (auto *b : bufs) b->release();
@@ -85,6 +86,8 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   out->cnt = r.cnt;
   out->rowsum = r.rowsum;
   have_batch = true;
+  batch_result = r;
+  batch_result.nnz = nnz;
   batch_observed = r.observed;
   batch_nnz = nnz;
   batch_stream = s;

@@ -10,6 +10,7 @@
 
 #include "../../include/cooc.h"
 #include "cooc_device.h"
+#include "cooc_shard.h"
 
 struct cooc_ctx;
 
@@ -104,6 +105,8 @@ struct cooc_ctx {
   cooc::Counter counter;
   cooc::KernelTimer timer;
   cooc::StreamState stream_state;
+  cooc::Sharder sharder;
+  cooc::CountResult batch_result;
   cooc::Operator op;
 
   // stateless batch buffers

@@ -1,0 +1,76 @@
+"""Multi-GPU sharding layer: users sharded over ranks, rows owned by a mod world.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Mirrors the
+reference's keyed data-parallelism:
+
+* keyBy(user) (FlinkCooccurrences.java:70)  -> every rank expands only its own users' histories;
+* keyBy(ItemCooccurrences::getItem) (:152)    -> an all-to-all of each rank's partial rows to the
+                                                 row's owner, then an owner-side merge;
+* rowSumStream.broadcast() (:163)             -> one all-reduce of the int64 row-sum vector.
+
+The compute (local reduce, pack, merge) runs in libcooc_hip.so; this module only moves buffers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def rows_owned(n_items: int, n_parts: int, part: int) -> int:
+    return (n_items - part + n_parts - 1) // n_parts if part < n_items else 0
+
+
+@dataclass
+class ShardResult:
+    part: int
+    n_parts: int
+    merged: object          # CoocDeviceResult of the owned rows (rows r -> items part + r * n_parts)
+    rowsum: torch.Tensor    # all-reduced exact row sums, int64 [n_items] (device)
+    observed: int           # global ordered pairs (sum over ranks)
+    local_observed: int
+    sent_entries: int
+    recv_entries: int
+
+
+def count_sharded(core, user_ptr, items, group=None, stream=None) -> ShardResult:
+    """One window over this rank's users, exchanged and merged by row owner."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = items.device
+    M = core.n_items
+    res = core.count_device(user_ptr, items, stream)
+    # row sums: all-reduce (the broadcast of the reference's row-sum stream)
+    rowsum = torch.empty(M, dtype=torch.int64, device=dev)
+    core.copy_rowsum_device(rowsum, stream)
+    _sync(dev, stream)
+    work = dist.all_reduce(rowsum, group=group, async_op=True)
+    # partial rows -> owners
+    send_counts = core.partition_plan(world)
+    row_nnz = torch.empty(M, dtype=torch.int32, device=dev)
+    entries = torch.empty(int(send_counts.sum()), dtype=torch.int64, device=dev)
+    core.partition_pack(world, row_nnz, entries, stream)
+    _sync(dev, stream)
+    counts = torch.as_tensor(send_counts, dtype=torch.int64, device=dev)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    recv_counts_h = recv_counts.cpu().tolist()
+    R = rows_owned(M, world, rank)
+    recv_nnz = torch.empty(R * world, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(recv_nnz, row_nnz, [R] * world, [rows_owned(M, world, o) for o in range(world)],
+                           group=group)
+    recv_entries = torch.empty(int(sum(recv_counts_h)), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_entries, entries, recv_counts_h, send_counts.tolist(), group=group)
+    work.wait()
+    obs = torch.tensor([res.observed], dtype=torch.int64, device=dev)
+    dist.all_reduce(obs, group=group)
+    _sync(dev, stream)
+    merged = core.merge_partitions(world, rank, recv_nnz, recv_entries, rowsum, stream)
+    return ShardResult(rank, world, merged, rowsum, int(obs.item()), int(res.observed), int(send_counts.sum()),
+                       int(sum(recv_counts_h)))
+
+
+def _sync(dev, stream):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)

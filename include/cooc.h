@@ -167,6 +167,27 @@ COOC_API int cooc_op_process_watermark(cooc_ctx *ctx, int64_t watermark, int32_t
  * [2] RowSumProcessWindowRowSum, [3] ItemRowRescorerRescoredItems, [4] rescorer observed. */
 COOC_API int cooc_op_counters(cooc_ctx *ctx, int64_t *counters5);
 
+/* ---- multi-GPU sharding layer (the keyBy(itemA) exchange, FlinkCooccurrences.java:152,163) ---------
+ * Users are sharded over GPUs; each GPU's cooc_count_device result holds PARTIAL rows.  Row a is
+ * owned by GPU (a mod n_parts).  The caller moves the packed partial rows with an all-to-all
+ * (RCCL over xGMI, e.g. torch.distributed.all_to_all_single) and the row sums with an all-reduce.
+ *   cooc_partition_plan   entries of the last cooc_count_device result per owner -> h_entries[n_parts]
+ *   cooc_partition_pack   into caller DEVICE buffers, owner-major then ascending row:
+ *                         d_row_nnz int32[n_items], d_entries uint64[sum h_entries] = (col << 32 | cnt)
+ *   cooc_copy_rowsum_device  the last result's exact row sums into a caller device int64[n_items]
+ *   cooc_merge_partitions for owner `part`: d_recv_row_nnz int32[n_parts * rows_owned] and
+ *                         d_recv_entries (both source-major, as delivered by the all-to-all);
+ *                         d_rowsum_global (the all-reduced row sums, may be NULL) checks every merged
+ *                         row.  Result rows r = 0..n_rows-1 are items part + r * n_parts (borrowed
+ *                         device views in *out; out->n_items = rows owned). */
+COOC_API int cooc_partition_plan(cooc_ctx *ctx, int32_t n_parts, int64_t *h_entries);
+COOC_API int cooc_partition_pack(cooc_ctx *ctx, int32_t n_parts, int32_t *d_row_nnz, uint64_t *d_entries,
+                                 void *hip_stream);
+COOC_API int cooc_copy_rowsum_device(cooc_ctx *ctx, int64_t *d_rowsum, void *hip_stream);
+COOC_API int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t *d_recv_row_nnz,
+                                   const uint64_t *d_recv_entries, const int64_t *d_rowsum_global, void *hip_stream,
+                                   cooc_device_result *out);
+
 /* ---- diagnostics (not part of the reference surface) ------------------------------------------
  * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the
  * stream it is launched on; read back after a call that ran it. */

@@ -266,3 +266,69 @@ def test_c2_scale_properties(pkg, oracle, torch_cuda):
         s, e = got.row_ptr[a], got.row_ptr[a + 1]
         assert np.array_equal(got.cols[s:e], np.nonzero(row)[0])
         assert np.array_equal(cnt[s:e], row[row != 0])
+
+
+def _d2h(ptr, n, dtype):
+    import ctypes
+
+    out = np.zeros(n, dtype)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr),
+                             ctypes.c_size_t(out.nbytes), ctypes.c_int(2)) == 0
+    return out
+
+
+@pytest.mark.parametrize("n_parts", [2, 3])
+def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts):
+    """The sharding kernels on one GPU: n_parts user shards reduced separately, packed by owner,
+    'all-to-all' done by slicing, merged per owner == C of all users together."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen, sharding
+
+    up, it = datagen.small_log(31, 1500, 700, 25.0)
+    M, U = 700, len(up) - 1
+    dev = torch.device("cuda")
+    cores, packs = [], []
+    rowsum = torch.zeros(M, dtype=torch.int64, device=dev)
+    for s in range(n_parts):
+        lo, hi = s * U // n_parts, (s + 1) * U // n_parts
+        sup = torch.from_numpy(up[lo:hi + 1] - up[lo]).to(dev)
+        sit = torch.from_numpy(it[up[lo]:up[hi]]).to(dev)
+        core = pkg.CooccurrenceCore(n_items=M, device=0)
+        core.count_device(sup, sit)
+        counts = core.partition_plan(n_parts)
+        row_nnz = torch.empty(M, dtype=torch.int32, device=dev)
+        entries = torch.empty(int(counts.sum()), dtype=torch.int64, device=dev)
+        core.partition_pack(n_parts, row_nnz, entries)
+        rs = torch.empty(M, dtype=torch.int64, device=dev)
+        core.copy_rowsum_device(rs)
+        torch.cuda.synchronize()
+        rowsum += rs
+        cores.append(core)
+        packs.append((counts, row_nnz, entries))
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert np.array_equal(rowsum.cpu().numpy(), rowsums)
+    for p in range(n_parts):
+        R = sharding.rows_owned(M, n_parts, p)
+        rstart = [sum(sharding.rows_owned(M, n_parts, o) for o in range(p))]
+        recv_nnz = torch.cat([pk[1][rstart[0]:rstart[0] + R] for pk in packs])
+        recv_ent = torch.cat([pk[2][int(pk[0][:p].sum()):int(pk[0][:p + 1].sum())] for pk in packs])
+        m = cores[p].merge_partitions(n_parts, p, recv_nnz, recv_ent, rowsum)
+        torch.cuda.synchronize()
+        assert m.n_items == R
+        base = _d2h(m.row_base, R, np.int64)
+        nnz = _d2h(m.row_nnz, R, np.int32)
+        cap = int(base[-1] + nnz[-1]) if R else 0
+        mc = _d2h(m.col, cap, np.int32)
+        mn = _d2h(m.cnt, cap, np.uint32)
+        msum = _d2h(m.rowsum, R, np.int64)
+        for r in range(R):
+            a = p + r * n_parts
+            s, e = rp[a], rp[a + 1]
+            assert nnz[r] == e - s
+            assert np.array_equal(mc[base[r]:base[r] + nnz[r]], cols[s:e])
+            assert np.array_equal(mn[base[r]:base[r] + nnz[r]].astype(np.int64), data[s:e])
+            assert msum[r] == rowsums[a]
+    for c in cores:
+        c.close()
