@@ -174,8 +174,15 @@ class CooccurrenceCore:
                                             _p(it, i32p)), self._h)
 
     def finish_window(self, window_ts: int) -> WindowResult:
+        return self._window(self.finish_window_info(window_ts))
+
+    def finish_window_info(self, window_ts: int) -> CoocWindowInfo:
+        """Process the staged window; its outputs stay on the device until window_result()."""
         info = CoocWindowInfo()
         check(_lib.load().cooc_finish_window(self._h, window_ts, ctypes.byref(info)), self._h)
+        return info
+
+    def window_result(self, info: CoocWindowInfo) -> WindowResult:
         return self._window(info)
 
     def _window(self, info: CoocWindowInfo) -> WindowResult:

@@ -12,7 +12,7 @@
 //   4. inclusive scan     of each contribution's segment length = its pair work
 //   5. k_plan_rows        per-row work, split into chunks of <= kChunkWork pairs, output capacity
 //   6. k_make_chunks      chunk table, heaviest rows first
-//   7. k_accumulate       ★ persistent: per chunk a dense M-counter LDS row, one ds_add_u32 per pair,
+//   7. k_accumulate2      ★ persistent: per chunk a dense M-counter LDS row, one ds_add_u32 per pair,
 //                           compacted in column order into the padded CSR (or flushed into a
 //                           staging row when the row is split over chunks)
 //   8. k_finalize_split   compacts staging rows of split rows
@@ -30,6 +30,7 @@ constexpr int kAccThreads = 1024;
 constexpr int kAccWaves = kAccThreads / 64;
 constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
 constexpr int kMaxLdsCounters = 40704;            // dense row in LDS (uint32 counters)
+constexpr int kTileMax = 32768;                   // column tile width when n_items exceeds one LDS row
 constexpr int kLdsBudget = 160 * 1024 - 256;      // dynamic LDS left after the kernels' static LDS
 
 template <class T>
@@ -88,18 +89,24 @@ struct WorkOp {  // pair work of a contribution = its segment length
 // ---- 5. per-row plan ------------------------------------------------------------------------------
 __global__ void k_plan_rows(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ epre, int32_t M,
                             uint64_t *__restrict__ row_work, int32_t *__restrict__ order,
-                            int32_t *__restrict__ row_nch, int64_t *__restrict__ row_cap,
-                            int32_t *__restrict__ row_split) {
+                            int32_t *__restrict__ row_nch, int32_t *__restrict__ row_split) {
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= M) return;
-  const int64_t c0 = row_ptr[a], c1 = row_ptr[a + 1];
-  const int64_t w = epre[c1] - epre[c0];
-  const int32_t nch = c1 > c0 ? int32_t(w > kChunkWork ? (w + kChunkWork - 1) / kChunkWork : 1) : 0;
+  const int64_t w = epre[row_ptr[a + 1]] - epre[row_ptr[a]];
+  const int32_t nch = w > 0 ? int32_t((w + kChunkWork - 1) / kChunkWork) : 0;
   row_work[a] = uint64_t(w);
   order[a] = a;
   row_nch[a] = nch;
-  row_cap[a] = c1 > c0 ? (w < M ? w : int64_t(M)) : 0;
   row_split[a] = nch > 1 ? 1 : 0;
+}
+
+// Output capacity of a row: min(M, pair work of the whole row) (its entry count cannot exceed either).
+__global__ void k_row_cap(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ epre, int32_t M,
+                          int64_t *__restrict__ row_cap) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  const int64_t w = epre[row_ptr[a + 1]] - epre[row_ptr[a]];
+  row_cap[a] = w < M ? w : int64_t(M);
 }
 
 __global__ void k_gather_i32(const int32_t *__restrict__ order, const int32_t *__restrict__ src, int32_t n,
@@ -114,16 +121,81 @@ __global__ void k_split_rows(const int32_t *__restrict__ row_split, const int32_
   if (a < M && row_split[a]) split_row[split_slot[a]] = a;
 }
 
-__global__ void k_totals(const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_base,
-                         const int32_t *__restrict__ split_slot, const int64_t *__restrict__ epre, int32_t M,
-                         int64_t n_contrib, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue) {
+__global__ void k_totals(const int32_t *__restrict__ ord_cbase, const int32_t *__restrict__ split_slot, int32_t M,
+                         PlanTotals *__restrict__ tot, int32_t *__restrict__ queue) {
   tot->n_chunks = ord_cbase[M];
-  tot->cap_total = row_base[M];
   tot->n_split = split_slot[M];
-  tot->work_total = epre[n_contrib];
-  tot->nnz_total = 0;
   queue[0] = 0;
   queue[1] = 0;
+}
+
+__global__ void k_cap_total(const int64_t *__restrict__ row_base, const int64_t *__restrict__ epre, int32_t M,
+                            int64_t n_contrib, PlanTotals *__restrict__ tot) {
+  tot->cap_total = row_base[M];
+  tot->work_total = epre[n_contrib];
+  tot->nnz_total = 0;
+}
+
+__device__ inline void wave_sync() {  // LDS visibility among the lanes of one wave
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Tile partition of every user's history (column tiles of width tw): per user, its items grouped by
+// tile (order inside a tile segment is irrelevant to the counts), and tb[j][t] = offset of tile t's
+// segment inside the user's list (t = 0..T).  One wave per user, tile cursors in LDS.
+__global__ __launch_bounds__(256) void k_tile_partition(int64_t n_users, const int64_t *__restrict__ off,
+                                                        const int32_t *__restrict__ len,
+                                                        const int32_t *__restrict__ arena, int32_t tw, int32_t T,
+                                                        int32_t *__restrict__ tarena, int32_t *__restrict__ tb) {
+  extern __shared__ int32_t cur[];  // [4 waves][T + 1]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t *c = cur + wave * (T + 1);
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = gw; j < n_users; j += n_waves) {
+    const int32_t *h = arena + off[j];
+    int32_t *o = tarena + off[j];
+    const int32_t n = len[j];
+    for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
+    wave_sync();
+    for (int32_t p = lane; p < n; p += 64) atomicAdd(&c[h[p] / tw], 1);
+    wave_sync();
+    if (lane == 0) {  // exclusive prefix (T is small)
+      int32_t run = 0;
+      for (int32_t t = 0; t <= T; t++) {
+        const int32_t x = c[t];
+        c[t] = run;
+        run += x;
+      }
+    }
+    wave_sync();
+    for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
+    wave_sync();
+    for (int32_t p = lane; p < n; p += 64) {
+      const int32_t it = h[p];
+      o[atomicAdd(&c[it / tw], 1)] = it;
+    }
+    wave_sync();
+  }
+}
+
+struct TileWorkOp {  // pair work of a contribution inside column tile t
+  const int32_t *tb;
+  int32_t T, t;
+  __host__ __device__ int64_t operator()(uint32_t v) const {
+    const int64_t j = v >> 1;
+    return int64_t(tb[j * (T + 1) + t + 1] - tb[j * (T + 1) + t]);
+  }
+};
+
+__global__ void k_seg_start_tile(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ aoff,
+                                 const int32_t *__restrict__ tb, int32_t T, int32_t t, int64_t *__restrict__ seg) {
+  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const uint32_t v = cvals[c];
+  const int64_t j = v >> 1;
+  seg[c] = (aoff[j] + tb[j * (T + 1) + t]) | (int64_t(1) << 63);  // batch path: every position is new
 }
 
 // ---- 6. chunk table -------------------------------------------------------------------------------
@@ -159,50 +231,11 @@ __device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t *s_red) {
   return t;
 }
 
-// Column-order compaction of a dense row (LDS or global) into (col, cnt) at out_base; zeroes the
-// source.  Returns the entry count (block-uniform) and the sum of counts.
-template <class Src>
-__device__ inline uint32_t compact_row(Src *row, int32_t M, int32_t *__restrict__ col_out,
-                                       uint32_t *__restrict__ cnt_out, int64_t out_base, uint64_t *sum,
-                                       uint32_t *s_wave) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t base = 0;
-  uint64_t my_sum = 0;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int32_t t0 = 0; t0 < M; t0 += kAccThreads) {
-    const int32_t b = t0 + tid;
-    uint32_t v = 0;
-    if (b < M) {
-      v = row[b];
-      if (v) row[b] = 0;
-    }
-    const uint64_t m = __ballot(v != 0);
-    if (lane == 0) s_wave[wave] = uint32_t(__popcll(m));
-    __syncthreads();
-    uint32_t woff = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kAccWaves; w++) {
-      const uint32_t x = s_wave[w];
-      woff += (w < wave) ? x : 0u;
-      tot += x;
-    }
-    if (v) {
-      const int64_t pos = out_base + base + woff + uint32_t(__popcll(m & lt_mask));
-      col_out[pos] = b;
-      cnt_out[pos] = v;
-      my_sum += v;
-    }
-    base += tot;
-    __syncthreads();
-  }
-  *sum = my_sum;
-  return base;
-}
-
 // Two-pass compaction: every wave owns a contiguous column range; pass 1 counts its nonzeros,
 // one block scan gives each wave its output offset, pass 2 writes (col, cnt) in column order.
 // Two barriers per row instead of two per 1024-column tile.
-__device__ inline uint32_t compact_row_ranges(uint32_t *row, int32_t M, int32_t *__restrict__ col_out,
+template <class Src>
+__device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_off, int32_t *__restrict__ col_out,
                                               uint32_t *__restrict__ cnt_out, int64_t out_base, uint64_t *sum,
                                               uint32_t *s_wave) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -229,7 +262,7 @@ __device__ inline uint32_t compact_row_ranges(uint32_t *row, int32_t M, int32_t 
     const uint64_t m = __ballot(v != 0u);
     if (v) {
       const int64_t pos = out_base + off + uint32_t(__popcll(m & lt_mask));
-      col_out[pos] = b;
+      col_out[pos] = col_off + b;
       cnt_out[pos] = v;
       row[b] = 0;
       my_sum += v;
@@ -239,85 +272,6 @@ __device__ inline uint32_t compact_row_ranges(uint32_t *row, int32_t M, int32_t 
   __syncthreads();
   *sum = my_sum;
   return tot;
-}
-
-// ---- 7. ★ the hot kernel --------------------------------------------------------------------------
-// Persistent: one 1024-thread workgroup per CU (the M-counter LDS row needs up to 159 KiB), chunks
-// dequeued heaviest-first from a device counter.  Waves take contributions round-robin; a
-// contribution's user list is streamed with coalesced 4 B loads (64 lanes, 4 loads in flight per
-// lane) and every partner id becomes one no-return ds_add_u32 on the row's counter.
-__global__ __launch_bounds__(kAccThreads) void k_accumulate(
-    const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
-    const uint32_t *__restrict__ cvals, const int64_t *__restrict__ aoff, const int32_t *__restrict__ alen,
-    const int32_t *__restrict__ aold, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
-    int32_t M, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, int32_t *__restrict__ col_out,
-    uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging, int64_t *__restrict__ rowsum,
-    int64_t *__restrict__ err) {
-  extern __shared__ uint32_t acc[];
-  __shared__ int32_t s_chunk;
-  __shared__ uint32_t s_self;
-  __shared__ uint32_t s_wave[kAccWaves];
-  __shared__ uint64_t s_red[kAccWaves];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t n_chunks = tot->n_chunks;
-  for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
-  for (;;) {
-    if (tid == 0) {
-      s_chunk = atomicAdd(queue, 1);
-      s_self = 0;
-    }
-    __syncthreads();
-    const int32_t ch = s_chunk;
-    if (ch >= n_chunks) break;
-    const Chunk c = chunks[ch];
-    uint32_t selfs = 0;
-    for (int64_t k = c.begin + wave; k < c.end; k += kAccWaves) {
-      const uint32_t v = cvals[k];
-      const uint32_t j = v >> 1;
-      const int32_t *h = arena + aoff[j];
-      const int32_t n = alen[j];
-      const int32_t start = (v & 1u) ? aold[j] : 0;
-      selfs += (v & 1u) ^ 1u;
-      for (int32_t i = start + lane; i < n; i += 256) {
-        const int32_t b0 = h[i];
-        const int32_t b1 = (i + 64 < n) ? h[i + 64] : -1;
-        const int32_t b2 = (i + 128 < n) ? h[i + 128] : -1;
-        const int32_t b3 = (i + 192 < n) ? h[i + 192] : -1;
-        atomicAdd(&acc[b0], 1u);
-        if (b1 >= 0) atomicAdd(&acc[b1], 1u);
-        if (b2 >= 0) atomicAdd(&acc[b2], 1u);
-        if (b3 >= 0) atomicAdd(&acc[b3], 1u);
-      }
-    }
-    if (lane == 0 && selfs) atomicAdd(&s_self, selfs);
-    __syncthreads();
-    const uint32_t self_total = s_self;
-    const int64_t chunk_rowsum = (epre[c.end] - epre[c.begin]) - int64_t(self_total);
-    if (tid == 0) {
-      acc[c.row] -= self_total;  // the -1 at x_p for every new position (p != q)
-      atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
-    }
-    __syncthreads();
-    if (c.split < 0) {
-      uint64_t sum;
-      const uint32_t nnz = compact_row(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
-      const uint64_t total = block_sum_u64(sum, s_red);
-      if (tid == 0) {
-        row_nnz[c.row] = int32_t(nnz);
-        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
-      }
-    } else {
-      uint32_t *srow = staging + int64_t(c.split) * M;
-      for (int32_t b = tid; b < M; b += kAccThreads) {
-        const uint32_t v = acc[b];
-        if (v) {
-          atomicAdd(srow + b, v);
-          acc[b] = 0;
-        }
-      }
-    }
-    __syncthreads();
-  }
 }
 
 // Segment start of every row-sorted contribution (arena offset of its first partner id), with
@@ -340,9 +294,9 @@ template <int U>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const int64_t *__restrict__ seg, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
-    int32_t M, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+    int32_t M, int32_t col_off, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
-    int64_t *__restrict__ rowsum, int64_t *__restrict__ err) {
+    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err) {
   extern __shared__ int64_t lds64[];
   int64_t *s_seg = lds64;                                            // [db] arena start - virtual start
   uint32_t *s_vst = reinterpret_cast<uint32_t *>(lds64 + db);        // [db + 1] virtual starts
@@ -413,24 +367,30 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
           for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? arena[a[k]] : -1;
 #pragma unroll
           for (int k = 0; k < U; k++)
-            if (it[k] >= 0) atomicAdd(&acc[it[k]], 1u);
+            if (it[k] >= 0) atomicAdd(&acc[it[k] - col_off], 1u);
         }
       }
       __syncthreads();
     }
-    const uint32_t self_total = s_self;
+    // the -1 at x_p for every new position applies to column x_p = row, in the tile that holds it
+    const bool own = c.row >= col_off && c.row < col_off + M;
+    const uint32_t self_total = own ? s_self : 0u;
     const int64_t chunk_rowsum = (epre[c.end] - epre[c.begin]) - int64_t(self_total);
     if (tid == 0) {
-      acc[c.row] -= self_total;
+      if (own) acc[c.row - col_off] -= self_total;
       atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
+      if (c.split >= 0)
+        atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
     }
     __syncthreads();
     if (c.split < 0) {
       uint64_t sum;
-      const uint32_t nnz = compact_row_ranges(acc, M, col_out, cnt_out, row_base[c.row], &sum, s_wave);
+      const int32_t filled = row_nnz[c.row];  // entries of earlier column tiles
+      const uint32_t nnz =
+          compact_row_ranges(acc, M, col_off, col_out, cnt_out, row_base[c.row] + filled, &sum, s_wave);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
-        row_nnz[c.row] = int32_t(nnz);
+        row_nnz[c.row] = filled + int32_t(nnz);
         if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       }
     } else {
@@ -449,21 +409,24 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
 
 // ---- 8. split rows: compact the staging rows ------------------------------------------------------
 __global__ __launch_bounds__(kAccThreads) void k_finalize_split(
-    const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M,
+    const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M, int32_t col_off,
     uint32_t *__restrict__ staging, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
-    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, const int64_t *__restrict__ rowsum,
+    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, int64_t *__restrict__ split_sum,
     int64_t *__restrict__ err) {
   __shared__ uint32_t s_wave[kAccWaves];
   __shared__ uint64_t s_red[kAccWaves];
   const int64_t n_split = tot->n_split;
   for (int64_t s = blockIdx.x; s < n_split; s += gridDim.x) {
     const int32_t a = split_row[s];
+    const int32_t filled = row_nnz[a];
     uint64_t sum;
-    const uint32_t nnz = compact_row(staging + s * M, M, col_out, cnt_out, row_base[a], &sum, s_wave);
+    const uint32_t nnz =
+        compact_row_ranges(staging + s * M, M, col_off, col_out, cnt_out, row_base[a] + filled, &sum, s_wave);
     const uint64_t total = block_sum_u64(sum, s_red);
     if (threadIdx.x == 0) {
-      row_nnz[a] = int32_t(nnz);
-      if (total != uint64_t(rowsum[a])) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+      row_nnz[a] = filled + int32_t(nnz);
+      if (total != uint64_t(split_sum[s])) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+      split_sum[s] = 0;
     }
   }
 }
@@ -547,28 +510,32 @@ Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr
 
 Status Counter::init(int32_t n_items) {
   if (n_items <= 0) return Status{1, "n_items must be positive"};
-  if (n_items > kMaxLdsCounters)
-    return Status{1, "n_items " + std::to_string(n_items) + " exceeds the single-tile LDS row (" +
-                         std::to_string(kMaxLdsCounters) + " items); column tiling is not built yet"};
   M_ = n_items;
+  // one LDS row over all items when it fits, else column tiles of <= kTileMax counters
+  if (n_items <= kMaxLdsCounters) {
+    T_ = 1;
+    tw_ = n_items;
+  } else {
+    T_ = (n_items + kTileMax - 1) / kTileMax;
+    tw_ = (n_items + T_ - 1) / T_;
+    if (T_ > 1024) return Status{1, "n_items too large (more than 1024 column tiles)"};
+  }
   COOC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_tot_), sizeof(PlanTotals), hipHostMallocDefault));
-  const size_t lds = size_t(M_) * 4;
-  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_accumulate),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-  // v2: descriptors share the LDS with the row; as many as fit, 64..1024
+  const size_t lds = size_t(tw_) * 4;
   db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
-  if (db_ < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
+  if (db_ < 32) return Status{1, "column tile too wide for the LDS row plus descriptors"};
   const size_t lds2 = size_t(db_) * 12 + 4 + lds;
   for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<4>),
                         reinterpret_cast<const void *>(k_accumulate2<8>),
                         reinterpret_cast<const void *>(k_accumulate2<16>),
                         reinterpret_cast<const void *>(k_accumulate2<32>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
-  const char *v = getenv("COOC_ACC_VARIANT");
-  variant_ = (v && v[0] == '1') ? 1 : 2;
   const char *u = getenv("COOC_ACC_UNROLL");
   unroll_ = u ? atoi(u) : 16;
   if (unroll_ != 4 && unroll_ != 8 && unroll_ != 32) unroll_ = 16;
+  int dev = 0;
+  COOC_HIP_TRY(hipGetDevice(&dev));
+  COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu_, hipDeviceAttributeMultiprocessorCount, dev));
   return Status::Ok();
 }
 
@@ -576,23 +543,94 @@ void Counter::release() {
   DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
-                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_};
+                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
+}
+
+// Plan, accumulate and compact one column tile [col_off, col_off + tw) given the per-contribution
+// work prefix (epre) and segment starts (seg) of that tile.
+Status Counter::run_tile(const int32_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer) {
+  const int32_t M = M_, tw = tw_;
+  int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
+  PlanTotals *tot = tot_.as<PlanTotals>();
+  uint64_t *okeys = order_keys_.as<uint64_t>();
+  int32_t *order = order_.as<int32_t>();
+  k_plan_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_work_.as<uint64_t>(), order + M,
+                                                 row_nch_.as<int32_t>(), row_split_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  size_t b = sort_tmp_.cap;
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint64_t>(), okeys,
+                                                            order + M, order, M, 0, 64, s));
+  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
+  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
+  b = sort_tmp_.cap;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
+                                                M, s));
+  b = sort_tmp_.cap;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
+                                                split_slot_.as<int32_t>() + 1, M, s));
+  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
+                                                  split_row_.as<int32_t>());
+  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>(), M, tot, queue_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+  const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
+  if (n_chunks == 0) return Status::Ok();
+  COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
+  COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
+  COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
+  if (n_split > 0) {
+    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(tw);
+    COOC_TRY(staging_.reserve(need));
+    COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
+  }
+  k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
+                                                   epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
+  COOC_HIP_TRY(hipGetLastError());
+  // ★ accumulate
+  const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
+  if (timer && timer->enabled && col_off == 0) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+  auto kern = unroll_ == 32 ? k_accumulate2<32>
+              : unroll_ == 8 ? k_accumulate2<8>
+              : unroll_ == 4 ? k_accumulate2<4> : k_accumulate2<16>;
+  kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(tw) * 4, s>>>(
+      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, tw, col_off, db_,
+      row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
+      staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
+      reinterpret_cast<int64_t *>(&tot->err));
+  COOC_HIP_TRY(hipGetLastError());
+  if (timer && timer->enabled && col_off + tw >= M) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+  if (n_split > 0) {
+    const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
+    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), tw, col_off,
+                                                          staging_.as<uint32_t>(), row_base_.as<int64_t>(),
+                                                          row_nnz_.as<int32_t>(), col_.as<int32_t>(),
+                                                          cnt_.as<uint32_t>(), split_sum_.as<int64_t>(),
+                                                          reinterpret_cast<int64_t *>(&tot->err));
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  return Status::Ok();
 }
 
 Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
   const int32_t M = M_;
   const int64_t n = au.n_contrib;
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
+  if (T_ > 1 && au.n_new != au.n_contrib)
+    return Status{1, "n_items > " + std::to_string(kMaxLdsCounters) +
+                         " (column tiling) is supported for one-window batches, not for streaming windows"};
   // ---- workspace
   COOC_TRY(keys_in_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n + 1)));
-  if (variant_ == 2) COOC_TRY(seg_.reserve(sizeof(int64_t) * (n + 1)));
+  COOC_TRY(seg_.reserve(sizeof(int64_t) * (n + 1)));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
   COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
   COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
@@ -628,121 +666,80 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
                                                                   reinterpret_cast<int64_t *>(&tot->err));
     COOC_HIP_TRY(hipGetLastError());
   }
-  // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152)
-  size_t tmp_bytes = 0;
+  // temp storage for every hipCUB call of the run
+  size_t tmp_bytes = 0, q = 0;
   const int nb = key_bits(M);
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
-  size_t scan_bytes = 0;
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
+  tmp_bytes = std::max(tmp_bytes, q);
   hipcub::TransformInputIterator<int64_t, WorkOp, const uint32_t *> work_it(vals, WorkOp{au.len, au.old});
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, work_it, epre + 1, int(n), s));
-  tmp_bytes = std::max(tmp_bytes, scan_bytes);
-  size_t sort2_bytes = 0;
-  uint64_t *okeys = order_keys_.as<uint64_t>();
-  int32_t *order = order_.as<int32_t>();
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort2_bytes, row_work_.as<uint64_t>(), okeys,
-                                                            order + M, order, M, 0, 64, s));
-  tmp_bytes = std::max(tmp_bytes, sort2_bytes);
-  size_t scan2_bytes = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan2_bytes, row_cap_.as<int64_t>(),
-                                                row_base_.as<int64_t>() + 1, M, s));
-  tmp_bytes = std::max(tmp_bytes, scan2_bytes);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, scan2_bytes, row_nch_.as<int32_t>(),
-                                                ord_cbase_.as<int32_t>() + 1, M, s));
-  tmp_bytes = std::max(tmp_bytes, scan2_bytes);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, work_it, epre + 1, int(n), s));
+  tmp_bytes = std::max(tmp_bytes, q);
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint64_t>(),
+                                                            order_keys_.as<uint64_t>(), order_.as<int32_t>() + M,
+                                                            order_.as<int32_t>(), M, 0, 64, s));
+  tmp_bytes = std::max(tmp_bytes, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_cap_.as<int64_t>(), row_base_.as<int64_t>() + 1, M, s));
+  tmp_bytes = std::max(tmp_bytes, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, M, s));
+  tmp_bytes = std::max(tmp_bytes, q);
   COOC_TRY(sort_tmp_.reserve(tmp_bytes));
 
+  // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152); 4. pair-work prefix
   if (n > 0) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
-    // 4. pair work prefix
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, work_it, epre + 1, int(n), s));
-    if (variant_ == 2) {
-      k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
-      COOC_HIP_TRY(hipGetLastError());
-    }
   }
-  // 3. row pointer
+  // 3. row pointer; output capacity per row from the whole row's work (all column tiles)
   k_row_ptr<<<blocks_for(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
-  // 5. per-row plan
-  k_plan_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_work_.as<uint64_t>(), order + M,
-                                                 row_nch_.as<int32_t>(), row_cap_.as<int64_t>(),
-                                                 row_split_.as<int32_t>());
-  COOC_HIP_TRY(hipGetLastError());
-  {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint64_t>(), okeys,
-                                                              order + M, order, M, 0, 64, s));
-  }
-  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
-  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
+  k_row_cap<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_cap_.as<int64_t>());
   COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
   {
     size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(),
-                                                  ord_cbase_.as<int32_t>() + 1, M, s));
-    b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_cap_.as<int64_t>(),
                                                   row_base_.as<int64_t>() + 1, M, s));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
-                                                  split_slot_.as<int32_t>() + 1, M, s));
   }
-  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
-                                                  split_row_.as<int32_t>());
-  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), row_base_.as<int64_t>(), split_slot_.as<int32_t>(), epre, M, n,
-                           tot, queue_.as<int32_t>());
+  k_cap_total<<<1, 1, 0, s>>>(row_base_.as<int64_t>(), epre, M, n, tot);
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
-
-  // ---- output + chunk buffers sized by the plan
-  const int64_t n_chunks = h_tot_->n_chunks, cap = h_tot_->cap_total, n_split = h_tot_->n_split;
-  COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
+  const int64_t cap = h_tot_->cap_total, work_total = h_tot_->work_total;
   COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
   COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
-  if (n_split > 0) {
-    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
-    COOC_TRY(staging_.reserve(need));
-    COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
-  }
-  k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
-                                                   epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
-  COOC_HIP_TRY(hipGetLastError());
 
-  // 7. ★ accumulate
-  int dev = 0, n_cu = 256;
-  COOC_HIP_TRY(hipGetDevice(&dev));
-  COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  const int64_t grid = std::min<int64_t>(n_chunks, n_cu);
-  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  if (grid > 0 && variant_ == 1) {
-    k_accumulate<<<unsigned(grid), kAccThreads, size_t(M) * 4, s>>>(
-        chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), vals, au.off, au.len, au.old, au.arena, epre, M,
-        row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
-        staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
-    COOC_HIP_TRY(hipGetLastError());
-  } else if (grid > 0) {
-    auto kern = unroll_ == 32 ? k_accumulate2<32>
-                : unroll_ == 8 ? k_accumulate2<8>
-                : unroll_ == 4 ? k_accumulate2<4> : k_accumulate2<16>;
-    kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
-        chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), au.arena, epre, M, db_,
-        row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
-        staging_.as<uint32_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
-    COOC_HIP_TRY(hipGetLastError());
-  }
-  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
-  // 8. split rows
-  if (n_split > 0) {
-    const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu));
-    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), M, staging_.as<uint32_t>(),
-                                                          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-                                                          col_.as<int32_t>(), cnt_.as<uint32_t>(),
-                                                          rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
-    COOC_HIP_TRY(hipGetLastError());
+  if (T_ == 1) {
+    if (n > 0) {
+      k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
+      COOC_HIP_TRY(hipGetLastError());
+    }
+    COOC_TRY(run_tile(au.arena, 0, n, s, timer));
+  } else {
+    // column tiles: each user's history regrouped by tile once, then one pass per tile
+    COOC_TRY(tarena_.reserve(sizeof(int32_t) * (n + 1)));
+    COOC_TRY(tb_.reserve(sizeof(int32_t) * size_t(au.n_active + 1) * size_t(T_ + 1)));
+    if (au.n_active > 0) {
+      const int64_t waves = std::min<int64_t>(au.n_active, 65536);
+      k_tile_partition<<<blocks_for(waves * 64, 256), 256, sizeof(int32_t) * 4 * (T_ + 1), s>>>(
+          au.n_active, au.off, au.len, au.arena, tw_, T_, tarena_.as<int32_t>(), tb_.as<int32_t>());
+      COOC_HIP_TRY(hipGetLastError());
+    }
+    for (int32_t t = 0; t < T_; t++) {
+      if (n > 0) {
+        hipcub::TransformInputIterator<int64_t, TileWorkOp, const uint32_t *> tw_it(
+            vals, TileWorkOp{tb_.as<int32_t>(), T_, t});
+        size_t b = 0;
+        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, tw_it, epre + 1, int(n), s));
+        COOC_TRY(sort_tmp_.reserve(b));
+        b = sort_tmp_.cap;
+        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, tw_it, epre + 1, int(n), s));
+        k_seg_start_tile<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, tb_.as<int32_t>(), T_, t,
+                                                            seg_.as<int64_t>());
+        COOC_HIP_TRY(hipGetLastError());
+      }
+      COOC_TRY(run_tile(tarena_.as<int32_t>(), t * tw_, n, s, timer));
+    }
   }
   k_nnz_total<<<1, 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
   COOC_HIP_TRY(hipGetLastError());
@@ -752,9 +749,9 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   out->col = col_.as<int32_t>();
   out->cnt = cnt_.as<uint32_t>();
   out->rowsum = rowsum_.as<int64_t>();
-  out->work = h_tot_->work_total;
-  out->observed = h_tot_->work_total - au.n_new;
-  out->nnz = -1;  // known after the stream drains: Counter::totals().nnz_total
+  out->work = work_total;
+  out->observed = work_total - au.n_new;
+  out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
   return Status::Ok();
 }
 

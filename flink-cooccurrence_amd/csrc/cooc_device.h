@@ -122,16 +122,20 @@ class Counter {
   int32_t n_items() const { return M_; }
 
  private:
+  Status run_tile(const int32_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
+
   int32_t M_ = 0;
-  int db_ = 0;       // segment descriptors staged per batch (accumulate v2)
-  int variant_ = 2;  // COOC_ACC_VARIANT=1 selects the per-contribution wave kernel (A/B)
+  int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)
+  int32_t tw_ = 0;   // column tile width
+  int db_ = 0;       // segment descriptors staged per batch
   int unroll_ = 16;  // COOC_ACC_UNROLL: partner loads in flight per lane (4, 8, 16, 32)
+  int n_cu_ = 256;
   // workspace
   DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
   DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
-  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_;
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_, tb_;
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

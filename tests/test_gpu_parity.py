@@ -332,3 +332,23 @@ def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts):
             assert msum[r] == rowsums[a]
     for c in cores:
         c.close()
+
+
+@pytest.mark.parametrize("M,U,mean,s", [(40705, 400, 80.0, 1.0), (70_000, 2000, 60.0, 0.8), (200_000, 3000, 120.0, 1.0)])
+def test_batch_column_tiled(pkg, oracle, torch_cuda, M, U, mean, s):
+    """n_items beyond one LDS row: column tiles of <= 32K counters, rows appended tile by tile."""
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(41, U, M, mean, s=s)
+    got = _batch_vs_closed_form(pkg, oracle, up, it, M)
+    assert got.cols.max() >= 32768  # entries beyond the first tile exist
+
+
+def test_batch_column_tiled_split_rows(pkg, oracle, torch_cuda):
+    """Column tiles with heavy rows split over chunks in every tile."""
+    rng = np.random.default_rng(5)
+    U, L, M = 2600, 1700, 100_000
+    it = np.concatenate([np.concatenate([[0, 99_999], rng.choice(np.arange(1, M - 1), L - 2, replace=False)])
+                         for _ in range(U)]).astype(np.int32)
+    up = (np.arange(U + 1) * L).astype(np.int64)
+    _batch_vs_closed_form(pkg, oracle, up, it, M)
