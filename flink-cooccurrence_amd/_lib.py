@@ -75,6 +75,8 @@ _SIGS = {
                                          ctypes.POINTER(CoocDeviceResult)]),
     "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
+    "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
+    "cooc_copy_topk_batch": (ctypes.c_int, [vp, i32p, i32p, f64p]),
     "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),
     "cooc_finish_window": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_window_delta": (ctypes.c_int, [vp, i32p, i64p, i32p, u32p, i16p]),

@@ -130,6 +130,18 @@ class CooccurrenceCore:
                                           _p(rs, i64p), _p(rs32, i32p)), self._h)
         return BatchResult(rp, cols, cnt, cnt16, rs, rs32, int(observed))
 
+    def topk_batch(self, topk: int, exact_scores: bool = False, stream=None):
+        """LLR top-k of every row of the last batch -> (sizes [M], values [M, k], scores [M, k])."""
+        L = _lib.load()
+        check(L.cooc_topk_batch(self._h, topk, _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0,
+                                None if stream is None else ctypes.c_void_p(int(stream))), self._h)
+        M = self.n_items
+        sizes = np.zeros(M, np.int32)
+        vals = np.zeros((M, topk), np.int32)
+        scores = np.zeros((M, topk), np.float64)
+        check(L.cooc_copy_topk_batch(self._h, _p(sizes, i32p), _p(vals, i32p), _p(scores, f64p)), self._h)
+        return sizes, vals, scores
+
     # ---- sharding layer (owner-partitioned exchange of partial rows) -----------------------------
     def partition_plan(self, n_parts: int) -> np.ndarray:
         out = np.zeros(n_parts, np.int64)

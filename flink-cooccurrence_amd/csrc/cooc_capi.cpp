@@ -81,6 +81,18 @@ int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cn
   return s.ok() ? COOC_OK : fail(ctx, s);
 }
 
+int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->topk_batch(topk, flags, hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->batch_stream);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores) {
+  if (!ctx) return COOC_ERR_ARG;
+  Status s = ctx->copy_topk_batch(sizes, values, scores);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
 int cooc_submit_batch(cooc_ctx *ctx, int64_t window_ts, int32_t n_users, const int32_t *user_ids,
                       const int64_t *user_ptr, const int32_t *items) {
   if (!ctx) return COOC_ERR_ARG;

@@ -769,11 +769,12 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
   COOC_TRY(pk_col_.reserve(sizeof(int32_t) * (nnz + 1)));
   COOC_TRY(pk_cnt_.reserve(sizeof(uint32_t) * (nnz + 1)));
   size_t b = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, row_nnz_.as<int32_t>(), pk_row_ptr_.as<int64_t>() + 1, M, s));
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> nnz64(row_nnz_.as<int32_t>(), WidenI64{});
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, nnz64, pk_row_ptr_.as<int64_t>() + 1, M, s));
   COOC_TRY(sort_tmp_.reserve(b));
   b = sort_tmp_.cap;
   COOC_HIP_TRY(hipMemsetAsync(pk_row_ptr_.p, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_nnz_.as<int32_t>(), pk_row_ptr_.as<int64_t>() + 1,
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, nnz64, pk_row_ptr_.as<int64_t>() + 1,
                                                 M, s));
   k_pack<<<blocks_for(int64_t(M) * 64, 256) < 8192 ? blocks_for(int64_t(M) * 64, 256) : 8192, 256, 0, s>>>(
       row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(), M,

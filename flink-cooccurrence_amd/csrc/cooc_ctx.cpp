@@ -1,5 +1,6 @@
 // cooc_ctx.cpp — context lifecycle and the stateless one-window batch entry points.
 #include "cooc_ctx.h"
+#include "cooc_stream_kernels.h"
 
 #include <algorithm>
 #include <cstring>
@@ -39,7 +40,7 @@ cooc_ctx::~cooc_ctx() {
   stream_state.release();
   sharder.release();
   counter.release();
-  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old};
+  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
   if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);
@@ -50,6 +51,7 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
                               int64_t n_interactions, hipStream_t s, cooc_device_result *out) {
   COOC_HIP_TRY(hipSetDevice(device));
   have_batch = false;
+  batch_topk = 0;
   const int64_t n_act = std::max<int64_t>(n_users, 1);
   COOC_TRY(b_off.reserve(sizeof(int64_t) * n_act));
   COOC_TRY(b_len.reserve(sizeof(int32_t) * n_act));
@@ -147,5 +149,34 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
     if (rowsum32)  // Java int accumulation (RowSumAggregator.java:25-27, Int2IntOpenHashMap.addTo)
       for (int32_t a = 0; a < M; a++) rowsum32[a] = int32_t(uint32_t(uint64_t(tmp[a])));
   }
+  return Status::Ok();
+}
+
+Status cooc_ctx::topk_batch(int32_t topk, int32_t flags, hipStream_t s) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  if (topk <= 0) return Status{COOC_ERR_ARG, std::to_string(topk) + " is <= 0"};  // ItemRowRescorer...java:52-54
+  COOC_HIP_TRY(hipSetDevice(device));
+  const int32_t M = cfg.n_items;
+  COOC_TRY(b_tk_size.reserve(sizeof(int32_t) * M));
+  COOC_TRY(b_tk_val.reserve(sizeof(int32_t) * size_t(M) * topk));
+  COOC_TRY(b_tk_score.reserve(sizeof(double) * size_t(M) * topk));
+  COOC_TRY(b_obs3.reserve(sizeof(int64_t) * 4));
+  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  const cooc::CountResult &r = batch_result;
+  COOC_TRY(cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum,
+                                      (flags & COOC_FLAG_EXACT_SCORES) != 0, topk, b_obs3.as<int64_t>(),
+                                      b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(), b_tk_score.as<double>()));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  batch_topk = topk;
+  return Status::Ok();
+}
+
+Status cooc_ctx::copy_topk_batch(int32_t *sizes, int32_t *values, double *scores) {
+  if (batch_topk <= 0) return Status{COOC_ERR_STATE, "cooc_topk_batch has not run"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  const size_t M = size_t(cfg.n_items), k = size_t(batch_topk);
+  if (sizes) COOC_HIP_TRY(hipMemcpy(sizes, b_tk_size.p, sizeof(int32_t) * M, hipMemcpyDeviceToHost));
+  if (values) COOC_HIP_TRY(hipMemcpy(values, b_tk_val.p, sizeof(int32_t) * M * k, hipMemcpyDeviceToHost));
+  if (scores) COOC_HIP_TRY(hipMemcpy(scores, b_tk_score.p, sizeof(double) * M * k, hipMemcpyDeviceToHost));
   return Status::Ok();
 }

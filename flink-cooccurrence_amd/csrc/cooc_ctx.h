@@ -95,6 +95,8 @@ struct cooc_ctx {
   cooc::Status count_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_window_info *info);
   cooc::Status copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                           int32_t *rowsum32);
+  cooc::Status topk_batch(int32_t topk, int32_t flags, hipStream_t s);
+  cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
 
   static std::string &create_error();
 
@@ -110,7 +112,8 @@ struct cooc_ctx {
   cooc::Operator op;
 
   // stateless batch buffers
-  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old;
+  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3;
+  int32_t batch_topk = 0;
   bool have_batch = false;
   int64_t batch_observed = 0;
   int64_t batch_nnz = 0;

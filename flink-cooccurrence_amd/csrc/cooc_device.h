@@ -38,6 +38,12 @@ struct Status {
     if (!s_.ok()) return s_;      \
   } while (0)
 
+// int32 -> int64 widening for prefix sums whose totals may exceed 2^31 (hipCUB accumulates in the
+// input value type).
+struct WidenI64 {
+  __host__ __device__ int64_t operator()(int32_t v) const { return int64_t(v); }
+};
+
 // Grow-only device buffer (the workspace of one context).  Never shrinks, so steady-state
 // windows perform no hipMalloc.
 struct DevBuf {

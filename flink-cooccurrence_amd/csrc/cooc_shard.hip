@@ -147,10 +147,11 @@ Status Sharder::plan(const CountResult &r, int32_t M, int32_t n_parts, hipStream
                                                    part_entries_.as<int64_t>());
   COOC_HIP_TRY(hipGetLastError());
   size_t b = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b, perm_nnz_.as<int32_t>(), perm_off_.as<int64_t>(), M, s));
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> nnz64(perm_nnz_.as<int32_t>(), WidenI64{});
+  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b, nnz64, perm_off_.as<int64_t>(), M, s));
   COOC_TRY(tmp_.reserve(b));
   b = tmp_.cap;
-  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp_.p, b, perm_nnz_.as<int32_t>(), perm_off_.as<int64_t>(), M, s));
+  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp_.p, b, nnz64, perm_off_.as<int64_t>(), M, s));
   COOC_HIP_TRY(hipMemcpyAsync(h_entries, part_entries_.p, sizeof(int64_t) * n_parts, hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   planned_parts_ = n_parts;
@@ -183,12 +184,13 @@ Status Sharder::merge(int32_t M, int32_t n_parts, int32_t part, const int32_t *d
   COOC_TRY(err_.reserve(sizeof(int64_t) * 2));
   COOC_HIP_TRY(hipMemsetAsync(err_.p, 0, sizeof(int64_t) * 2, s));
   size_t b1 = 0, b2 = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, d_recv_nnz, recv_off_.as<int64_t>(), int(K), s));
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> recv64(d_recv_nnz, WidenI64{});
+  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, recv64, recv_off_.as<int64_t>(), int(K), s));
   COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, cap_.as<int64_t>(), row_base_.as<int64_t>(), R + 1, s));
   COOC_TRY(tmp_.reserve(std::max(b1, b2)));
   if (K > 0) {
     size_t b = tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp_.p, b, d_recv_nnz, recv_off_.as<int64_t>(), int(K), s));
+    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp_.p, b, recv64, recv_off_.as<int64_t>(), int(K), s));
   }
   COOC_HIP_TRY(hipMemsetAsync(cap_.as<int64_t>() + R, 0, sizeof(int64_t), s));
   if (R > 0) k_merge_plan<<<blocks_for(R, 256), 256, 0, s>>>(d_recv_nnz, n_parts, R, M, cap_.as<int64_t>());

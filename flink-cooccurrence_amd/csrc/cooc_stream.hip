@@ -121,28 +121,57 @@ __device__ inline void heap_update(int32_t *hv, double *hs, int32_t size, int32_
   hs[i] = score;
 }
 
-// One wave per touched row; the wave scores 64 consecutive columns at a time (ascending column =
+// Row sources for the rescoring kernel: a dense global row (streaming state) or a padded CSR row
+// (a batch result).  Both are iterated in ascending column order (the tie contract).
+struct DenseRows {
+  const uint32_t *G;
+  int32_t M;
+  __device__ int64_t size(int32_t) const { return M; }
+  __device__ void get(int32_t a, int64_t i, int32_t &c, uint32_t &v) const {
+    c = int32_t(i);
+    v = G[int64_t(a) * M + i];
+  }
+};
+
+struct CsrRows {
+  const int64_t *row_base;
+  const int32_t *row_nnz;
+  const int32_t *col;
+  const uint32_t *cnt;
+  __device__ int64_t size(int32_t a) const { return row_nnz[a]; }
+  __device__ void get(int32_t a, int64_t i, int32_t &c, uint32_t &v) const {
+    const int64_t k = row_base[a] + i;
+    c = col[k];
+    v = cnt[k];
+  }
+};
+
+// One wave per rescored row; the wave scores 64 consecutive entries at a time (ascending column =
 // the iteration order contract) and feeds the lanes that can enter the heap to it in lane order,
 // which is exactly the sequential loop of ItemRowRescorer...java:199-223.
-__global__ void k_rescore(const int32_t *__restrict__ touched, const int64_t *__restrict__ scal, int32_t M,
-                          const uint32_t *__restrict__ G, const int64_t *__restrict__ grs, int32_t exact,
+// rows == nullptr: rescored row t is item t.  obs[0] = the rescorer's observed (sum of int
+// deltas), obs[1] = the exact pair count.
+template <class Rows>
+__global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__restrict__ n_rows_p, Rows src,
+                          const int64_t *__restrict__ grs, const int64_t *__restrict__ obs, int32_t exact,
                           int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
                           double *__restrict__ out_score) {
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + int64_t(waves) * (topk + 1)) + int64_t(wave) * (topk + 1);
-  const int64_t n_touched = scal[0];
-  const int64_t observed = exact ? scal[3] : scal[2];
-  for (int64_t t = int64_t(blockIdx.x) * waves + wave; t < n_touched; t += int64_t(gridDim.x) * waves) {
-    const int32_t a = touched[t];
+  const int64_t n_rows = n_rows_p[0];
+  const int64_t observed = exact ? obs[1] : obs[0];
+  for (int64_t t = int64_t(blockIdx.x) * waves + wave; t < n_rows; t += int64_t(gridDim.x) * waves) {
+    const int32_t a = rows ? rows[t] : int32_t(t);
     const int64_t rs_a = exact ? grs[a] : int64_t(int32_t(uint32_t(uint64_t(grs[a]))));
-    const uint32_t *g = G + int64_t(a) * M;
+    const int64_t n = src.size(a);
     int32_t size = 0;
     double least = 0.0;
-    for (int32_t c0 = 0; c0 < M; c0 += 64) {
-      const int32_t c = c0 + lane;
-      const uint32_t v = c < M ? g[c] : 0u;
+    for (int64_t i0 = 0; i0 < n; i0 += 64) {
+      int32_t c = 0;
+      uint32_t v = 0u;
+      if (i0 + lane < n) src.get(a, i0 + lane, c, v);
       double score = 0.0;
       if (v != 0u) {
         // ItemRowRescorer...java:203-205,230-240
@@ -158,10 +187,11 @@ __global__ void k_rescore(const int32_t *__restrict__ touched, const int64_t *__
         const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
         m &= m - 1;
         const double sc = __shfl(score, l, 64);
+        const int32_t cl = __shfl(c, l, 64);
         if (size < topk) {
-          heap_add(hv, hs, size, c0 + l, sc);
+          heap_add(hv, hs, size, cl, sc);
         } else if (sc > hs[1]) {
-          heap_update(hv, hs, size, c0 + l, sc);
+          heap_update(hv, hs, size, cl, sc);
         }
         least = hs[1];
       }
@@ -171,6 +201,32 @@ __global__ void k_rescore(const int32_t *__restrict__ touched, const int64_t *__
       out_val[t * topk + i] = hv[i + 1];
       out_score[t * topk + i] = hs[i + 1];
     }
+  }
+}
+
+// The rescorer's observed total after one window from an empty state: sum of the int views of the
+// row-sum updates (ItemRowRescorer...java:154), and the exact total.
+__global__ void k_observed(const int64_t *__restrict__ rowsum, int32_t M, int64_t *__restrict__ out3) {
+  __shared__ int64_t sr[256], se[256];
+  int64_t r = 0, e = 0;
+  for (int32_t a = threadIdx.x; a < M; a += 256) {
+    r += int64_t(int32_t(uint32_t(uint64_t(rowsum[a]))));
+    e += rowsum[a];
+  }
+  sr[threadIdx.x] = r;
+  se[threadIdx.x] = e;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sr[threadIdx.x] += sr[threadIdx.x + o];
+      se[threadIdx.x] += se[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out3[0] = sr[0];
+    out3[1] = se[0];
+    out3[2] = M;
   }
 }
 
@@ -217,23 +273,43 @@ size_t rescore_lds_bytes(int32_t topk) {
   return size_t(rescore_waves_per_block(topk)) * size_t(topk + 1) * (sizeof(double) + sizeof(int32_t));
 }
 
-Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
-                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
-                      int32_t *out_val, double *out_score) {
+template <class Rows>
+Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_rows_dev, int64_t max_rows, Rows src,
+                           const int64_t *grs, const int64_t *obs, bool exact, int32_t topk, int32_t *out_size,
+                           int32_t *out_val, double *out_score) {
   const int waves = rescore_waves_per_block(topk);
   const size_t lds = rescore_lds_bytes(topk);
+  if (lds > 160 * 1024 - 256) return Status{1, "topk too large for the LDS heaps"};
   if (lds > 64 * 1024)
-    COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore),
+    COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore<Rows>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   int dev = 0, n_cu = 256;
   COOC_HIP_TRY(hipGetDevice(&dev));
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  const int64_t want = (int64_t(max_rows) + waves - 1) / waves;
+  const int64_t want = (max_rows + waves - 1) / waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
-  k_rescore<<<grid, 64 * waves, lds, s>>>(touched, scal, M, G, grs, exact ? 1 : 0, topk, out_size, out_val,
-                                         out_score);
+  k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, obs, exact ? 1 : 0, topk, out_size,
+                                                 out_val, out_score);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
+}
+
+Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
+                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
+                      int32_t *out_val, double *out_score) {
+  // scal: [0] touched rows, [2] rescorer observed, [3] exact observed
+  return launch_rescore_rows(s, touched, scal, max_rows, DenseRows{G, M}, grs, scal + 2, exact, topk, out_size,
+                             out_val, out_score);
+}
+
+Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
+                            const int32_t *col, const uint32_t *cnt, const int64_t *rowsum, bool exact, int32_t topk,
+                            int64_t *obs3, int32_t *out_size, int32_t *out_val, double *out_score) {
+  k_observed<<<1, 256, 0, s>>>(rowsum, M, obs3);
+  COOC_HIP_TRY(hipGetLastError());
+  // obs3: [0] rescorer observed, [1] exact, [2] n_rows (= M)
+  return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, rowsum, obs3, exact,
+                             topk, out_size, out_val, out_score);
 }
 
 }  // namespace cooc

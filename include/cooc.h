@@ -124,6 +124,15 @@ COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user
 COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                     int32_t *rowsum32);
 
+/* LLR top-k of every row of the last cooc_count_device / cooc_count_host result: what
+ * ItemRowRescorer...java:195-241 emits after that one window from an empty state (rows iterated in
+ * ascending column order, LogLikelihood.java:41-57 scores, IntDoublePriorityQueue layout).  flags:
+ * COOC_FLAG_EXACT_SCORES to score exact counts instead of the reference's wrapped int16/int32.
+ * cooc_copy_topk_batch: sizes int32[n_items], values int32[n_items*topk], scores double[n_items*topk]
+ * (heap positions 1..size, least score first; rows without entries have size 0). */
+COOC_API int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream);
+COOC_API int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores);
+
 /* ---- streaming (resident per-user histories, global rows, row sums) ------------------------
  * cooc_submit_batch stages the interactions of one tumbling window: n_users users with their
  * new items in arrival order (user_ptr int64[n_users+1] into items).  Several submits to the same

