@@ -214,9 +214,26 @@ __global__ void k_make_chunks(const int32_t *__restrict__ order, const int32_t *
   int64_t b = c0;
   for (int32_t j = 0; j < nch; j++) {
     const int64_t e = (j == nch - 1) ? c1 : c0 + lower_bound_i64<int64_t>(epre + c0, c1 - c0, w0 + (j + 1) * kChunkWork);
-    chunks[ord_cbase[r] + j] = Chunk{a, slot, b, e, 0};
+    chunks[ord_cbase[r] + j] = Chunk{a, slot, b, e, (int64_t(j) << 32) | int64_t(r)};
     b = e;
   }
+}
+
+// Chunk queue order: j-major (every row's j-th chunk together, heaviest rows first within a j), so
+// that the workgroups running at the same time sweep the same users (contributions are in user
+// order inside a row) and share those users' lists in L2.
+__global__ void k_chunk_keys(const Chunk *__restrict__ chunks, int64_t n, uint64_t *__restrict__ keys,
+                             int32_t *__restrict__ idx) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = uint64_t(chunks[i].pad);
+  idx[i] = int32_t(i);
+}
+
+__global__ void k_chunk_gather(const Chunk *__restrict__ src, const int32_t *__restrict__ idx, int64_t n,
+                               Chunk *__restrict__ dst) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
 }
 
 // Block-wide sum of a uint64 (kAccThreads threads).
@@ -530,6 +547,8 @@ Status Counter::init(int32_t n_items) {
                         reinterpret_cast<const void *>(k_accumulate2<16>),
                         reinterpret_cast<const void *>(k_accumulate2<32>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  const char *co = getenv("COOC_CHUNK_ORDER");
+  chunk_order_ = co ? atoi(co) : 0;
   const char *u = getenv("COOC_ACC_UNROLL");
   unroll_ = u ? atoi(u) : 16;
   if (unroll_ != 4 && unroll_ != 8 && unroll_ != 32) unroll_ = 16;
@@ -543,7 +562,7 @@ void Counter::release() {
   DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
-                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_};
+                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
@@ -592,6 +611,23 @@ Status Counter::run_tile(const int32_t *arena, int32_t col_off, int64_t n, hipSt
   k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
                                                    epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
   COOC_HIP_TRY(hipGetLastError());
+  if (chunk_order_ == 1 && n_split > 0) {
+    COOC_TRY(chunks2_.reserve(sizeof(Chunk) * (n_chunks + 1)));
+    COOC_TRY(ckeys_.reserve(sizeof(uint64_t) * 2 * (n_chunks + 1)));
+    COOC_TRY(cidx_.reserve(sizeof(int32_t) * 2 * (n_chunks + 1)));
+    uint64_t *k_in = ckeys_.as<uint64_t>(), *k_out = k_in + n_chunks + 1;
+    int32_t *i_in = cidx_.as<int32_t>(), *i_out = i_in + n_chunks + 1;
+    k_chunk_keys<<<blocks_for(n_chunks, 256), 256, 0, s>>>(chunks_.as<Chunk>(), n_chunks, k_in, i_in);
+    size_t q = 0;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, k_in, k_out, i_in, i_out, int(n_chunks), 0, 64, s));
+    COOC_TRY(sort_tmp_.reserve(q));
+    q = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, q, k_in, k_out, i_in, i_out, int(n_chunks), 0, 64, s));
+    k_chunk_gather<<<blocks_for(n_chunks, 256), 256, 0, s>>>(chunks_.as<Chunk>(), i_out, n_chunks,
+                                                             chunks2_.as<Chunk>());
+    COOC_HIP_TRY(hipGetLastError());
+    std::swap(chunks_, chunks2_);
+  }
   // ★ accumulate
   const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
   if (timer && timer->enabled && col_off == 0) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));

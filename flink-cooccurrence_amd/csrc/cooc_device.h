@@ -141,7 +141,8 @@ class Counter {
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
   DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
-  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_, tb_;
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_, tb_, chunks2_, ckeys_, cidx_;
+  int chunk_order_ = 0;  // COOC_CHUNK_ORDER=1: j-major chunk queue (A/B)
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 
