@@ -147,7 +147,7 @@ __device__ inline void wave_sync() {  // LDS visibility among the lanes of one w
 __global__ __launch_bounds__(256) void k_tile_partition(int64_t n_users, const int64_t *__restrict__ off,
                                                         const int32_t *__restrict__ len,
                                                         const int32_t *__restrict__ arena, int32_t tw, int32_t T,
-                                                        int32_t *__restrict__ tarena, int32_t *__restrict__ tb) {
+                                                        uint16_t *__restrict__ tarena, int32_t *__restrict__ tb) {
   extern __shared__ int32_t cur[];  // [4 waves][T + 1]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int32_t *c = cur + wave * (T + 1);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_tile_partition(int64_t n_users, const i
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   for (int64_t j = gw; j < n_users; j += n_waves) {
     const int32_t *h = arena + off[j];
-    int32_t *o = tarena + off[j];
+    uint16_t *o = tarena + off[j];
     const int32_t n = len[j];
     for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
     wave_sync();
@@ -174,9 +174,21 @@ __global__ __launch_bounds__(256) void k_tile_partition(int64_t n_users, const i
     wave_sync();
     for (int32_t p = lane; p < n; p += 64) {
       const int32_t it = h[p];
-      o[atomicAdd(&c[it / tw], 1)] = it;
+      const int32_t t = it / tw;
+      o[atomicAdd(&c[t], 1)] = uint16_t(it - t * tw);  // tile-relative id (< 32768)
     }
     wave_sync();
+  }
+}
+
+// The one-tile path reads partner ids as u16 (n_items <= 40,704): half the bytes per pair.
+__global__ void k_narrow(const int32_t *__restrict__ src, int64_t n, uint16_t *__restrict__ dst) {
+  const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const int4 v = *reinterpret_cast<const int4 *>(src + i);
+    *reinterpret_cast<ushort4 *>(dst + i) = make_ushort4(uint16_t(v.x), uint16_t(v.y), uint16_t(v.z), uint16_t(v.w));
+  } else {
+    for (int64_t k = i; k < n; k++) dst[k] = uint16_t(src[k]);
   }
 }
 
@@ -310,7 +322,7 @@ __global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const
 template <int U>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
-    const int64_t *__restrict__ seg, const int32_t *__restrict__ arena, const int64_t *__restrict__ epre,
+    const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
     int32_t M, int32_t col_off, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
     int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err) {
@@ -379,12 +391,12 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
               a[k] = base + vk;
             }
           }
-          int32_t it[U];
+          uint32_t it[U];
 #pragma unroll
-          for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? arena[a[k]] : -1;
+          for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? uint32_t(arena[a[k]]) : 0xFFFFFFFFu;
 #pragma unroll
           for (int k = 0; k < U; k++)
-            if (it[k] >= 0) atomicAdd(&acc[it[k] - col_off], 1u);
+            if (it[k] != 0xFFFFFFFFu) atomicAdd(&acc[it[k]], 1u);
         }
       }
       __syncthreads();
@@ -570,7 +582,7 @@ void Counter::release() {
 
 // Plan, accumulate and compact one column tile [col_off, col_off + tw) given the per-contribution
 // work prefix (epre) and segment starts (seg) of that tile.
-Status Counter::run_tile(const int32_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer) {
+Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer) {
   const int32_t M = M_, tw = tw_;
   int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
   PlanTotals *tot = tot_.as<PlanTotals>();
@@ -750,15 +762,25 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
       k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
       COOC_HIP_TRY(hipGetLastError());
     }
-    COOC_TRY(run_tile(au.arena, 0, n, s, timer));
+    const uint16_t *a16 = au.arena16;
+    if (!a16) {  // narrow the arena range the contributions reference
+      const int64_t span = au.arena_span;
+      COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (span + 8)));
+      if (span > 0) {
+        k_narrow<<<blocks_for((span + 3) / 4, 256), 256, 0, s>>>(au.arena, span, tarena_.as<uint16_t>());
+        COOC_HIP_TRY(hipGetLastError());
+      }
+      a16 = tarena_.as<uint16_t>();
+    }
+    COOC_TRY(run_tile(a16, 0, n, s, timer));
   } else {
     // column tiles: each user's history regrouped by tile once, then one pass per tile
-    COOC_TRY(tarena_.reserve(sizeof(int32_t) * (n + 1)));
+    COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (n + 8)));
     COOC_TRY(tb_.reserve(sizeof(int32_t) * size_t(au.n_active + 1) * size_t(T_ + 1)));
     if (au.n_active > 0) {
       const int64_t waves = std::min<int64_t>(au.n_active, 65536);
       k_tile_partition<<<blocks_for(waves * 64, 256), 256, sizeof(int32_t) * 4 * (T_ + 1), s>>>(
-          au.n_active, au.off, au.len, au.arena, tw_, T_, tarena_.as<int32_t>(), tb_.as<int32_t>());
+          au.n_active, au.off, au.len, au.arena, tw_, T_, tarena_.as<uint16_t>(), tb_.as<int32_t>());
       COOC_HIP_TRY(hipGetLastError());
     }
     for (int32_t t = 0; t < T_; t++) {
@@ -774,7 +796,7 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
                                                             seg_.as<int64_t>());
         COOC_HIP_TRY(hipGetLastError());
       }
-      COOC_TRY(run_tile(tarena_.as<int32_t>(), t * tw_, n, s, timer));
+      COOC_TRY(run_tile(tarena_.as<uint16_t>(), t * tw_, n, s, timer));
     }
   }
   k_nnz_total<<<1, 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);

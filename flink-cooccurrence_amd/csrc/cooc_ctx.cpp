@@ -67,6 +67,7 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   au.n_contrib = n_interactions;
   au.n_new = n_interactions;
   au.arena = d_items;
+  au.arena_span = n_interactions;
   cooc::CountResult r;
   COOC_TRY(counter.run(au, s, &r, timer.enabled ? &timer : nullptr));
   COOC_HIP_TRY(hipStreamSynchronize(s));

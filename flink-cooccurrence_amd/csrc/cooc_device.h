@@ -65,6 +65,8 @@ struct ActiveUsers {
   int64_t n_contrib = 0;           // == cbase[n_active] (host copy)
   int64_t n_new = 0;               // interactions of the window == sum(len - old) (host copy)
   const int32_t *arena = nullptr;  // item ids of all histories
+  const uint16_t *arena16 = nullptr;  // optional u16 mirror of arena (n_items <= 40,704); else narrowed per run
+  int64_t arena_span = 0;             // arena entries [0, span) the contributions may reference
 };
 
 // One row's share of the work (heavy rows are split over several chunks).
@@ -128,7 +130,7 @@ class Counter {
   int32_t n_items() const { return M_; }
 
  private:
-  Status run_tile(const int32_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
+  Status run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
 
   int32_t M_ = 0;
   int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)

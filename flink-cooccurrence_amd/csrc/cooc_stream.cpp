@@ -182,6 +182,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   au.n_contrib = cbase[n_act];
   au.n_new = new_ptr[n_act];
   au.arena = arena_.as<int32_t>();
+  au.arena_span = arena_used_;
   CountResult r;
   COOC_TRY(ctx.counter.run(au, s, &r));
 
