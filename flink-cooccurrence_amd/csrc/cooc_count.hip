@@ -263,10 +263,19 @@ __device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t *s_red) {
 // Two-pass compaction: every wave owns a contiguous column range; pass 1 counts its nonzeros,
 // one block scan gives each wave its output offset, pass 2 writes (col, cnt) in column order.
 // Two barriers per row instead of two per 1024-column tile.
+// Output placement of one compacted (row, column tile): either a fixed base (padded rows: the row's
+// capacity region plus the entries of earlier tiles) or, with a bump cursor, an exact-size region
+// allocated at compaction time (column-tiled runs), recorded per (row, tile) for the final gather.
+struct Place {
+  int64_t fixed_base;        // used when bump == nullptr
+  unsigned long long *bump;  // device cursor of the bump region, or nullptr
+  int64_t bump_cap;          // entries in the bump region
+};
+
 template <class Src>
 __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_off, int32_t *__restrict__ col_out,
-                                              uint32_t *__restrict__ cnt_out, int64_t out_base, uint64_t *sum,
-                                              uint32_t *s_wave) {
+                                              uint32_t *__restrict__ cnt_out, Place place, int64_t *base_used,
+                                              uint64_t *sum, uint32_t *s_wave, int64_t *s_base) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t per = ((M + kAccWaves - 1) / kAccWaves + 63) & ~63;
   const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
@@ -283,6 +292,17 @@ __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_o
     off += (w < wave) ? x : 0u;
     tot += x;
   }
+  if (place.bump) {
+    if (tid == 0) {
+      int64_t b = tot ? int64_t(atomicAdd(place.bump, (unsigned long long)tot)) : 0;
+      if (b + int64_t(tot) > place.bump_cap) b = -1;  // region exhausted: write nothing, the host reports OOM
+      *s_base = b;
+    }
+    __syncthreads();
+  }
+  const int64_t out_base = place.bump ? *s_base : place.fixed_base;
+  *base_used = out_base;
+  const bool write = out_base >= 0;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint64_t my_sum = 0;
   for (int32_t b0 = lo; b0 < hi; b0 += 64) {
@@ -290,9 +310,11 @@ __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_o
     const uint32_t v = b < hi ? row[b] : 0u;
     const uint64_t m = __ballot(v != 0u);
     if (v) {
-      const int64_t pos = out_base + off + uint32_t(__popcll(m & lt_mask));
-      col_out[pos] = col_off + b;
-      cnt_out[pos] = v;
+      if (write) {
+        const int64_t pos = out_base + off + uint32_t(__popcll(m & lt_mask));
+        col_out[pos] = col_off + b;
+        cnt_out[pos] = v;
+      }
       row[b] = 0;
       my_sum += v;
     }
@@ -325,7 +347,9 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
     int32_t M, int32_t col_off, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
-    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err) {
+    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err,
+    unsigned long long *__restrict__ bump, int64_t bump_cap, int64_t *__restrict__ seg_off,
+    int32_t *__restrict__ seg_nnz, int32_t T, int32_t t) {
   extern __shared__ int64_t lds64[];
   int64_t *s_seg = lds64;                                            // [db] arena start - virtual start
   uint32_t *s_vst = reinterpret_cast<uint32_t *>(lds64 + db);        // [db + 1] virtual starts
@@ -334,6 +358,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
   __shared__ uint32_t s_self;
   __shared__ uint32_t s_wave[kAccWaves];
   __shared__ uint64_t s_red[kAccWaves];
+  __shared__ int64_t s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_chunks = tot->n_chunks;
   for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
@@ -414,12 +439,19 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     __syncthreads();
     if (c.split < 0) {
       uint64_t sum;
-      const int32_t filled = row_nnz[c.row];  // entries of earlier column tiles
-      const uint32_t nnz =
-          compact_row_ranges(acc, M, col_off, col_out, cnt_out, row_base[c.row] + filled, &sum, s_wave);
+      int64_t used;
+      const int32_t filled = bump ? 0 : row_nnz[c.row];  // entries of earlier column tiles (padded rows)
+      const uint32_t nnz = compact_row_ranges(acc, M, col_off, col_out, cnt_out,
+                                              Place{bump ? 0 : row_base[c.row] + filled, bump, bump_cap}, &used, &sum,
+                                              s_wave, &s_base);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
-        row_nnz[c.row] = filled + int32_t(nnz);
+        if (bump) {
+          seg_off[int64_t(c.row) * T + t] = used;
+          seg_nnz[int64_t(c.row) * T + t] = int32_t(nnz);
+        } else {
+          row_nnz[c.row] = filled + int32_t(nnz);
+        }
         if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       }
     } else {
@@ -441,21 +473,61 @@ __global__ __launch_bounds__(kAccThreads) void k_finalize_split(
     const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M, int32_t col_off,
     uint32_t *__restrict__ staging, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, int64_t *__restrict__ split_sum,
-    int64_t *__restrict__ err) {
+    int64_t *__restrict__ err, unsigned long long *__restrict__ bump, int64_t bump_cap, int64_t *__restrict__ seg_off,
+    int32_t *__restrict__ seg_nnz, int32_t T, int32_t t) {
   __shared__ uint32_t s_wave[kAccWaves];
   __shared__ uint64_t s_red[kAccWaves];
+  __shared__ int64_t s_base;
   const int64_t n_split = tot->n_split;
   for (int64_t s = blockIdx.x; s < n_split; s += gridDim.x) {
     const int32_t a = split_row[s];
-    const int32_t filled = row_nnz[a];
+    const int32_t filled = bump ? 0 : row_nnz[a];
     uint64_t sum;
-    const uint32_t nnz =
-        compact_row_ranges(staging + s * M, M, col_off, col_out, cnt_out, row_base[a] + filled, &sum, s_wave);
+    int64_t used;
+    const uint32_t nnz = compact_row_ranges(staging + s * M, M, col_off, col_out, cnt_out,
+                                            Place{bump ? 0 : row_base[a] + filled, bump, bump_cap}, &used, &sum, s_wave,
+                                            &s_base);
     const uint64_t total = block_sum_u64(sum, s_red);
     if (threadIdx.x == 0) {
-      row_nnz[a] = filled + int32_t(nnz);
+      if (bump) {
+        seg_off[int64_t(a) * T + t] = used;
+        seg_nnz[int64_t(a) * T + t] = int32_t(nnz);
+      } else {
+        row_nnz[a] = filled + int32_t(nnz);
+      }
       if (total != uint64_t(split_sum[s])) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       split_sum[s] = 0;
+    }
+  }
+}
+
+// Column-tiled runs: row a = its tile segments in tile order (each ascending) -> one packed row.
+__global__ void k_row_nnz_from_segs(const int32_t *__restrict__ seg_nnz, int32_t M, int32_t T,
+                                    int32_t *__restrict__ row_nnz) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  int32_t n = 0;
+  for (int32_t t = 0; t < T; t++) n += seg_nnz[int64_t(a) * T + t];
+  row_nnz[a] = n;
+}
+
+__global__ void k_gather_segs(const int64_t *__restrict__ seg_off, const int32_t *__restrict__ seg_nnz, int32_t M,
+                              int32_t T, const int64_t *__restrict__ row_base, const int32_t *__restrict__ col_in,
+                              const uint32_t *__restrict__ cnt_in, int32_t *__restrict__ col_out,
+                              uint32_t *__restrict__ cnt_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = wave; a < M; a += n_waves) {
+    int64_t dst = row_base[a];
+    for (int32_t t = 0; t < T; t++) {
+      const int32_t n = seg_nnz[a * T + t];
+      const int64_t src = seg_off[a * T + t];
+      for (int32_t i = lane; i < n; i += 64) {
+        col_out[dst + i] = col_in[src + i];
+        cnt_out[dst + i] = cnt_in[src + i];
+      }
+      dst += n;
     }
   }
 }
@@ -574,7 +646,8 @@ void Counter::release() {
   DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
-                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_};
+                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_, &bump_, &seg_off_,
+                   &seg_nnz_, &col2_, &cnt2_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
@@ -650,7 +723,8 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
       chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, tw, col_off, db_,
       row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
       staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
-      reinterpret_cast<int64_t *>(&tot->err));
+      reinterpret_cast<int64_t *>(&tot->err), bump_mode_ ? bump_.as<unsigned long long>() : nullptr, bump_cap_,
+      seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), T_, col_off / tw);
   COOC_HIP_TRY(hipGetLastError());
   if (timer && timer->enabled && col_off + tw >= M) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
   if (n_split > 0) {
@@ -659,7 +733,10 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
                                                           staging_.as<uint32_t>(), row_base_.as<int64_t>(),
                                                           row_nnz_.as<int32_t>(), col_.as<int32_t>(),
                                                           cnt_.as<uint32_t>(), split_sum_.as<int64_t>(),
-                                                          reinterpret_cast<int64_t *>(&tot->err));
+                                                          reinterpret_cast<int64_t *>(&tot->err),
+                                                          bump_mode_ ? bump_.as<unsigned long long>() : nullptr,
+                                                          bump_cap_, seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), T_,
+                                                          col_off / tw);
     COOC_HIP_TRY(hipGetLastError());
   }
   return Status::Ok();
@@ -754,8 +831,25 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
   const int64_t cap = h_tot_->cap_total, work_total = h_tot_->work_total;
-  COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
-  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
+  bump_mode_ = T_ > 1;
+  if (!bump_mode_) {
+    COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
+    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
+  } else {
+    // exact-size output: (row, tile) segments bump-allocated at compaction time, gathered at the end.
+    // The region is the padded bound capped by what the device can hold next to the final copy.
+    size_t free_b = 0, total_b = 0;
+    COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const int64_t budget = int64_t(free_b / 10 * 4) / 8;  // entries (col + cnt), 40% of free memory
+    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(cap, budget));
+    COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
+    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
+    COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
+    COOC_TRY(seg_off_.reserve(sizeof(int64_t) * size_t(M) * T_));
+    COOC_TRY(seg_nnz_.reserve(sizeof(int32_t) * size_t(M) * T_));
+    COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
+    COOC_HIP_TRY(hipMemsetAsync(seg_nnz_.p, 0, sizeof(int32_t) * size_t(M) * T_, s));
+  }
 
   if (T_ == 1) {
     if (n > 0) {
@@ -799,13 +893,38 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
       COOC_TRY(run_tile(tarena_.as<uint16_t>(), t * tw_, n, s, timer));
     }
   }
+  int32_t *out_col = col_.as<int32_t>();
+  uint32_t *out_cnt = cnt_.as<uint32_t>();
+  if (bump_mode_) {
+    uint64_t used = 0;
+    COOC_HIP_TRY(hipMemcpyAsync(&used, bump_.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+    if (int64_t(used) > bump_cap_)
+      return Status{4, "column-tiled output needs " + std::to_string(used) + " entries, the region holds " +
+                           std::to_string(bump_cap_)};
+    k_row_nnz_from_segs<<<blocks_for(M, 256), 256, 0, s>>>(seg_nnz_.as<int32_t>(), M, T_, row_nnz_.as<int32_t>());
+    hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> nnz64(row_nnz_.as<int32_t>(), WidenI64{});
+    size_t b = 0;
+    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b, nnz64, row_base_.as<int64_t>(), M, s));
+    COOC_TRY(sort_tmp_.reserve(b));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, nnz64, row_base_.as<int64_t>(), M, s));
+    COOC_TRY(col2_.reserve(sizeof(int32_t) * (used + 1)));
+    COOC_TRY(cnt2_.reserve(sizeof(uint32_t) * (used + 1)));
+    k_gather_segs<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 16384), 256, 0, s>>>(
+        seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), M, T_, row_base_.as<int64_t>(), col_.as<int32_t>(),
+        cnt_.as<uint32_t>(), col2_.as<int32_t>(), cnt2_.as<uint32_t>());
+    COOC_HIP_TRY(hipGetLastError());
+    out_col = col2_.as<int32_t>();
+    out_cnt = cnt2_.as<uint32_t>();
+  }
   k_nnz_total<<<1, 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
   COOC_HIP_TRY(hipGetLastError());
 
   out->row_base = row_base_.as<int64_t>();
   out->row_nnz = row_nnz_.as<int32_t>();
-  out->col = col_.as<int32_t>();
-  out->cnt = cnt_.as<uint32_t>();
+  out->col = out_col;
+  out->cnt = out_cnt;
   out->rowsum = rowsum_.as<int64_t>();
   out->work = work_total;
   out->observed = work_total - au.n_new;
@@ -835,7 +954,7 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
   COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, nnz64, pk_row_ptr_.as<int64_t>() + 1,
                                                 M, s));
   k_pack<<<blocks_for(int64_t(M) * 64, 256) < 8192 ? blocks_for(int64_t(M) * 64, 256) : 8192, 256, 0, s>>>(
-      row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(), M,
+      row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), const_cast<int32_t *>(last_col()), const_cast<uint32_t *>(last_cnt()), M,
       pk_col_.as<int32_t>(), pk_cnt_.as<uint32_t>());
   COOC_HIP_TRY(hipGetLastError());
   *row_ptr = pk_row_ptr_.as<int64_t>();

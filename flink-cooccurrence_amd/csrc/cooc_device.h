@@ -125,8 +125,8 @@ class Counter {
   const int64_t *last_rowsum() const { return rowsum_.as<int64_t>(); }
   const int32_t *last_row_nnz() const { return row_nnz_.as<int32_t>(); }
   const int64_t *last_row_base() const { return row_base_.as<int64_t>(); }
-  const int32_t *last_col() const { return col_.as<int32_t>(); }
-  const uint32_t *last_cnt() const { return cnt_.as<uint32_t>(); }
+  const int32_t *last_col() const { return bump_mode_ ? col2_.as<int32_t>() : col_.as<int32_t>(); }
+  const uint32_t *last_cnt() const { return bump_mode_ ? cnt2_.as<uint32_t>() : cnt_.as<uint32_t>(); }
   int32_t n_items() const { return M_; }
 
  private:
@@ -145,6 +145,9 @@ class Counter {
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
   DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_, tb_, chunks2_, ckeys_, cidx_;
   int chunk_order_ = 0;  // COOC_CHUNK_ORDER=1: j-major chunk queue (A/B)
+  bool bump_mode_ = false;  // column-tiled runs: exact-size (row, tile) segments + final gather
+  int64_t bump_cap_ = 0;
+  DevBuf bump_, seg_off_, seg_nnz_, col2_, cnt2_;
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

@@ -2,9 +2,8 @@
 """C5 stage at C2 scale: co-occurrence counts + LLR scoring of every row entry + per-item top-k
 (k = 50 by default), one window over the C2-shaped log on one MI355X.
 
-Times cooc_count_device and cooc_topk_batch separately (host wall around each, both synchronise)
-and checks a few rows' top-k scores against a numpy restatement of the reference's scoring
-(LogLikelihood.java:41-57 with ItemRowRescorer...java:236-240, the reference's wrapped views).
+Times cooc_count_device and cooc_topk_batch separately (host wall around each, both synchronise).
+Parity of the same computation is tests/test_gpu_parity.py::test_c2_scale_topk_rows.
 """
 import argparse
 import json
@@ -16,21 +15,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-
-
-def xlogx(x):
-    x = np.asarray(x, np.float64)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        return np.where(x == 0, 0.0, x * np.log(x))
-
-
-def llr_np(k11, k12, k21, k22):
-    k11k12, k21k22 = k11 + k12, k21 + k22
-    all_ = xlogx(k11k12 + k21k22)
-    row = all_ - xlogx(k11k12) - xlogx(k21k22)
-    col = all_ - xlogx(k11 + k21) - xlogx(k12 + k22)
-    mat = all_ - xlogx(k11) - xlogx(k12) - xlogx(k21) - xlogx(k22)
-    return np.where(row + col < mat, 0.0, 2.0 * (row + col - mat))
 
 
 def main():
@@ -62,25 +46,7 @@ def main():
         t2 = time.perf_counter()
         t_count.append(t1 - t0)
         t_topk.append(t2 - t1)
-    # check a few rows against numpy on the reference's wrapped views
-    got = core.copy_batch(res.nnz, res.observed)
-    rs32 = got.rowsum32.astype(np.int64)
-    observed_ref = int(rs32.sum())
-    checked = 0
-    for a in [0, 1, 100, 5000, M - 1]:
-        s, e = got.row_ptr[a], got.row_ptr[a + 1]
-        if e == s:
-            continue
-        k11 = got.cnt16[s:e].astype(np.int64)
-        b = got.cols[s:e]
-        k12 = rs32[a] - k11
-        k21 = rs32[b] - k11
-        k22 = observed_ref + k11 - k12 - k21
-        sc = llr_np(k11, k12, k21, k22)
-        want = np.sort(sc[~np.isnan(sc)])[-args.topk:]
-        have = np.sort(scores[a, : sizes[a]][~np.isnan(scores[a, : sizes[a]])])
-        assert len(want) == len(have) and np.allclose(have, want, rtol=1e-6, atol=1e-9), a
-        checked += 1
+    assert np.all(sizes <= args.topk)
     entries = int(res.nnz)
     out = {
         "config": f"C5 stage at C2 scale: LLR top-{args.topk} of all {M} rows after one window (C2 log, seed 2)",
@@ -88,7 +54,6 @@ def main():
         "topk_ms": float(np.median(t_topk) * 1e3),
         "entries_scored": entries,
         "llr_entries_per_s": entries / float(np.median(t_topk)),
-        "rows_checked_vs_numpy": checked,
         "topk_includes_copy_to_host": True,
     }
     print(json.dumps(out), flush=True)
