@@ -125,6 +125,21 @@ def config_c2(seed: int = 2, U: int = 138_493, M: int = 26_744, N: int = 20_000_
                 name="C2 MovieLens-20M-shaped 138,493 users x 26,744 items, 20,000,263 interactions", seed=seed)
 
 
+def config_c3(seed: int = 3, U: int = 10_000_000, M: int = 1_000_000, N: int = 1_000_000_000, shard: int = 0,
+              n_shards: int = 1, cap: int = 10_000):
+    """C3, Zipf-skewed 1B log: n_u ~ lognormal(sigma=1) scaled to mean N/U and capped at 10,000; items
+    Zipf(1.0) with replacement.  `shard`/`n_shards` generate one contiguous user shard (seed 3 +
+    shard) so that each rank of a multi-GPU run materialises only its own users."""
+    rng = np.random.Generator(np.random.PCG64(seed + shard))
+    Us = U // n_shards + (1 if shard < U % n_shards else 0)
+    Ns = int(round(N * Us / U))
+    lens = lognormal_lengths(rng, Us, Ns, 1, cap)
+    items = zipf_with_replacement(rng, lens, M, 1.0)
+    user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return dict(user_ptr=user_ptr, items=items, ts=None, n_items=M, window_ms=None,
+                name=f"C3 Zipf 1B: shard {shard}/{n_shards} ({Us} users, {Ns} interactions, 1e6 items)", seed=seed + shard)
+
+
 def spread_over_windows(rng, user_ptr: np.ndarray, n_windows: int, window_ms: int) -> np.ndarray:
     """C4: event times spread over n_windows tumbling windows, ascending within each user."""
     n = int(user_ptr[-1])
