@@ -192,6 +192,38 @@ __global__ void k_narrow(const int32_t *__restrict__ src, int64_t n, uint16_t *_
   }
 }
 
+// Padded u16 arena for the vector path: user j's list at poff[j] (16-B aligned), padded to a
+// multiple of 8 ids with 0xFFFF.
+__global__ void k_pad_lens(int64_t n, const int32_t *__restrict__ len, int64_t *__restrict__ plen) {
+  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) plen[j] = (int64_t(len[j]) + 7) & ~int64_t(7);
+}
+
+__global__ void k_narrow_pad(int64_t n_users, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                             const int64_t *__restrict__ poff, const int32_t *__restrict__ arena,
+                             uint16_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = wave; j < n_users; j += n_waves) {
+    const int32_t *h = arena + off[j];
+    uint16_t *o = out + poff[j];
+    const int32_t n = len[j], pn = (n + 7) & ~7;
+    for (int32_t i = lane; i < pn; i += 64) o[i] = i < n ? uint16_t(h[i]) : uint16_t(0xFFFF);
+  }
+}
+
+struct PadLenOp {  // padded segment length of a (kind-0) contribution
+  const int64_t *plen;
+  __host__ __device__ int64_t operator()(uint32_t v) const { return plen[v >> 1]; }
+};
+
+__global__ void k_seg_start_pad(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ poff,
+                                int64_t *__restrict__ seg) {
+  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c < n) seg[c] = poff[cvals[c] >> 1] | (int64_t(1) << 63);
+}
+
 struct TileWorkOp {  // pair work of a contribution inside column tile t
   const int32_t *tb;
   int32_t T, t;
@@ -341,10 +373,14 @@ __global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const
 // segment descriptors (virtual start, arena start) are staged in LDS per batch; the 16 waves split
 // the batch's range into equal contiguous pieces and walk it 64 lanes wide, so every lane stays
 // busy whatever the user-list lengths, and no wave waits on a per-user descriptor chain.
-template <int U>
+// VEC: every segment starts 16-B aligned and spans a multiple of 8 ids (user lists padded with
+// 0xFFFF in the arena, virtual starts from the padded prefix `vpre`), so each lane loads 8 partner
+// ids with one 16-B load: 8x fewer load instructions in flight for the same bytes.
+template <int U, bool VEC>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
+    const int64_t *__restrict__ vpre,
     int32_t M, int32_t col_off, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
     int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err,
@@ -373,10 +409,11 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk c = chunks[ch];
     for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
       const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
-      const int64_t e0 = epre[b0];
+      const int64_t *vp = VEC ? vpre : epre;
+      const int64_t e0 = vp[b0];
       uint32_t selfs = 0;
       for (int32_t i = tid; i <= nb; i += kAccThreads) {
-        const uint32_t vs = uint32_t(epre[b0 + i] - e0);
+        const uint32_t vs = uint32_t(vp[b0 + i] - e0);
         s_vst[i] = vs;
         if (i < nb) {
           const int64_t sg = seg[b0 + i];
@@ -388,40 +425,88 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       if (lane == 0 && bal) atomicAdd(&s_self, uint32_t(__popcll(bal)));
       __syncthreads();
       const uint32_t total = s_vst[nb];
-      const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
-      const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
-      uint32_t v = lo + lane;
-      if (v < hi) {
-        // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
-        int32_t l = 0, r = nb;
-        while (r - l > 1) {
-          const int32_t m = (l + r) >> 1;
-          if (s_vst[m] <= v) l = m; else r = m;
-        }
-        int32_t cur = l;
-        uint32_t next = s_vst[cur + 1];
-        int64_t base = s_seg[cur];
-        for (; v < hi; v += 64u * U) {
-          int64_t a[U];
+      if (!VEC) {
+        const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
+        const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
+        uint32_t v = lo + lane;
+        if (v < hi) {
+          // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
+          int32_t l = 0, r = nb;
+          while (r - l > 1) {
+            const int32_t m = (l + r) >> 1;
+            if (s_vst[m] <= v) l = m; else r = m;
+          }
+          int32_t cur = l;
+          uint32_t next = s_vst[cur + 1];
+          int64_t base = s_seg[cur];
+          for (; v < hi; v += 64u * U) {
+            int64_t a[U];
 #pragma unroll
-          for (int k = 0; k < U; k++) {
-            const uint32_t vk = v + 64u * k;
-            a[k] = -1;
-            if (vk < hi) {
-              while (vk >= next) {
-                cur++;
-                next = s_vst[cur + 1];
-                base = s_seg[cur];
+            for (int k = 0; k < U; k++) {
+              const uint32_t vk = v + 64u * k;
+              a[k] = -1;
+              if (vk < hi) {
+                while (vk >= next) {
+                  cur++;
+                  next = s_vst[cur + 1];
+                  base = s_seg[cur];
+                }
+                a[k] = base + vk;
               }
-              a[k] = base + vk;
+            }
+            uint32_t it[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? uint32_t(arena[a[k]]) : 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < U; k++)
+              if (it[k] != 0xFFFFFFFFu) atomicAdd(&acc[it[k]], 1u);
+          }
+        }
+      } else {
+        // groups of 8 ids; every segment boundary is a multiple of 8
+        const uint32_t groups = total >> 3;
+        const uint32_t lo = uint32_t((uint64_t(groups) * uint32_t(wave)) / kAccWaves);
+        const uint32_t hi = uint32_t((uint64_t(groups) * uint32_t(wave + 1)) / kAccWaves);
+        uint32_t g = lo + lane;
+        if (g < hi) {
+          int32_t l = 0, r = nb;
+          while (r - l > 1) {
+            const int32_t m = (l + r) >> 1;
+            if (s_vst[m] <= (g << 3)) l = m; else r = m;
+          }
+          int32_t cur = l;
+          uint32_t next = s_vst[cur + 1];
+          int64_t base = s_seg[cur];
+          for (; g < hi; g += 64u * U) {
+            int64_t a[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+              const uint32_t gk = g + 64u * k;
+              a[k] = -1;
+              if (gk < hi) {
+                while ((gk << 3) >= next) {
+                  cur++;
+                  next = s_vst[cur + 1];
+                  base = s_seg[cur];
+                }
+                a[k] = base + (int64_t(gk) << 3);
+              }
+            }
+            uint4 q[U];
+#pragma unroll
+            for (int k = 0; k < U; k++)
+              q[k] = a[k] >= 0 ? *reinterpret_cast<const uint4 *>(arena + a[k]) : make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+              const uint32_t w4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+              for (int h = 0; h < 4; h++) {
+                const uint32_t lo16 = w4[h] & 0xFFFFu, hi16 = w4[h] >> 16;
+                if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
+                if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
+              }
             }
           }
-          uint32_t it[U];
-#pragma unroll
-          for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? uint32_t(arena[a[k]]) : 0xFFFFFFFFu;
-#pragma unroll
-          for (int k = 0; k < U; k++)
-            if (it[k] != 0xFFFFFFFFu) atomicAdd(&acc[it[k]], 1u);
         }
       }
       __syncthreads();
@@ -626,13 +711,21 @@ Status Counter::init(int32_t n_items) {
   db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
   if (db_ < 32) return Status{1, "column tile too wide for the LDS row plus descriptors"};
   const size_t lds2 = size_t(db_) * 12 + 4 + lds;
-  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<4>),
-                        reinterpret_cast<const void *>(k_accumulate2<8>),
-                        reinterpret_cast<const void *>(k_accumulate2<16>),
-                        reinterpret_cast<const void *>(k_accumulate2<32>)})
+  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<4, false>),
+                        reinterpret_cast<const void *>(k_accumulate2<8, false>),
+                        reinterpret_cast<const void *>(k_accumulate2<16, false>),
+                        reinterpret_cast<const void *>(k_accumulate2<32, false>),
+                        reinterpret_cast<const void *>(k_accumulate2<2, true>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true>),
+                        reinterpret_cast<const void *>(k_accumulate2<8, true>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
   const char *co = getenv("COOC_CHUNK_ORDER");
   chunk_order_ = co ? atoi(co) : 0;
+  const char *vv = getenv("COOC_ACC_VEC");
+  vec_allowed_ = !(vv && vv[0] == '0');
+  const char *vu = getenv("COOC_ACC_VUNROLL");
+  vunroll_ = vu ? atoi(vu) : 4;
+  if (vunroll_ != 2 && vunroll_ != 8) vunroll_ = 4;
   const char *u = getenv("COOC_ACC_UNROLL");
   unroll_ = u ? atoi(u) : 16;
   if (unroll_ != 4 && unroll_ != 8 && unroll_ != 32) unroll_ = 16;
@@ -647,7 +740,7 @@ void Counter::release() {
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
                    &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_, &bump_, &seg_off_,
-                   &seg_nnz_, &col2_, &cnt2_};
+                   &seg_nnz_, &col2_, &cnt2_, &plen_, &poff_, &vpre_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
@@ -716,11 +809,14 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
   // ★ accumulate
   const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
   if (timer && timer->enabled && col_off == 0) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  auto kern = unroll_ == 32 ? k_accumulate2<32>
-              : unroll_ == 8 ? k_accumulate2<8>
-              : unroll_ == 4 ? k_accumulate2<4> : k_accumulate2<16>;
+  auto kern = vec_ ? (vunroll_ == 8 ? k_accumulate2<8, true> : vunroll_ == 2 ? k_accumulate2<2, true>
+                                                              : k_accumulate2<4, true>)
+                    : (unroll_ == 32 ? k_accumulate2<32, false>
+                       : unroll_ == 8 ? k_accumulate2<8, false>
+                       : unroll_ == 4 ? k_accumulate2<4, false> : k_accumulate2<16, false>);
   kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(tw) * 4, s>>>(
-      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, tw, col_off, db_,
+      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, vpre_.as<int64_t>(), tw,
+      col_off, db_,
       row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
       staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
       reinterpret_cast<int64_t *>(&tot->err), bump_mode_ ? bump_.as<unsigned long long>() : nullptr, bump_cap_,
@@ -851,7 +947,34 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
     COOC_HIP_TRY(hipMemsetAsync(seg_nnz_.p, 0, sizeof(int32_t) * size_t(M) * T_, s));
   }
 
-  if (T_ == 1) {
+  vec_ = T_ == 1 && vec_allowed_ && au.n_new == au.n_contrib && n > 0;  // one-window batch: all kind 0
+  if (vec_) {
+    const int64_t U = au.n_active;
+    COOC_TRY(plen_.reserve(sizeof(int64_t) * (U + 1)));
+    COOC_TRY(poff_.reserve(sizeof(int64_t) * (U + 1)));
+    COOC_TRY(vpre_.reserve(sizeof(int64_t) * (n + 1)));
+    k_pad_lens<<<blocks_for(U, 256), 256, 0, s>>>(U, au.len, plen_.as<int64_t>());
+    COOC_HIP_TRY(hipMemsetAsync(poff_.p, 0, sizeof(int64_t), s));
+    COOC_HIP_TRY(hipMemsetAsync(vpre_.p, 0, sizeof(int64_t), s));
+    hipcub::TransformInputIterator<int64_t, PadLenOp, const uint32_t *> pad_it(vals, PadLenOp{plen_.as<int64_t>()});
+    size_t b1 = 0, b2 = 0;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b1, plen_.as<int64_t>(), poff_.as<int64_t>() + 1, int(U), s));
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, pad_it, vpre_.as<int64_t>() + 1, int(n), s));
+    COOC_TRY(sort_tmp_.reserve(std::max(b1, b2)));
+    b1 = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b1, plen_.as<int64_t>(), poff_.as<int64_t>() + 1, int(U), s));
+    b2 = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b2, pad_it, vpre_.as<int64_t>() + 1, int(n), s));
+    int64_t padded = 0;
+    COOC_HIP_TRY(hipMemcpyAsync(&padded, poff_.as<int64_t>() + U, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+    COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (padded + 16)));
+    k_narrow_pad<<<std::min<unsigned>(blocks_for(U * 64, 256), 16384), 256, 0, s>>>(
+        U, au.off, au.len, poff_.as<int64_t>(), au.arena, tarena_.as<uint16_t>());
+    k_seg_start_pad<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, poff_.as<int64_t>(), seg_.as<int64_t>());
+    COOC_HIP_TRY(hipGetLastError());
+    COOC_TRY(run_tile(tarena_.as<uint16_t>(), 0, n, s, timer));
+  } else if (T_ == 1) {
     if (n > 0) {
       k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
       COOC_HIP_TRY(hipGetLastError());

@@ -148,6 +148,9 @@ class Counter {
   bool bump_mode_ = false;  // column-tiled runs: exact-size (row, tile) segments + final gather
   int64_t bump_cap_ = 0;
   DevBuf bump_, seg_off_, seg_nnz_, col2_, cnt2_;
+  bool vec_ = false, vec_allowed_ = true;  // 16-B partner-id loads over a padded arena (batch, one tile)
+  int vunroll_ = 4;                        // COOC_ACC_VUNROLL: 16-B loads in flight per lane (2, 4, 8)
+  DevBuf plen_, poff_, vpre_;
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 
