@@ -40,10 +40,12 @@ class StreamState {
 
  private:
   Status ensure_global(cooc_ctx &ctx);
+  int32_t slot_for(int32_t user_id);
   Status grow_arena(cooc_ctx &ctx, int64_t need);
 
   // host metadata of the per-user histories
-  std::unordered_map<int32_t, int32_t> slot_of_;
+  std::unordered_map<int32_t, int32_t> slot_of_;  // user ids outside [0, 2^26)
+  std::vector<int32_t> dense_slot_;               // user ids in [0, 2^26)
   std::vector<int64_t> h_off_;
   std::vector<int32_t> h_len_, h_cap_;
   int64_t arena_used_ = 0;
@@ -51,9 +53,12 @@ class StreamState {
   // staged window
   bool staged_ = false;
   int64_t staged_ts_ = 0;
-  std::unordered_map<int32_t, int32_t> staged_idx_;  // slot -> index into staged_items_
+  int64_t window_seq_ = 0;
+  int32_t n_staged_ = 0;
+  std::vector<int64_t> staged_stamp_;  // per slot: window_seq_ when staged in the current window
+  std::vector<int32_t> staged_pos_;    // per slot: index into staged_slots_/staged_items_
   std::vector<int32_t> staged_slots_;
-  std::vector<std::vector<int32_t>> staged_items_;
+  std::vector<std::vector<int32_t>> staged_items_;  // reused across windows
   // device uploads of one window
   DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
   // global state

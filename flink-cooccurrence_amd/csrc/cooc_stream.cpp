@@ -7,6 +7,9 @@
 // reductions run on the device (cooc_count.hip); this file only keeps per-user metadata, stages
 // the window's interactions and moves results.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "cooc_ctx.h"
@@ -30,6 +33,27 @@ Status upload(DevBuf &b, const std::vector<T> &v, hipStream_t s) {
   return Status::Ok();
 }
 
+// COOC_TRACE=1: per-window phase times on stderr (host wall; device phases end at a sync).
+struct PhaseTrace {
+  bool on = getenv("COOC_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+  char buf[512];
+  int len = 0;
+  void mark(const char *name, hipStream_t s = nullptr) {
+    if (!on) return;
+    if (s) (void)hipStreamSynchronize(s);
+    const auto now = std::chrono::steady_clock::now();
+    len += snprintf(buf + len, sizeof(buf) - len, " %s=%.3f", name,
+                    std::chrono::duration<double, std::milli>(now - last).count());
+    last = now;
+  }
+  void done(int64_t ts) {
+    if (on)
+      fprintf(stderr, "[cooc] window %lld:%s total=%.3f ms\n", (long long)ts, buf,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 }  // namespace
 
 void StreamState::release() {
@@ -39,6 +63,29 @@ void StreamState::release() {
                    &d_topk_score_, &d_topk_size_};
   for (DevBuf *b : all) b->release();
   global_ready_ = false;
+}
+
+// Keyed user state lookup (userHistoryState, NonSampled...java:129-132): a dense table for
+// non-negative ids below 2^26, a hash map otherwise.
+int32_t StreamState::slot_for(int32_t uid) {
+  int32_t slot = -1;
+  if (uid >= 0 && uid < (1 << 26)) {
+    if (size_t(uid) >= dense_slot_.size()) dense_slot_.resize(std::max<size_t>(size_t(uid) + 1, dense_slot_.size() * 2), -1);
+    slot = dense_slot_[uid];
+  } else {
+    auto it = slot_of_.find(uid);
+    if (it != slot_of_.end()) slot = it->second;
+  }
+  if (slot >= 0) return slot;
+  slot = int32_t(h_off_.size());  // userHistoryState.value() == null -> new IntArrayList(), :130-132
+  if (uid >= 0 && uid < (1 << 26)) dense_slot_[uid] = slot;
+  else slot_of_.emplace(uid, slot);
+  h_off_.push_back(0);
+  h_len_.push_back(0);
+  h_cap_.push_back(0);
+  staged_stamp_.push_back(-1);
+  staged_pos_.push_back(0);
+  return slot;
 }
 
 Status StreamState::submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int32_t *user_ids,
@@ -54,27 +101,21 @@ Status StreamState::submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int
         return Status{COOC_ERR_ARG, "item id " + std::to_string(items[i]) + " outside [0, n_items)"};
   }
   for (int32_t u = 0; u < n_users; u++) {
-    const int32_t uid = user_ids[u];
-    auto it = slot_of_.find(uid);
-    int32_t slot;
-    if (it == slot_of_.end()) {  // userHistoryState.value() == null -> new IntArrayList(), :130-132
-      slot = int32_t(h_off_.size());
-      slot_of_.emplace(uid, slot);
-      h_off_.push_back(0);
-      h_len_.push_back(0);
-      h_cap_.push_back(0);
-    } else {
-      slot = it->second;
-    }
-    auto st = staged_idx_.find(slot);
+    const int32_t slot = slot_for(user_ids[u]);
     int32_t j;
-    if (st == staged_idx_.end()) {
-      j = int32_t(staged_slots_.size());
-      staged_idx_.emplace(slot, j);
-      staged_slots_.push_back(slot);
-      staged_items_.emplace_back();
+    if (staged_stamp_[slot] != window_seq_) {  // first appearance of this user in the window
+      staged_stamp_[slot] = window_seq_;
+      j = n_staged_++;
+      staged_pos_[slot] = j;
+      if (int32_t(staged_slots_.size()) < n_staged_) {
+        staged_slots_.push_back(slot);
+        staged_items_.emplace_back();
+      } else {
+        staged_slots_[j] = slot;
+        staged_items_[j].clear();  // keeps the capacity of earlier windows
+      }
     } else {
-      j = st->second;
+      j = staged_pos_[slot];
     }
     auto &dst = staged_items_[j];
     dst.insert(dst.end(), items + user_ptr[u], items + user_ptr[u + 1]);
@@ -126,7 +167,8 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
                                       std::to_string(staged_ts_) + " is staged"};
   hipStream_t s = ctx.stream;
   const int32_t M = ctx.cfg.n_items;
-  const int64_t n_act = int64_t(staged_slots_.size());
+  const int64_t n_act = n_staged_;
+  PhaseTrace tr;
 
   // ---- host plan: history capacity (relocation on growth), append destinations, contributions
   std::vector<int64_t> act_off(n_act), cbase(n_act + 1, 0), new_ptr(n_act + 1, 0), new_dst(n_act), reloc;
@@ -159,6 +201,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
     observed_window += need * (need - 1) - old * (old - 1);  // sum over new positions of 2*|history|
     h_len_[slot] = int32_t(need);
   }
+  tr.mark("host_plan");
   COOC_TRY(grow_arena(ctx, std::max<int64_t>(arena_used_, 1024)));
   COOC_TRY(upload(d_reloc_, reloc, s));
   COOC_TRY(upload(d_new_items_, new_items, s));
@@ -184,7 +227,9 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   au.arena = arena_.as<int32_t>();
   au.arena_span = arena_used_;
   CountResult r;
+  tr.mark("upload_append", s);
   COOC_TRY(ctx.counter.run(au, s, &r));
+  tr.mark("count", s);
 
   // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
   COOC_TRY(ensure_global(ctx));
@@ -202,6 +247,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
                             (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_topk_size_.as<int32_t>(),
                             d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
   }
+  tr.mark("merge_rescore", s);
   int64_t h_scal[8];
   COOC_HIP_TRY(hipMemcpyAsync(h_scal, scal, sizeof(h_scal), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
@@ -225,10 +271,10 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   *info = last_;
   have_window_ = true;
 
+  tr.done(ts);
   staged_ = false;
-  staged_idx_.clear();
-  staged_slots_.clear();
-  staged_items_.clear();
+  n_staged_ = 0;
+  window_seq_++;
   return Status::Ok();
 }
 
