@@ -31,7 +31,7 @@ constexpr int kAccWaves = kAccThreads / 64;
 constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
 constexpr int kMaxLdsCounters = 40704;            // dense row in LDS (uint32 counters)
 constexpr int kTileMax = 32768;                   // column tile width when n_items exceeds one LDS row
-constexpr int kLdsBudget = 160 * 1024 - 256;      // dynamic LDS left after the kernels' static LDS
+constexpr int kLdsBudget = 160 * 1024 - 512;      // dynamic LDS left after the kernels' static LDS
 
 template <class T>
 __device__ inline int64_t lower_bound_i64(const T *a, int64_t n, T x) {
@@ -376,7 +376,11 @@ __global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const
 // VEC: every segment starts 16-B aligned and spans a multiple of 8 ids (user lists padded with
 // 0xFFFF in the arena, virtual starts from the padded prefix `vpre`), so each lane loads 8 partner
 // ids with one 16-B load: 8x fewer load instructions in flight for the same bytes.
-template <int U, bool VEC>
+// X (experiments only, never the default): bit 0 = no LDS atomics (ids folded into a register),
+// bit 1 = partner loads redirected into the first 256 KB of the arena (L2-resident).
+// S (VEC): lanes per walker; each walker owns a contiguous range of 8-id groups and steps S groups
+// at a time (S = 8: one 128-B line per walker-step, a segment boundary every few steps).
+template <int U, bool VEC, int X = 0, int S = 64>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
@@ -398,6 +402,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_chunks = tot->n_chunks;
   for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
+  uint32_t xr = 0;
   for (;;) {
     if (tid == 0) {
       s_chunk = atomicAdd(queue, 1);
@@ -465,10 +470,12 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       } else {
         // groups of 8 ids; every segment boundary is a multiple of 8
         const uint32_t groups = total >> 3;
-        const uint32_t lo = uint32_t((uint64_t(groups) * uint32_t(wave)) / kAccWaves);
-        const uint32_t hi = uint32_t((uint64_t(groups) * uint32_t(wave + 1)) / kAccWaves);
-        uint32_t g = lo + lane;
-        if (g < hi) {
+        constexpr uint32_t kWalkers = kAccThreads / S;
+        const uint32_t q = uint32_t(tid) / S;
+        const uint32_t lo = uint32_t((uint64_t(groups) * q) / kWalkers);
+        const uint32_t hi = uint32_t((uint64_t(groups) * (q + 1)) / kWalkers);
+        uint32_t g = lo + uint32_t(tid) % S;
+        if (!(X & 4) && g < hi) {
           int32_t l = 0, r = nb;
           while (r - l > 1) {
             const int32_t m = (l + r) >> 1;
@@ -477,11 +484,11 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
           int32_t cur = l;
           uint32_t next = s_vst[cur + 1];
           int64_t base = s_seg[cur];
-          for (; g < hi; g += 64u * U) {
+          for (; g < hi; g += uint32_t(S) * U) {
             int64_t a[U];
 #pragma unroll
             for (int k = 0; k < U; k++) {
-              const uint32_t gk = g + 64u * k;
+              const uint32_t gk = g + uint32_t(S) * k;
               a[k] = -1;
               if (gk < hi) {
                 while ((gk << 3) >= next) {
@@ -490,6 +497,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
                   base = s_seg[cur];
                 }
                 a[k] = base + (int64_t(gk) << 3);
+                if (X & 2) a[k] &= 0x1FFF8;
               }
             }
             uint4 q[U];
@@ -502,8 +510,12 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
 #pragma unroll
               for (int h = 0; h < 4; h++) {
                 const uint32_t lo16 = w4[h] & 0xFFFFu, hi16 = w4[h] >> 16;
-                if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
-                if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
+                if (X & 1) {
+                  xr += (lo16 != 0xFFFFu ? lo16 : 0u) ^ (hi16 != 0xFFFFu ? hi16 : 0u);
+                } else {
+                  if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
+                  if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
+                }
               }
             }
           }
@@ -511,6 +523,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       }
       __syncthreads();
     }
+    if ((X & 1) && xr == 0xDEADBEEFu) acc[0] = 1;  // keeps the folded loads alive
     // the -1 at x_p for every new position applies to column x_p = row, in the tile that holds it
     const bool own = c.row >= col_off && c.row < col_off + M;
     const uint32_t self_total = own ? s_self : 0u;
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
         } else {
           row_nnz[c.row] = filled + int32_t(nnz);
         }
-        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+        if (X == 0 && total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       }
     } else {
       uint32_t *srow = staging + int64_t(c.split) * M;
@@ -617,17 +630,18 @@ __global__ void k_gather_segs(const int64_t *__restrict__ seg_off, const int32_t
   }
 }
 
+// Sum of row_nnz into tot->nnz_total (which the run zeroed); any grid of 256-thread blocks.
 __global__ void k_nnz_total(const int32_t *__restrict__ row_nnz, int32_t M, PlanTotals *__restrict__ tot) {
-  __shared__ int64_t s[256];
-  int64_t v = 0;
-  for (int32_t a = threadIdx.x; a < M; a += 256) v += row_nnz[a];
-  s[threadIdx.x] = v;
+  __shared__ uint64_t s[4];
+  uint64_t v = 0;
+  for (int32_t a = blockIdx.x * 256 + threadIdx.x; a < M; a += gridDim.x * 256) v += uint64_t(row_nnz[a]);
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t = s[0] + s[1] + s[2] + s[3];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->nnz_total), (unsigned long long)t);
   }
-  if (threadIdx.x == 0) tot->nnz_total = s[0];
 }
 
 // Pack: padded CSR -> contiguous CSR (one wave per row).
@@ -653,6 +667,361 @@ __global__ void k_iota_users(int64_t n, const int64_t *__restrict__ user_ptr, in
     off[j] = user_ptr[j];
     len[j] = int32_t(user_ptr[j + 1] - user_ptr[j]);
     old[j] = 0;
+  }
+}
+
+// ==== batch planner: one window over empty histories, straight from the CSR of user histories =====
+// A contribution is (row a, user u) for every interaction (u, a): row a adds u's whole list, then
+// -1 at column a (NonSampled...java:129-161 with an empty resident history).  The planner builds
+// the row-grouped contribution list as the transpose of A by a counting sort, in 4 passes over N:
+//   k_batch_users   padded lengths pad8(n_u), sum n_u^2, sum n_u pad8(n_u), max n_u
+//   k_batch_hist    per-block LDS histogram of items + the padded u16 arena (pad id = M: sink slot)
+//   k_batch_colscan per-item exclusive prefix over the block histograms -> per-block row offsets
+//   k_batch_scatter contribution descriptors (n_u << 40 | arena offset) at their row positions
+// and no per-contribution prefix sums: k_acc_batch scans segment lengths inside the workgroup.
+constexpr int kPlanThreads = 1024;
+constexpr int kUserGroup = 16;  // lanes per user in the planner passes (4 users per wave)
+constexpr uint64_t kOffMask = (uint64_t(1) << 40) - 1;
+
+__global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *__restrict__ up,
+                                                     int64_t *__restrict__ plen, PlanTotals *__restrict__ tot) {
+  __shared__ uint64_t s2[4], spl[4];
+  __shared__ int64_t smax[4];
+  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint64_t l2 = 0, lpl = 0;
+  int64_t mx = 0;
+  if (j < U) {
+    const int64_t l = up[j + 1] - up[j];
+    const int64_t pl = (l + 7) & ~int64_t(7);
+    plen[j] = pl;
+    l2 = uint64_t(l) * uint64_t(l);
+    lpl = uint64_t(l) * uint64_t(pl);
+    mx = l;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    l2 += __shfl_xor(l2, o, 64);
+    lpl += __shfl_xor(lpl, o, 64);
+    mx = max(mx, __shfl_xor(mx, o, 64));
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s2[w] = l2;
+    spl[w] = lpl;
+    smax[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; k++) {
+      l2 += s2[k];
+      lpl += spl[k];
+      mx = max(mx, smax[k]);
+    }
+    if (l2) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_l2), (unsigned long long)l2);
+    if (lpl) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_lpl), (unsigned long long)lpl);
+    if (mx) atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_len), (unsigned long long)mx);
+  }
+}
+
+// Users of partition block b: [ub[b], ub[b+1]), cut where the interaction prefix crosses N*b/B.
+__global__ void k_batch_bounds(int64_t U, const int64_t *__restrict__ up, int32_t B, int32_t *__restrict__ ub) {
+  const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > B) return;
+  const int64_t N = up[U];
+  const int64_t target = (b == B) ? N + 1 : (N * b) / B;
+  ub[b] = b == B ? int32_t(U) : int32_t(lower_bound_i64<int64_t>(up, U, target));
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_batch_hist(const int64_t *__restrict__ up,
+                                                             const int32_t *__restrict__ items,
+                                                             const int32_t *__restrict__ ub,
+                                                             const int64_t *__restrict__ poff, int32_t M,
+                                                             uint16_t *__restrict__ arena, int32_t *__restrict__ bh,
+                                                             PlanTotals *__restrict__ tot) {
+  extern __shared__ uint32_t hist[];  // [M]
+  const int tid = threadIdx.x, b = blockIdx.x;
+  for (int32_t a = tid; a < M; a += kPlanThreads) hist[a] = 0;
+  __syncthreads();
+  const int32_t j0 = ub[b], j1 = ub[b + 1];
+  const int gl = tid % kUserGroup;
+  bool bad = false;
+  for (int32_t j = j0 + tid / kUserGroup; j < j1; j += kPlanThreads / kUserGroup) {
+    const int64_t s = up[j];
+    const int32_t l = int32_t(up[j + 1] - s), pl = (l + 7) & ~7;
+    uint16_t *o = arena + poff[j];
+    for (int32_t p = gl; p < pl; p += kUserGroup) {
+      uint16_t v = uint16_t(M);
+      if (p < l) {
+        const int32_t it = items[s + p];
+        if (uint32_t(it) < uint32_t(M)) {
+          atomicAdd(&hist[it], 1u);
+          v = uint16_t(it);
+        } else {
+          bad = true;
+        }
+      }
+      o[p] = v;
+    }
+  }
+  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
+  __syncthreads();
+  int32_t *row = bh + int64_t(b) * M;
+  for (int32_t a = tid; a < M; a += kPlanThreads) row[a] = int32_t(hist[a]);
+}
+
+// Column-wise exclusive prefix over the B block histograms (in place); rcnt[a] = column total.
+__global__ void k_batch_colscan(int32_t B, int32_t M, int32_t *__restrict__ bh, int32_t *__restrict__ rcnt) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  int32_t run = 0;
+  int32_t b = 0;
+  for (; b + 8 <= B; b += 8) {
+    int32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = bh[int64_t(b + k) * M + a];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      bh[int64_t(b + k) * M + a] = run;
+      run += v[k];
+    }
+  }
+  for (; b < B; b++) {
+    const int32_t v = bh[int64_t(b) * M + a];
+    bh[int64_t(b) * M + a] = run;
+    run += v;
+  }
+  rcnt[a] = run;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(const int64_t *__restrict__ up,
+                                                                const int32_t *__restrict__ items,
+                                                                const int32_t *__restrict__ ub,
+                                                                const int64_t *__restrict__ poff,
+                                                                const int64_t *__restrict__ row_ptr, int32_t M,
+                                                                const int32_t *__restrict__ bh,
+                                                                uint64_t *__restrict__ desc) {
+  extern __shared__ uint32_t next_pos[];  // [M] next free position of each row inside this block's share
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int32_t *row = bh + int64_t(b) * M;
+  for (int32_t a = tid; a < M; a += kPlanThreads) next_pos[a] = uint32_t(row_ptr[a] + row[a]);
+  __syncthreads();
+  const int32_t j0 = ub[b], j1 = ub[b + 1];
+  const int gl = tid % kUserGroup;
+  for (int32_t j = j0 + tid / kUserGroup; j < j1; j += kPlanThreads / kUserGroup) {
+    const int64_t s = up[j];
+    const int32_t l = int32_t(up[j + 1] - s);
+    const uint64_t d = (uint64_t(l) << 40) | uint64_t(poff[j]);
+    for (int32_t p = gl; p < l; p += kUserGroup) {
+      const int32_t it = items[s + p];
+      if (uint32_t(it) < uint32_t(M)) desc[atomicAdd(&next_pos[it], 1u)] = d;
+    }
+  }
+}
+
+// Chunks of a row: equal shares of its contributions, as many as its estimated pair work needs
+// (contributions x mean padded list length per contribution).  Heaviest rows first (sort by count).
+__global__ void k_batch_plan(const int32_t *__restrict__ rcnt, int32_t M, const PlanTotals *__restrict__ tot,
+                             int64_t n, uint32_t *__restrict__ key, int32_t *__restrict__ order,
+                             int32_t *__restrict__ row_nch, int32_t *__restrict__ row_split) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  const double lbar = n > 0 ? double(tot->sum_lpl) / double(n) : 0.0;
+  const int32_t c = rcnt[a];
+  int32_t nch = 0;
+  if (c > 0) {
+    const double w = double(c) * lbar;
+    nch = int32_t(min(double(c), max(1.0, ceil(w / double(kChunkWork)))));
+  }
+  key[a] = uint32_t(c);
+  order[a] = a;
+  row_nch[a] = nch;
+  row_split[a] = nch > 1 ? 1 : 0;
+}
+
+__global__ void k_batch_chunks(const int32_t *__restrict__ order, const int32_t *__restrict__ ord_nch,
+                               const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_ptr,
+                               const int32_t *__restrict__ split_slot, int32_t M, Chunk *__restrict__ chunks) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= M) return;
+  const int32_t nch = ord_nch[r];
+  if (nch == 0) return;
+  const int32_t a = order[r];
+  const int64_t c0 = row_ptr[a], cnt = row_ptr[a + 1] - c0;
+  const int32_t slot = nch > 1 ? split_slot[a] : -1;
+  for (int32_t j = 0; j < nch; j++)
+    chunks[ord_cbase[r] + j] = Chunk{a, slot, c0 + cnt * j / nch, c0 + cnt * (j + 1) / nch, 0};
+}
+
+__device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// ★ batch accumulate.  Per chunk (row a, contribution range): up to `db` descriptors per batch;
+// their group counts (8 ids per 16-B group) are block-scanned into LDS segment starts; walkers of S
+// lanes own equal contiguous group ranges and step S groups at a time, U 16-B loads in flight per
+// lane, the next step's loads issued before this step's atomics.  Pad ids (= M) land on the sink
+// counter acc[M], so the inner loop has no compares: per partner id one shift/mask and one
+// ds_add_u32.  Descriptors of the next batch are loaded while the current one is walked.
+template <int U, int S>
+__global__ __launch_bounds__(kAccThreads) void k_acc_batch(
+    const Chunk *__restrict__ chunks, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
+    const uint64_t *__restrict__ desc, const uint16_t *__restrict__ arena, int32_t M, int32_t db,
+    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump,
+    int64_t bump_cap, int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, uint32_t *__restrict__ staging,
+    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum) {
+  extern __shared__ uint32_t acc[];                                   // [M + 1]: counters, sink at M
+  int64_t *s_seg = reinterpret_cast<int64_t *>(acc + ((M + 2) & ~1));  // [db] arena group - group start
+  uint32_t *s_vst = reinterpret_cast<uint32_t *>(s_seg + db);          // [db + 1] group starts
+  __shared__ int32_t s_chunk;
+  __shared__ uint32_t s_wtot[kAccWaves];
+  __shared__ uint32_t s_wave[kAccWaves];
+  __shared__ uint64_t s_red[kAccWaves];
+  __shared__ int64_t s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n_chunks = tot->n_chunks;
+  const uint4 *A = reinterpret_cast<const uint4 *>(arena);
+  constexpr uint32_t kWalkers = kAccThreads / S;
+  const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
+  for (int32_t b = tid; b <= M; b += kAccThreads) acc[b] = 0;
+  for (;;) {
+    if (tid == 0) s_chunk = atomicAdd(queue, 1);
+    __syncthreads();
+    const int32_t ch = s_chunk;
+    if (ch >= n_chunks) break;
+    const Chunk c = chunks[ch];
+    uint64_t my_len = 0;
+    uint64_t d = (tid < db && c.begin + tid < c.end) ? desc[c.begin + tid] : 0;
+    for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
+      const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
+      uint32_t ng = 0;
+      int64_t gsrc = 0;
+      if (tid < nb) {
+        const uint32_t l = uint32_t(d >> 40);
+        my_len += l;
+        ng = (l + 7) >> 3;
+        gsrc = int64_t(d & kOffMask) >> 3;
+      }
+      const int64_t b1 = b0 + db;
+      d = (tid < db && b1 + tid < c.end) ? desc[b1 + tid] : 0;  // next batch, lands during the walk
+      const uint32_t incl = wave_incl_scan_u32(ng);
+      if (lane == 63) s_wtot[wave] = incl;
+      __syncthreads();
+      uint32_t pre = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < kAccWaves; w++) {
+        const uint32_t x = s_wtot[w];
+        pre += (w < wave) ? x : 0u;
+        total += x;
+      }
+      if (tid < nb) {
+        const uint32_t ex = pre + incl - ng;
+        s_vst[tid] = ex;
+        s_seg[tid] = gsrc - int64_t(ex);
+      }
+      if (tid == 0) s_vst[nb] = total;
+      __syncthreads();
+      const uint32_t lo = uint32_t((uint64_t(total) * q) / kWalkers);
+      const uint32_t hi = uint32_t((uint64_t(total) * (q + 1)) / kWalkers);
+      uint32_t g = lo + ql;
+      if (g < hi) {
+        int32_t l = 0, r = nb;
+        while (r - l > 1) {
+          const int32_t m = (l + r) >> 1;
+          if (s_vst[m] <= g) l = m; else r = m;
+        }
+        int32_t cur = l;
+        uint32_t next = s_vst[cur + 1];
+        int64_t base = s_seg[cur];
+        uint4 v[U];
+        bool ok[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+          const uint32_t gk = g + uint32_t(S) * k;
+          ok[k] = gk < hi;
+          if (ok[k]) {
+            while (gk >= next) {
+              cur++;
+              next = s_vst[cur + 1];
+              base = s_seg[cur];
+            }
+            v[k] = A[base + gk];
+          }
+        }
+        for (; g < hi; g += uint32_t(S) * U) {
+          uint4 vn[U];
+          bool okn[U];
+#pragma unroll
+          for (int k = 0; k < U; k++) {
+            const uint32_t gk = g + uint32_t(S) * (U + k);
+            okn[k] = gk < hi;
+            if (okn[k]) {
+              while (gk >= next) {
+                cur++;
+                next = s_vst[cur + 1];
+                base = s_seg[cur];
+              }
+              vn[k] = A[base + gk];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < U; k++) {
+            if (ok[k]) {
+              const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+              for (int h = 0; h < 4; h++) {
+                atomicAdd(&acc[w4[h] & 0xFFFFu], 1u);
+                atomicAdd(&acc[w4[h] >> 16], 1u);
+              }
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < U; k++) {
+            v[k] = vn[k];
+            ok[k] = okn[k];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // every contribution is a new position of item c.row: the -1 self term at column c.row
+    const int64_t n_c = c.end - c.begin;
+    const uint64_t len_sum = block_sum_u64(my_len, s_red);
+    const int64_t chunk_rowsum = int64_t(len_sum) - n_c;
+    if (tid == 0) {
+      acc[M] = 0;
+      acc[c.row] -= uint32_t(n_c);
+      atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
+      if (c.split >= 0)
+        atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
+    }
+    __syncthreads();
+    if (c.split < 0) {
+      uint64_t sum;
+      int64_t used;
+      const uint32_t nnz =
+          compact_row_ranges(acc, M, 0, col_out, cnt_out, Place{0, bump, bump_cap}, &used, &sum, s_wave, &s_base);
+      const uint64_t total = block_sum_u64(sum, s_red);
+      if (tid == 0) {
+        row_base[c.row] = used;
+        row_nnz[c.row] = int32_t(nnz);
+        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+      }
+    } else {
+      uint32_t *srow = staging + int64_t(c.split) * M;
+      for (int32_t b = tid; b < M; b += kAccThreads) {
+        const uint32_t v = acc[b];
+        if (v) {
+          atomicAdd(srow + b, v);
+          acc[b] = 0;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -717,14 +1086,47 @@ Status Counter::init(int32_t n_items) {
                         reinterpret_cast<const void *>(k_accumulate2<32, false>),
                         reinterpret_cast<const void *>(k_accumulate2<2, true>),
                         reinterpret_cast<const void *>(k_accumulate2<4, true>),
-                        reinterpret_cast<const void *>(k_accumulate2<8, true>)})
+                        reinterpret_cast<const void *>(k_accumulate2<8, true>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 1>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 2>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 3>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 8>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 16>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 32>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 3, 8>),
+                        reinterpret_cast<const void *>(k_accumulate2<8, true, 0, 8>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 7>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  if (n_items < kBatchMaxItems) {
+    const int acc_bytes = int(sizeof(uint32_t)) * ((n_items + 2) & ~1);
+    const int dbb = std::min(1024, (kLdsBudget - acc_bytes - 4) / 12);
+    const int lds_b = acc_bytes + dbb * 12 + 4;
+    for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<2, 4>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 4>),
+                          reinterpret_cast<const void *>(k_acc_batch<2, 8>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8>),
+                          reinterpret_cast<const void *>(k_acc_batch<8, 8>),
+                          reinterpret_cast<const void *>(k_acc_batch<2, 16>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 16>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 64>)})
+      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_b));
+    for (const void *k : {reinterpret_cast<const void *>(k_batch_hist), reinterpret_cast<const void *>(k_batch_scatter)})
+      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(sizeof(uint32_t)) * n_items));
+  }
+  const char *bs = getenv("COOC_BATCH_STRIDE");
+  bstride_ = bs ? atoi(bs) : 8;
+  const char *bu = getenv("COOC_BATCH_UNROLL");
+  bunroll_ = bu ? atoi(bu) : 4;
   const char *co = getenv("COOC_CHUNK_ORDER");
   chunk_order_ = co ? atoi(co) : 0;
   const char *vv = getenv("COOC_ACC_VEC");
   vec_allowed_ = !(vv && vv[0] == '0');
   const char *vu = getenv("COOC_ACC_VUNROLL");
   vunroll_ = vu ? atoi(vu) : 4;
+  const char *vx = getenv("COOC_ACC_X");
+  xmode_ = vx ? atoi(vx) : 0;
+  const char *vs = getenv("COOC_ACC_VSTRIDE");
+  vstride_ = vs ? atoi(vs) : 64;
   if (vunroll_ != 2 && vunroll_ != 8) vunroll_ = 4;
   const char *u = getenv("COOC_ACC_UNROLL");
   unroll_ = u ? atoi(u) : 16;
@@ -736,7 +1138,7 @@ Status Counter::init(int32_t n_items) {
 }
 
 void Counter::release() {
-  DevBuf *all[] = {&keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
+  DevBuf *all[] = {&bh_, &ub_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
                    &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_, &bump_, &seg_off_,
@@ -809,7 +1211,12 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
   // ★ accumulate
   const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
   if (timer && timer->enabled && col_off == 0) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  auto kern = vec_ ? (vunroll_ == 8 ? k_accumulate2<8, true> : vunroll_ == 2 ? k_accumulate2<2, true>
+  auto kern = vec_ ? (vstride_ == 8 ? (xmode_ == 3 ? k_accumulate2<4, true, 3, 8> : vunroll_ == 8 ? k_accumulate2<8, true, 0, 8>
+                                                                          : k_accumulate2<4, true, 0, 8>)
+                      : vstride_ == 16 ? k_accumulate2<4, true, 0, 16> : vstride_ == 32 ? k_accumulate2<4, true, 0, 32>
+                      : xmode_ == 7 ? k_accumulate2<4, true, 7>
+                      : xmode_ == 1 ? k_accumulate2<4, true, 1> : xmode_ == 2 ? k_accumulate2<4, true, 2>
+                      : xmode_ == 3 ? k_accumulate2<4, true, 3> : vunroll_ == 8 ? k_accumulate2<8, true> : vunroll_ == 2 ? k_accumulate2<2, true>
                                                               : k_accumulate2<4, true>)
                     : (unroll_ == 32 ? k_accumulate2<32, false>
                        : unroll_ == 8 ? k_accumulate2<8, false>
@@ -1041,7 +1448,7 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
     out_col = col2_.as<int32_t>();
     out_cnt = cnt2_.as<uint32_t>();
   }
-  k_nnz_total<<<1, 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
+  k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
   COOC_HIP_TRY(hipGetLastError());
 
   out->row_base = row_base_.as<int64_t>();
@@ -1083,6 +1490,184 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
   *row_ptr = pk_row_ptr_.as<int64_t>();
   *col = pk_col_.as<int32_t>();
   *cnt = pk_cnt_.as<uint32_t>();
+  return Status::Ok();
+}
+
+Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
+                          CountResult *out, KernelTimer *timer) {
+  const int32_t M = M_;
+  if (!batch_ok()) return Status{1, "run_batch needs n_items < " + std::to_string(kBatchMaxItems)};
+  if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
+  if (U > int64_t(INT32_MAX)) return Status{1, "more than 2^31 users in one window"};
+  const int32_t B = int32_t(std::max<int64_t>(1, std::min<int64_t>(n_cu_, std::max<int64_t>(U, 1))));
+  const int64_t U1 = std::max<int64_t>(U, 1);
+  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
+  COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
+  COOC_TRY(plen_.reserve(sizeof(int64_t) * U1));
+  COOC_TRY(poff_.reserve(sizeof(int64_t) * (U1 + 1)));
+  COOC_TRY(ub_.reserve(sizeof(int32_t) * (B + 1)));
+  COOC_TRY(bh_.reserve(sizeof(int32_t) * size_t(B) * M));
+  COOC_TRY(rcnt_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(desc_.reserve(sizeof(uint64_t) * (n + 1)));
+  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(order_.reserve(sizeof(int32_t) * M * 2));
+  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(row_split_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (M + 1)));
+  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * (M + 1)));
+  COOC_TRY(split_row_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
+  COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
+  PlanTotals *tot = tot_.as<PlanTotals>();
+  int64_t *plen = plen_.as<int64_t>(), *poff = poff_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
+  int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *ub = ub_.as<int32_t>();
+  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
+  COOC_HIP_TRY(hipMemsetAsync(queue_.p, 0, sizeof(int32_t) * 4, s));
+  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * M, s));
+  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * M, s));
+  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t) * (M + 1), s));
+  COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
+  COOC_HIP_TRY(hipMemsetAsync(poff, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(row_ptr, 0, sizeof(int64_t), s));
+  if (U > 0) {
+    k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, plen, tot);
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  // hipCUB temp storage for every scan / sort of the plan
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> cnt64(rcnt, WidenI64{});
+  size_t tmp = 0, q = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, poff + 1, int(U1), s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, cnt64, row_ptr + 1, M, s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint32_t>(),
+                                                            order_keys_.as<uint32_t>(), order_.as<int32_t>() + M,
+                                                            order_.as<int32_t>(), M, 0, 32, s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, M, s));
+  tmp = std::max(tmp, q);
+  COOC_TRY(sort_tmp_.reserve(tmp));
+  if (U > 0) {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, poff + 1, int(U), s));
+  }
+  // padded arena: every list 16-B aligned and padded to 8 ids with the sink id M; one pad group
+  // at the end (never referenced by a segment, keeps the last 16-B load in bounds)
+  const int64_t arena_cap = n + 7 * U1 + 16;
+  COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
+  k_batch_bounds<<<blocks_for(B + 1, 256), 256, 0, s>>>(U, up, B, ub);
+  const size_t lds_m = sizeof(uint32_t) * size_t(M);
+  if (U > 0) {
+    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(up, items, ub, poff, M, tarena_.as<uint16_t>(), bh, tot);
+    k_batch_colscan<<<blocks_for(M, 256), 256, 0, s>>>(B, M, bh, rcnt);
+  } else {
+    COOC_HIP_TRY(hipMemsetAsync(rcnt, 0, sizeof(int32_t) * M, s));
+  }
+  COOC_HIP_TRY(hipGetLastError());
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt64, row_ptr + 1, M, s));
+  }
+  if (U > 0) {
+    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(up, items, ub, poff, row_ptr, M, bh, desc_.as<uint64_t>());
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  // chunk plan: rows by contribution count, heaviest first
+  int32_t *order = order_.as<int32_t>();
+  k_batch_plan<<<blocks_for(M, 256), 256, 0, s>>>(rcnt, M, tot, n, row_work_.as<uint32_t>(), order + M,
+                                                  row_nch_.as<int32_t>(), row_split_.as<int32_t>());
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint32_t>(),
+                                                              order_keys_.as<uint32_t>(), order + M, order, M, 0,
+                                                              32, s));
+  }
+  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
+  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
+                                                  M, s));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
+                                                  split_slot_.as<int32_t>() + 1, M, s));
+  }
+  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
+                                                  split_row_.as<int32_t>());
+  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>(), M, tot, queue_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+  if (h_tot_->max_len >= (int64_t(1) << 24)) return Status{1, "a user history longer than 2^24 items"};
+  const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
+  const int64_t work_total = h_tot_->sum_l2;
+  const int64_t pairs = work_total - n;
+  // output region: distinct keys <= min(M^2, ordered pairs)
+  bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(int64_t(M) * M, pairs));
+  COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
+  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
+  bump_mode_ = false;  // the bump region IS the output (one column tile): no gather
+  if (n_chunks > 0) {
+    COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
+    COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
+    COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
+    if (n_split > 0) {
+      const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
+      COOC_TRY(staging_.reserve(need));
+      COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
+    }
+    k_batch_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
+                                                      row_ptr, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
+    COOC_HIP_TRY(hipGetLastError());
+    const size_t acc_bytes = sizeof(uint32_t) * size_t((M + 2) & ~1);
+    const int db = int(std::min<int64_t>(1024, (int64_t(kLdsBudget) - int64_t(acc_bytes) - 4) / 12));
+    if (db < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
+    const size_t lds = acc_bytes + size_t(db) * 12 + 4;
+    const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
+    auto kern = bstride_ == 16 ? (bunroll_ == 2 ? k_acc_batch<2, 16> : k_acc_batch<4, 16>)
+              : bstride_ == 4  ? (bunroll_ == 2 ? k_acc_batch<2, 4> : k_acc_batch<4, 4>)
+              : bstride_ == 64 ? k_acc_batch<4, 64>
+                               : (bunroll_ == 2 ? k_acc_batch<2, 8> : bunroll_ == 8 ? k_acc_batch<8, 8>
+                                                                                    : k_acc_batch<4, 8>);
+    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+    kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(),
+                                                  desc_.as<uint64_t>(), tarena_.as<uint16_t>(), M, db,
+                                                  col_.as<int32_t>(), cnt_.as<uint32_t>(),
+                                                  bump_.as<unsigned long long>(), bump_cap_, row_base_.as<int64_t>(),
+                                                  row_nnz_.as<int32_t>(), staging_.as<uint32_t>(),
+                                                  split_sum_.as<int64_t>(), rowsum_.as<int64_t>());
+    COOC_HIP_TRY(hipGetLastError());
+    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+    if (n_split > 0) {
+      const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
+      k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(
+          tot, split_row_.as<int32_t>(), M, 0, staging_.as<uint32_t>(), row_base_.as<int64_t>(),
+          row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(), split_sum_.as<int64_t>(),
+          reinterpret_cast<int64_t *>(&tot->err), bump_.as<unsigned long long>(), bump_cap_,
+          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), 1, 0);
+      COOC_HIP_TRY(hipGetLastError());
+    }
+  } else if (timer && timer->enabled) {
+    COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+    COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+  }
+  k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
+  COOC_HIP_TRY(hipGetLastError());
+  out->row_base = row_base_.as<int64_t>();
+  out->row_nnz = row_nnz_.as<int32_t>();
+  out->col = col_.as<int32_t>();
+  out->cnt = cnt_.as<uint32_t>();
+  out->rowsum = rowsum_.as<int64_t>();
+  out->work = work_total;
+  out->observed = pairs;
+  out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
   return Status::Ok();
 }
 

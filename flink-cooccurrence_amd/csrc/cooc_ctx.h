@@ -97,6 +97,9 @@ struct cooc_ctx {
 
   cooc::Status count_device(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
                             hipStream_t s, cooc_device_result *out);
+  cooc::Status count_general(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                             int64_t n_interactions, hipStream_t s, cooc::CountResult *r);
+  cooc::Status finish_batch(const cooc::CountResult &r, hipStream_t s, cooc_device_result *out);
   cooc::Status count_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_window_info *info);
   cooc::Status copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                           int32_t *rowsum32);

@@ -86,7 +86,11 @@ struct PlanTotals {
   int64_t work_total; // sum over contributions of segment length (ordered pairs + self terms)
   int64_t nnz_total;  // filled after the run
   int64_t err;        // bit 0: item id out of range, bit 1: uint32 count overflow
-  int64_t pad[2];
+  // batch planner (run_batch) statistics of the user histories
+  int64_t sum_l2;     // sum_u n_u^2  (= ordered pairs + self terms)
+  int64_t sum_lpl;    // sum_u n_u * pad8(n_u): padded partner ids read
+  int64_t max_len;    // longest history
+  int64_t pad;
 };
 
 // Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
@@ -116,6 +120,15 @@ class Counter {
   // Expand + reduce the given contributions; returns the padded CSR.  Synchronises `stream`
   // once (to size the output).
   Status run(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
+
+  // One window over empty histories straight from a device CSR (user_ptr int64[U+1], items
+  // int32[N]): the batch planner (per-block item histograms -> transpose of A by counting sort) and
+  // k_acc_batch.  Needs n_items <= 40,703 (one LDS row plus the pad sink); returns the same padded
+  // CSR as run().  Synchronises `stream` once (to size chunks and the output region).
+  Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
+                   CountResult *out, KernelTimer *timer = nullptr);
+  bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems; }
+  static constexpr int32_t kBatchMaxItems = 40704;
 
   // Pack the padded CSR of the last run into contiguous CSR (device), for copy-out.
   Status pack(hipStream_t stream, int64_t **row_ptr, int32_t **col, uint32_t **cnt);
@@ -149,8 +162,12 @@ class Counter {
   int64_t bump_cap_ = 0;
   DevBuf bump_, seg_off_, seg_nnz_, col2_, cnt2_;
   bool vec_ = false, vec_allowed_ = true;  // 16-B partner-id loads over a padded arena (batch, one tile)
+  int vstride_ = 64;                       // COOC_ACC_VSTRIDE: lanes per walker of the VEC path (8, 16, 32, 64)
+  int xmode_ = 0;                          // COOC_ACC_X: experiment modes of k_accumulate2 (bench only)
   int vunroll_ = 4;                        // COOC_ACC_VUNROLL: 16-B loads in flight per lane (2, 4, 8)
   DevBuf plen_, poff_, vpre_;
+  DevBuf bh_, ub_, rcnt_, desc_;      // batch planner: block histograms, user bounds, row counts, descriptors
+  int bstride_ = 8, bunroll_ = 4;     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

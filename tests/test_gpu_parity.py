@@ -41,7 +41,9 @@ def _batch_vs_closed_form(pkg, oracle, up, it, M):
     (1, 500, 97, 12.0, True),
     (2, 3000, 1000, 20.0, True),      # C1 shape, scaled
     (3, 2000, 4096, 40.0, False),     # rating-log shape
-    (4, 300, 40704, 60.0, True),      # the largest single-tile LDS row
+    (4, 300, 40704, 60.0, True),      # the largest single-tile LDS row (general planner)
+    (6, 300, 40703, 60.0, True),      # the largest batch-planner row (+ pad sink)
+    (7, 5000, 2000, 150.0, False),    # long lists, many batches per chunk
 ])
 def test_batch_random_logs(pkg, oracle, torch_cuda, seed, U, M, mean, repl):
     from flink_cooccurrence_amd import datagen
