@@ -21,6 +21,8 @@ COOC_ERR_HIP = 3
 COOC_ERR_OOM = 4
 COOC_ERR_OVERFLOW = 5
 COOC_FLAG_EXACT_SCORES = 1
+COOC_FLAG_OUTPUT_CSR = 2
+COOC_FLAG_OUTPUT_DENSE = 4
 
 i16p = ctypes.POINTER(ctypes.c_int16)
 i32p = ctypes.POINTER(ctypes.c_int32)
@@ -62,6 +64,7 @@ class CoocDeviceResult(ctypes.Structure):
         ("col", vp),
         ("cnt", vp),
         ("rowsum", vp),
+        ("dense", vp),
     ]
 
 

@@ -76,9 +76,14 @@ class CooccurrenceCore:
     """One context of the C-ABI (one Flink subtask)."""
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
-                 exact_scores: bool = False):
+                 exact_scores: bool = False, output: str = "auto"):
+        """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2)."""
         L = _lib.load()
-        cfg = CoocConfig(device, n_items, topk, _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0, window_size_ms)
+        flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
+        if output not in ("auto", "csr", "dense"):
+            raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown output layout {output!r}")
+        flags |= {"auto": 0, "csr": _lib.COOC_FLAG_OUTPUT_CSR, "dense": _lib.COOC_FLAG_OUTPUT_DENSE}[output]
+        cfg = CoocConfig(device, n_items, topk, flags, window_size_ms)
         h = ctypes.c_void_p()
         check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
         self._h = h

@@ -224,6 +224,7 @@ int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part, const in
   out->col = m.col;
   out->cnt = m.cnt;
   out->rowsum = m.rowsum;
+  out->dense = nullptr;
   return COOC_OK;
 }
 

@@ -32,6 +32,7 @@ constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances h
 constexpr int kMaxLdsCounters = 40704;            // dense row in LDS (uint32 counters)
 constexpr int kTileMax = 32768;                   // column tile width when n_items exceeds one LDS row
 constexpr int kLdsBudget = 160 * 1024 - 512;      // dynamic LDS left after the kernels' static LDS
+constexpr int kBatchLdsBudget = 160 * 1024 - 1536;  // k_acc_batch: its static LDS is under 1.5 KB
 
 template <class T>
 __device__ inline int64_t lower_bound_i64(const T *a, int64_t n, T x) {
@@ -304,7 +305,9 @@ struct Place {
   int64_t bump_cap;          // entries in the bump region
 };
 
-template <class Src>
+// kStore: 0 = no stores (experiments), 1 = plain stores, 2 = sc1 stores (written through, the lines
+// dropped from the XCD's L2 so that the output does not evict the partner-id working set), 3 = nt.
+template <class Src, int kStore = 1>
 __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_off, int32_t *__restrict__ col_out,
                                               uint32_t *__restrict__ cnt_out, Place place, int64_t *base_used,
                                               uint64_t *sum, uint32_t *s_wave, int64_t *s_base) {
@@ -342,10 +345,18 @@ __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_o
     const uint32_t v = b < hi ? row[b] : 0u;
     const uint64_t m = __ballot(v != 0u);
     if (v) {
-      if (write) {
+      if (kStore && write) {
         const int64_t pos = out_base + off + uint32_t(__popcll(m & lt_mask));
-        col_out[pos] = col_off + b;
-        cnt_out[pos] = v;
+        if (kStore == 2) {
+          __hip_atomic_store(col_out + pos, col_off + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cnt_out + pos, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (kStore == 3) {
+          __builtin_nontemporal_store(col_off + b, col_out + pos);
+          __builtin_nontemporal_store(v, cnt_out + pos);
+        } else {
+          col_out[pos] = col_off + b;
+          cnt_out[pos] = v;
+        }
       }
       row[b] = 0;
       my_sum += v;
@@ -673,14 +684,17 @@ __global__ void k_iota_users(int64_t n, const int64_t *__restrict__ user_ptr, in
 // ==== batch planner: one window over empty histories, straight from the CSR of user histories =====
 // A contribution is (row a, user u) for every interaction (u, a): row a adds u's whole list, then
 // -1 at column a (NonSampled...java:129-161 with an empty resident history).  The planner builds
-// the row-grouped contribution list as the transpose of A by a counting sort, in 4 passes over N:
-//   k_batch_users   padded lengths pad8(n_u), sum n_u^2, sum n_u pad8(n_u), max n_u
-//   k_batch_hist    per-block LDS histogram of items + the padded u16 arena (pad id = M: sink slot)
-//   k_batch_colscan per-item exclusive prefix over the block histograms -> per-block row offsets
-//   k_batch_scatter contribution descriptors (n_u << 40 | arena offset) at their row positions
+// the row-grouped contribution list as the transpose of A by a counting sort.  Every pass over the
+// N interactions is flat (coalesced, balanced whatever the list lengths):
+//   k_batch_users    padded lengths pad8(n_u), sum n_u^2, sum n_u pad8(n_u), max n_u
+//   k_batch_fill     user index of every interaction (uidx) + the pads of the u16 arena (pad id = M)
+//   k_batch_hist     per-block LDS histogram of items over a fixed interaction range + the arena
+//   k_batch_colscan  per-item exclusive prefix over the block histograms -> per-block row offsets
+//   k_batch_scatter  contribution descriptors (n_u << 40 | arena offset) at their row positions
 // and no per-contribution prefix sums: k_acc_batch scans segment lengths inside the workgroup.
 constexpr int kPlanThreads = 1024;
-constexpr int kUserGroup = 16;  // lanes per user in the planner passes (4 users per wave)
+constexpr int kPlanUnroll = 4;       // interactions per thread per step of hist / scatter
+constexpr int32_t kFillThread = 2048;  // longer lists get a workgroup each in k_batch_fill_long
 constexpr uint64_t kOffMask = (uint64_t(1) << 40) - 1;
 
 __global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *__restrict__ up,
@@ -722,18 +736,49 @@ __global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *_
   }
 }
 
-// Users of partition block b: [ub[b], ub[b+1]), cut where the interaction prefix crosses N*b/B.
-__global__ void k_batch_bounds(int64_t U, const int64_t *__restrict__ up, int32_t B, int32_t *__restrict__ ub) {
-  const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > B) return;
-  const int64_t N = up[U];
-  const int64_t target = (b == B) ? N + 1 : (N * b) / B;
-  ub[b] = b == B ? int32_t(U) : int32_t(lower_bound_i64<int64_t>(up, U, target));
+// One thread per user: uidx[up[j] .. up[j+1]) = j (16-B stores where aligned) and the arena pads
+// [n_j, pad8(n_j)).  Lists longer than kFillThread are queued for k_batch_fill_long.
+__global__ __launch_bounds__(256) void k_batch_fill(int64_t U, const int64_t *__restrict__ up,
+                                                    const int64_t *__restrict__ poff, int32_t M,
+                                                    int32_t *__restrict__ uidx, uint16_t *__restrict__ arena,
+                                                    int32_t *__restrict__ long_list, PlanTotals *__restrict__ tot) {
+  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= U) return;
+  const int64_t s = up[j], l = up[j + 1] - s, o = poff[j];
+  for (int64_t i = l; i < ((l + 7) & ~int64_t(7)); i++) arena[o + i] = uint16_t(M);
+  if (l > kFillThread) {
+    long_list[atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_long), 1ull)] = int32_t(j);
+    return;
+  }
+  const int32_t v = int32_t(j);
+  int64_t p = s;
+  const int64_t e = s + l;
+  for (; p < e && (p & 3); p++) uidx[p] = v;
+  for (; p + 4 <= e; p += 4) *reinterpret_cast<int4 *>(uidx + p) = make_int4(v, v, v, v);
+  for (; p < e; p++) uidx[p] = v;
 }
 
-__global__ __launch_bounds__(kPlanThreads) void k_batch_hist(const int64_t *__restrict__ up,
+__global__ __launch_bounds__(256) void k_batch_fill_long(const int64_t *__restrict__ up,
+                                                         const int32_t *__restrict__ long_list,
+                                                         const PlanTotals *__restrict__ tot,
+                                                         int32_t *__restrict__ uidx) {
+  const int64_t n_long = tot->n_long;
+  for (int64_t k = blockIdx.x; k < n_long; k += gridDim.x) {
+    const int32_t j = long_list[k];
+    const int64_t s = up[j], e = up[j + 1];
+    for (int64_t p = s + threadIdx.x; p < e; p += blockDim.x) uidx[p] = j;
+  }
+}
+
+// Interaction range of partition block b (the same in hist and scatter).
+__device__ inline void block_range(int64_t n, int32_t B, int32_t b, int64_t *p0, int64_t *p1) {
+  *p0 = n * b / B;
+  *p1 = n * (b + 1) / B;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_batch_hist(int64_t n, int32_t B, const int64_t *__restrict__ up,
                                                              const int32_t *__restrict__ items,
-                                                             const int32_t *__restrict__ ub,
+                                                             const int32_t *__restrict__ uidx,
                                                              const int64_t *__restrict__ poff, int32_t M,
                                                              uint16_t *__restrict__ arena, int32_t *__restrict__ bh,
                                                              PlanTotals *__restrict__ tot) {
@@ -741,25 +786,34 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_hist(const int64_t *__re
   const int tid = threadIdx.x, b = blockIdx.x;
   for (int32_t a = tid; a < M; a += kPlanThreads) hist[a] = 0;
   __syncthreads();
-  const int32_t j0 = ub[b], j1 = ub[b + 1];
-  const int gl = tid % kUserGroup;
+  int64_t p0, p1;
+  block_range(n, B, b, &p0, &p1);
   bool bad = false;
-  for (int32_t j = j0 + tid / kUserGroup; j < j1; j += kPlanThreads / kUserGroup) {
-    const int64_t s = up[j];
-    const int32_t l = int32_t(up[j + 1] - s), pl = (l + 7) & ~7;
-    uint16_t *o = arena + poff[j];
-    for (int32_t p = gl; p < pl; p += kUserGroup) {
+  for (int64_t pb = p0; pb < p1; pb += int64_t(kPlanThreads) * kPlanUnroll) {
+    int32_t it[kPlanUnroll], j[kPlanUnroll];
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++) {
+      const int64_t p = pb + k * kPlanThreads + tid;
+      it[k] = p < p1 ? items[p] : -1;
+      j[k] = p < p1 ? uidx[p] : -1;
+    }
+    int64_t dst[kPlanUnroll];
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++) {
+      const int64_t p = pb + k * kPlanThreads + tid;
+      dst[k] = j[k] >= 0 ? poff[j[k]] + (p - up[j[k]]) : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++) {
+      if (dst[k] < 0) continue;
       uint16_t v = uint16_t(M);
-      if (p < l) {
-        const int32_t it = items[s + p];
-        if (uint32_t(it) < uint32_t(M)) {
-          atomicAdd(&hist[it], 1u);
-          v = uint16_t(it);
-        } else {
-          bad = true;
-        }
+      if (uint32_t(it[k]) < uint32_t(M)) {
+        atomicAdd(&hist[it[k]], 1u);
+        v = uint16_t(it[k]);
+      } else {
+        bad = true;
       }
-      o[p] = v;
+      arena[dst[k]] = v;
     }
   }
   if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
@@ -792,9 +846,9 @@ __global__ void k_batch_colscan(int32_t B, int32_t M, int32_t *__restrict__ bh, 
   rcnt[a] = run;
 }
 
-__global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(const int64_t *__restrict__ up,
+__global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(int64_t n, int32_t B, const int64_t *__restrict__ up,
                                                                 const int32_t *__restrict__ items,
-                                                                const int32_t *__restrict__ ub,
+                                                                const int32_t *__restrict__ uidx,
                                                                 const int64_t *__restrict__ poff,
                                                                 const int64_t *__restrict__ row_ptr, int32_t M,
                                                                 const int32_t *__restrict__ bh,
@@ -804,16 +858,23 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(const int64_t *_
   const int32_t *row = bh + int64_t(b) * M;
   for (int32_t a = tid; a < M; a += kPlanThreads) next_pos[a] = uint32_t(row_ptr[a] + row[a]);
   __syncthreads();
-  const int32_t j0 = ub[b], j1 = ub[b + 1];
-  const int gl = tid % kUserGroup;
-  for (int32_t j = j0 + tid / kUserGroup; j < j1; j += kPlanThreads / kUserGroup) {
-    const int64_t s = up[j];
-    const int32_t l = int32_t(up[j + 1] - s);
-    const uint64_t d = (uint64_t(l) << 40) | uint64_t(poff[j]);
-    for (int32_t p = gl; p < l; p += kUserGroup) {
-      const int32_t it = items[s + p];
-      if (uint32_t(it) < uint32_t(M)) desc[atomicAdd(&next_pos[it], 1u)] = d;
+  int64_t p0, p1;
+  block_range(n, B, b, &p0, &p1);
+  for (int64_t pb = p0; pb < p1; pb += int64_t(kPlanThreads) * kPlanUnroll) {
+    int32_t it[kPlanUnroll], j[kPlanUnroll];
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++) {
+      const int64_t p = pb + k * kPlanThreads + tid;
+      it[k] = p < p1 ? items[p] : -1;
+      j[k] = p < p1 ? uidx[p] : -1;
     }
+    uint64_t d[kPlanUnroll];
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++)
+      d[k] = j[k] >= 0 ? (uint64_t(up[j[k] + 1] - up[j[k]]) << 40) | uint64_t(poff[j[k]]) : 0;
+#pragma unroll
+    for (int k = 0; k < kPlanUnroll; k++)
+      if (uint32_t(it[k]) < uint32_t(M)) desc[atomicAdd(&next_pos[it[k]], 1u)] = d[k];
   }
 }
 
@@ -863,17 +924,25 @@ __device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
 
 // ★ batch accumulate.  Per chunk (row a, contribution range): up to `db` descriptors per batch;
 // their group counts (8 ids per 16-B group) are block-scanned into LDS segment starts; walkers of S
-// lanes own equal contiguous group ranges and step S groups at a time, U 16-B loads in flight per
-// lane, the next step's loads issued before this step's atomics.  Pad ids (= M) land on the sink
-// counter acc[M], so the inner loop has no compares: per partner id one shift/mask and one
-// ds_add_u32.  Descriptors of the next batch are loaded while the current one is walked.
-template <int U, int S>
+// lanes own equal contiguous group ranges (start segment from a table written by the scan) and
+// step S groups at a time, U 16-B loads in flight per lane, the next step's loads issued before this
+// step's atomics.  Pad ids (= M) land on the sink counter acc[M], so the inner loop has no
+// compares: per partner id one shift/mask and one ds_add_u32.  Latency hiding across chunks: the
+// next chunk is dequeued when a chunk starts, and its descriptor and first descriptor batch are
+// loaded before this chunk's compaction.
+// Output: DENSE = the counts as a dense row-major uint32 [M x M] matrix in HBM (row a written whole
+// from LDS with coalesced stores; split rows add their chunks into the zeroed dense row with
+// global atomics); otherwise the column-order sparse compaction into a bump-allocated padded CSR.
+// X (experiments only, never the default): bit 2 = skip the walk, bit 3 = compaction without stores.
+// ST: sparse output store flavour (compact_row_ranges kStore).
+template <int U, int S, bool DENSE, int X = 0, int ST = 1>
 __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
     const Chunk *__restrict__ chunks, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const uint64_t *__restrict__ desc, const uint16_t *__restrict__ arena, int32_t M, int32_t db,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump,
     int64_t bump_cap, int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, uint32_t *__restrict__ staging,
-    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum) {
+    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, uint32_t *__restrict__ dense) {
+  constexpr uint32_t kWalkers = kAccThreads / S;
   extern __shared__ uint32_t acc[];                                   // [M + 1]: counters, sink at M
   int64_t *s_seg = reinterpret_cast<int64_t *>(acc + ((M + 2) & ~1));  // [db] arena group - group start
   uint32_t *s_vst = reinterpret_cast<uint32_t *>(s_seg + db);          // [db + 1] group starts
@@ -882,20 +951,21 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
   __shared__ uint32_t s_wave[kAccWaves];
   __shared__ uint64_t s_red[kAccWaves];
   __shared__ int64_t s_base;
+  __shared__ int32_t s_qstart[kWalkers];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_chunks = tot->n_chunks;
   const uint4 *A = reinterpret_cast<const uint4 *>(arena);
-  constexpr uint32_t kWalkers = kAccThreads / S;
   const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
   for (int32_t b = tid; b <= M; b += kAccThreads) acc[b] = 0;
-  for (;;) {
-    if (tid == 0) s_chunk = atomicAdd(queue, 1);
-    __syncthreads();
-    const int32_t ch = s_chunk;
-    if (ch >= n_chunks) break;
-    const Chunk c = chunks[ch];
+  if (tid == 0) s_chunk = atomicAdd(queue, 1);
+  __syncthreads();
+  int32_t ch = s_chunk;
+  Chunk c = ch < n_chunks ? chunks[ch] : Chunk{0, -1, 0, 0, 0};
+  uint64_t d = (tid < db && c.begin + tid < c.end) ? desc[c.begin + tid] : 0;
+  while (ch < n_chunks) {
+    int32_t nxt = 0;
+    if (tid == 0) nxt = atomicAdd(queue, 1);  // lands while this chunk is walked
     uint64_t my_len = 0;
-    uint64_t d = (tid < db && c.begin + tid < c.end) ? desc[c.begin + tid] : 0;
     for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
       const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
       uint32_t ng = 0;
@@ -922,19 +992,18 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         const uint32_t ex = pre + incl - ng;
         s_vst[tid] = ex;
         s_seg[tid] = gsrc - int64_t(ex);
+        // walkers whose range starts inside this segment: lo_q = floor(total q / kWalkers) in [ex, ex + ng)
+        const uint32_t q0 = uint32_t((uint64_t(ex) * kWalkers + total - 1) / total);
+        const uint32_t q1 = uint32_t((uint64_t(ex + ng) * kWalkers + total - 1) / total);
+        for (uint32_t w = q0; w < q1 && w < kWalkers; w++) s_qstart[w] = tid;
       }
       if (tid == 0) s_vst[nb] = total;
       __syncthreads();
       const uint32_t lo = uint32_t((uint64_t(total) * q) / kWalkers);
       const uint32_t hi = uint32_t((uint64_t(total) * (q + 1)) / kWalkers);
       uint32_t g = lo + ql;
-      if (g < hi) {
-        int32_t l = 0, r = nb;
-        while (r - l > 1) {
-          const int32_t m = (l + r) >> 1;
-          if (s_vst[m] <= g) l = m; else r = m;
-        }
-        int32_t cur = l;
+      if (!(X & 4) && g < hi) {
+        int32_t cur = s_qstart[q];
         uint32_t next = s_vst[cur + 1];
         int64_t base = s_seg[cur];
         uint4 v[U];
@@ -988,10 +1057,14 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       }
       __syncthreads();
     }
+    if (tid == 0) s_chunk = nxt;
     // every contribution is a new position of item c.row: the -1 self term at column c.row
     const int64_t n_c = c.end - c.begin;
-    const uint64_t len_sum = block_sum_u64(my_len, s_red);
+    const uint64_t len_sum = block_sum_u64(my_len, s_red);  // (its barriers publish s_chunk)
     const int64_t chunk_rowsum = int64_t(len_sum) - n_c;
+    const int32_t ch2 = s_chunk;
+    const Chunk c2 = ch2 < n_chunks ? chunks[ch2] : Chunk{0, -1, 0, 0, 0};
+    const uint64_t d2 = (tid < db && c2.begin + tid < c2.end) ? desc[c2.begin + tid] : 0;
     if (tid == 0) {
       acc[M] = 0;
       acc[c.row] -= uint32_t(n_c);
@@ -1000,16 +1073,44 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
     }
     __syncthreads();
-    if (c.split < 0) {
+    if (DENSE && c.split < 0) {
+      uint32_t *dst = dense + int64_t(c.row) * M;
+      uint64_t sum = 0;
+      uint32_t nnz = 0;
+      for (int32_t b = tid; b < M; b += kAccThreads) {
+        const uint32_t v = acc[b];
+        if (!(X & 8)) dst[b] = v;
+        acc[b] = 0;
+        sum += v;
+        nnz += v != 0u;
+      }
+      // a row sum fits 40 bits (uint32 counts over < 2^8 columns per thread), nnz < 2^16 per thread
+      const uint64_t both = block_sum_u64((sum << 24) | uint64_t(nnz), s_red);
+      if (tid == 0) {
+        row_nnz[c.row] = int32_t(both & 0xFFFFFFu);
+        if (X == 0 && (both >> 24) != uint64_t(chunk_rowsum))
+          atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+      }
+    } else if (DENSE) {
+      uint32_t *dst = dense + int64_t(c.row) * M;  // zeroed before the launch; k_dense_split_check closes it
+      for (int32_t b = tid; b < M; b += kAccThreads) {
+        const uint32_t v = acc[b];
+        if (v) {
+          atomicAdd(dst + b, v);
+          acc[b] = 0;
+        }
+      }
+    } else if (c.split < 0) {
       uint64_t sum;
       int64_t used;
-      const uint32_t nnz =
-          compact_row_ranges(acc, M, 0, col_out, cnt_out, Place{0, bump, bump_cap}, &used, &sum, s_wave, &s_base);
+      const uint32_t nnz = compact_row_ranges<uint32_t, (X & 8) ? 0 : ST>(
+          acc, M, 0, col_out, cnt_out, Place{0, bump, bump_cap}, &used, &sum, s_wave, &s_base);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
         row_base[c.row] = used;
         row_nnz[c.row] = int32_t(nnz);
-        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+        if (X == 0 && total != uint64_t(chunk_rowsum))
+          atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
       }
     } else {
       uint32_t *srow = staging + int64_t(c.split) * M;
@@ -1020,6 +1121,93 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
           acc[b] = 0;
         }
       }
+    }
+    __syncthreads();
+    ch = ch2;
+    c = c2;
+    d = d2;
+  }
+}
+
+// Dense output: rows of items without interactions (no chunk) are zero; one wave per row.
+__global__ void k_zero_empty_rows(const int32_t *__restrict__ rcnt, int32_t M, uint32_t *__restrict__ dense) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = wave; a < M; a += n_waves) {
+    if (rcnt[a] != 0) continue;
+    uint32_t *d = dense + a * M;
+    for (int32_t b = lane; b < M; b += 64) d[b] = 0;
+  }
+}
+
+// Dense output: the rows that several chunks add into start at zero.
+__global__ void k_zero_rows(const int32_t *__restrict__ rows, const PlanTotals *__restrict__ tot, int32_t M,
+                            uint32_t *__restrict__ dense) {
+  const int64_t n = tot->n_split;
+  for (int64_t s = blockIdx.x; s < n; s += gridDim.x) {
+    uint32_t *d = dense + int64_t(rows[s]) * M;
+    for (int32_t b = threadIdx.x; b < M; b += blockDim.x) d[b] = 0;
+  }
+}
+
+// Dense output, split rows: entries and the overflow check (row sum == the chunks' closed form).
+__global__ __launch_bounds__(kAccThreads) void k_dense_split_check(const int32_t *__restrict__ split_row,
+                                                                   PlanTotals *__restrict__ tot, int32_t M,
+                                                                   const uint32_t *__restrict__ dense,
+                                                                   int64_t *__restrict__ split_sum,
+                                                                   int32_t *__restrict__ row_nnz) {
+  __shared__ uint64_t s_red[kAccWaves];
+  const int64_t n = tot->n_split;
+  for (int64_t s = blockIdx.x; s < n; s += gridDim.x) {
+    const int32_t a = split_row[s];
+    const uint32_t *d = dense + int64_t(a) * M;
+    uint64_t sum = 0;
+    uint32_t nnz = 0;
+    for (int32_t b = threadIdx.x; b < M; b += kAccThreads) {
+      const uint32_t v = d[b];
+      sum += v;
+      nnz += v != 0u;
+    }
+    const uint64_t both = block_sum_u64((sum << 24) | uint64_t(nnz), s_red);
+    if (threadIdx.x == 0) {
+      row_nnz[a] = int32_t(both & 0xFFFFFFu);
+      if ((both >> 24) != uint64_t(split_sum[s])) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+      split_sum[s] = 0;
+    }
+  }
+}
+
+// Dense -> packed CSR (copy-out): one workgroup per row, column order, at pk_row_ptr[a].
+__global__ __launch_bounds__(kAccThreads) void k_pack_dense(const uint32_t *__restrict__ dense, int32_t M,
+                                                            const int64_t *__restrict__ pk_row_ptr,
+                                                            int32_t *__restrict__ pk_col,
+                                                            uint32_t *__restrict__ pk_cnt) {
+  __shared__ uint32_t s_wave[kAccWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t per = ((M + kAccWaves - 1) / kAccWaves + 63) & ~63;
+  const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t a = blockIdx.x; a < M; a += gridDim.x) {
+    const uint32_t *d = dense + int64_t(a) * M;
+    uint32_t cnt = 0;
+    for (int32_t b = lo + lane; b < hi; b += 64) cnt += uint32_t(__popcll(__ballot(d[b] != 0u)));
+    cnt = __shfl(cnt, 0, 64);
+    if (lane == 0) s_wave[wave] = cnt;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; w++) off += s_wave[w];
+    const int64_t base = pk_row_ptr[a];
+    for (int32_t b0 = lo; b0 < hi; b0 += 64) {
+      const int32_t b = b0 + lane;
+      const uint32_t v = b < hi ? d[b] : 0u;
+      const uint64_t m = __ballot(v != 0u);
+      if (v) {
+        const int64_t pos = base + off + uint32_t(__popcll(m & lt_mask));
+        pk_col[pos] = b;
+        pk_cnt[pos] = v;
+      }
+      off += uint32_t(__popcll(m));
     }
     __syncthreads();
   }
@@ -1099,22 +1287,25 @@ Status Counter::init(int32_t n_items) {
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
   if (n_items < kBatchMaxItems) {
     const int acc_bytes = int(sizeof(uint32_t)) * ((n_items + 2) & ~1);
-    const int dbb = std::min(1024, (kLdsBudget - acc_bytes - 4) / 12);
-    const int lds_b = acc_bytes + dbb * 12 + 4;
-    for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<2, 4>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 4>),
-                          reinterpret_cast<const void *>(k_acc_batch<2, 8>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8>),
-                          reinterpret_cast<const void *>(k_acc_batch<8, 8>),
-                          reinterpret_cast<const void *>(k_acc_batch<2, 16>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 16>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 64>)})
-      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_b));
+    for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 4>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 8>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 16, true>),
+                          reinterpret_cast<const void *>(k_acc_batch<2, 8, true>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, true>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 4>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 8>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 0, 3>),
+                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false>)})
+      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsBudget));
     for (const void *k : {reinterpret_cast<const void *>(k_batch_hist), reinterpret_cast<const void *>(k_batch_scatter)})
       COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(sizeof(uint32_t)) * n_items));
   }
+  const char *sm = getenv("COOC_ACC_STORE");
+  store_mode_ = sm ? atoi(sm) : 1;
+  const char *aw = getenv("COOC_ACC_WGS");
+  acc_wgs_ = aw ? atoi(aw) : 1;
   const char *bs = getenv("COOC_BATCH_STRIDE");
-  bstride_ = bs ? atoi(bs) : 8;
+  bstride_ = bs ? atoi(bs) : 16;
   const char *bu = getenv("COOC_BATCH_UNROLL");
   bunroll_ = bu ? atoi(bu) : 4;
   const char *co = getenv("COOC_CHUNK_ORDER");
@@ -1138,7 +1329,7 @@ Status Counter::init(int32_t n_items) {
 }
 
 void Counter::release() {
-  DevBuf *all[] = {&bh_, &ub_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
+  DevBuf *all[] = {&dense_, &bh_, &uidx_, &long_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
                    &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
                    &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
                    &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_, &bump_, &seg_off_,
@@ -1247,6 +1438,7 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
 
 Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
   const int32_t M = M_;
+  dense_mode_ = false;
   const int64_t n = au.n_contrib;
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
   if (T_ > 1 && au.n_new != au.n_contrib)
@@ -1483,9 +1675,14 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
   COOC_HIP_TRY(hipMemsetAsync(pk_row_ptr_.p, 0, sizeof(int64_t), s));
   COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, nnz64, pk_row_ptr_.as<int64_t>() + 1,
                                                 M, s));
-  k_pack<<<blocks_for(int64_t(M) * 64, 256) < 8192 ? blocks_for(int64_t(M) * 64, 256) : 8192, 256, 0, s>>>(
-      row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), const_cast<int32_t *>(last_col()), const_cast<uint32_t *>(last_cnt()), M,
-      pk_col_.as<int32_t>(), pk_cnt_.as<uint32_t>());
+  if (dense_mode_) {
+    k_pack_dense<<<unsigned(std::max<int32_t>(1, std::min<int32_t>(M, 4 * n_cu_))), kAccThreads, 0, s>>>(
+        dense_.as<uint32_t>(), M, pk_row_ptr_.as<int64_t>(), pk_col_.as<int32_t>(), pk_cnt_.as<uint32_t>());
+  } else {
+    k_pack<<<blocks_for(int64_t(M) * 64, 256) < 8192 ? blocks_for(int64_t(M) * 64, 256) : 8192, 256, 0, s>>>(
+        row_base_.as<int64_t>(), pk_row_ptr_.as<int64_t>(), const_cast<int32_t *>(last_col()),
+        const_cast<uint32_t *>(last_cnt()), M, pk_col_.as<int32_t>(), pk_cnt_.as<uint32_t>());
+  }
   COOC_HIP_TRY(hipGetLastError());
   *row_ptr = pk_row_ptr_.as<int64_t>();
   *col = pk_col_.as<int32_t>();
@@ -1499,13 +1696,15 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   if (!batch_ok()) return Status{1, "run_batch needs n_items < " + std::to_string(kBatchMaxItems)};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
   if (U > int64_t(INT32_MAX)) return Status{1, "more than 2^31 users in one window"};
-  const int32_t B = int32_t(std::max<int64_t>(1, std::min<int64_t>(n_cu_, std::max<int64_t>(U, 1))));
+  // partition blocks of the hist / scatter passes: one per CU, fewer for tiny inputs
+  const int32_t B = int32_t(std::max<int64_t>(1, std::min<int64_t>(n_cu_, n / 4096 + 1)));
   const int64_t U1 = std::max<int64_t>(U, 1);
   COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
   COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
   COOC_TRY(plen_.reserve(sizeof(int64_t) * U1));
   COOC_TRY(poff_.reserve(sizeof(int64_t) * (U1 + 1)));
-  COOC_TRY(ub_.reserve(sizeof(int32_t) * (B + 1)));
+  COOC_TRY(uidx_.reserve(sizeof(int32_t) * (n + 4)));
+  COOC_TRY(long_.reserve(sizeof(int32_t) * U1));
   COOC_TRY(bh_.reserve(sizeof(int32_t) * size_t(B) * M));
   COOC_TRY(rcnt_.reserve(sizeof(int32_t) * M));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
@@ -1525,7 +1724,7 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
   PlanTotals *tot = tot_.as<PlanTotals>();
   int64_t *plen = plen_.as<int64_t>(), *poff = poff_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
-  int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *ub = ub_.as<int32_t>();
+  int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *uidx = uidx_.as<int32_t>();
   COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
   COOC_HIP_TRY(hipMemsetAsync(queue_.p, 0, sizeof(int32_t) * 4, s));
   COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * M, s));
@@ -1560,10 +1759,12 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   // at the end (never referenced by a segment, keeps the last 16-B load in bounds)
   const int64_t arena_cap = n + 7 * U1 + 16;
   COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
-  k_batch_bounds<<<blocks_for(B + 1, 256), 256, 0, s>>>(U, up, B, ub);
   const size_t lds_m = sizeof(uint32_t) * size_t(M);
   if (U > 0) {
-    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(up, items, ub, poff, M, tarena_.as<uint16_t>(), bh, tot);
+    k_batch_fill<<<blocks_for(U, 256), 256, 0, s>>>(U, up, poff, M, uidx, tarena_.as<uint16_t>(), long_.as<int32_t>(),
+                                                   tot);
+    k_batch_fill_long<<<256, 256, 0, s>>>(up, long_.as<int32_t>(), tot, uidx);
+    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, M, tarena_.as<uint16_t>(), bh, tot);
     k_batch_colscan<<<blocks_for(M, 256), 256, 0, s>>>(B, M, bh, rcnt);
   } else {
     COOC_HIP_TRY(hipMemsetAsync(rcnt, 0, sizeof(int32_t) * M, s));
@@ -1574,7 +1775,7 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt64, row_ptr + 1, M, s));
   }
   if (U > 0) {
-    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(up, items, ub, poff, row_ptr, M, bh, desc_.as<uint64_t>());
+    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, bh, desc_.as<uint64_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
   // chunk plan: rows by contribution count, heaviest first
@@ -1609,16 +1810,40 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
   const int64_t work_total = h_tot_->sum_l2;
   const int64_t pairs = work_total - n;
-  // output region: distinct keys <= min(M^2, ordered pairs)
-  bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(int64_t(M) * M, pairs));
-  COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
-  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
-  bump_mode_ = false;  // the bump region IS the output (one column tile): no gather
+  // Output layout.  Dense uint32 [M x M] when the pairs cover the matrix (P >= M^2 / 2: dense is then
+  // no larger than the sparse (col, cnt) entries it replaces, and written with plain coalesced row
+  // stores) and it fits in 40% of free HBM; else the sparse bump-allocated padded CSR, whose entries
+  // are at most min(M^2, P).
+  const int64_t MM = int64_t(M) * M;
+  bool dense = output_pref_ == 2;
+  if (output_pref_ == 0 && 2 * pairs >= MM) {
+    size_t free_b = 0, total_b = 0;
+    COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    dense = size_t(MM) * sizeof(uint32_t) <= free_b / 10 * 4 + dense_.cap;
+  }
+  dense_mode_ = dense;
+  bump_mode_ = false;  // the bump region IS the sparse output (one column tile): no gather
+  if (dense) {
+    COOC_TRY(dense_.reserve(sizeof(uint32_t) * size_t(std::max<int64_t>(MM, 1))));
+  } else {
+    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(MM, pairs));
+    COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
+    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
+  }
+  if (dense && n_chunks == 0 && MM > 0) COOC_HIP_TRY(hipMemsetAsync(dense_.p, 0, sizeof(uint32_t) * size_t(MM), s));
   if (n_chunks > 0) {
     COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
     COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
     COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
-    if (n_split > 0) {
+    if (dense) {
+      // rows without contributions stay all-zero; rows of several chunks are zeroed, then added into
+      COOC_TRY(zero_unplanned_rows(s));
+      if (n_split > 0) {
+        k_zero_rows<<<unsigned(std::min<int64_t>(n_split, 4 * int64_t(n_cu_))), 1024, 0, s>>>(
+            split_row_.as<int32_t>(), tot, M, dense_.as<uint32_t>());
+        COOC_HIP_TRY(hipGetLastError());
+      }
+    } else if (n_split > 0) {
       const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
       COOC_TRY(staging_.reserve(need));
       COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
@@ -1627,25 +1852,32 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
                                                       row_ptr, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
     COOC_HIP_TRY(hipGetLastError());
     const size_t acc_bytes = sizeof(uint32_t) * size_t((M + 2) & ~1);
-    const int db = int(std::min<int64_t>(1024, (int64_t(kLdsBudget) - int64_t(acc_bytes) - 4) / 12));
+    const int db = int(std::min<int64_t>(1024, (int64_t(kBatchLdsBudget) - int64_t(acc_bytes) - 4) / 12));
     if (db < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
-    const size_t lds = acc_bytes + size_t(db) * 12 + 4;
-    const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
-    auto kern = bstride_ == 16 ? (bunroll_ == 2 ? k_acc_batch<2, 16> : k_acc_batch<4, 16>)
-              : bstride_ == 4  ? (bunroll_ == 2 ? k_acc_batch<2, 4> : k_acc_batch<4, 4>)
-              : bstride_ == 64 ? k_acc_batch<4, 64>
-                               : (bunroll_ == 2 ? k_acc_batch<2, 8> : bunroll_ == 8 ? k_acc_batch<8, 8>
-                                                                                    : k_acc_batch<4, 8>);
+    size_t lds = acc_bytes + size_t(db) * 12 + 4;
+    static const char *lp = getenv("COOC_ACC_LDS_MIN");  // experiments: inflate LDS to limit occupancy
+    if (lp) lds = std::max<size_t>(lds, size_t(atol(lp)));
+    const int64_t grid = std::min<int64_t>(n_chunks, int64_t(n_cu_) * std::max<int64_t>(1, acc_wgs_));
+    auto kern = dense_mode_ ? (xmode_ == 4 ? k_acc_batch<4, 8, true, 4> : xmode_ == 8 ? k_acc_batch<4, 8, true, 8>
+                               : bstride_ == 16 ? k_acc_batch<4, 16, true> : bunroll_ == 2 ? k_acc_batch<2, 8, true>
+                                                                                         : k_acc_batch<4, 8, true>)
+              : xmode_ == 4 ? k_acc_batch<4, 8, false, 4> : xmode_ == 8 ? k_acc_batch<4, 8, false, 8>
+              : store_mode_ == 3 ? k_acc_batch<4, 8, false, 0, 3> : k_acc_batch<4, 8, false>;
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(),
                                                   desc_.as<uint64_t>(), tarena_.as<uint16_t>(), M, db,
                                                   col_.as<int32_t>(), cnt_.as<uint32_t>(),
                                                   bump_.as<unsigned long long>(), bump_cap_, row_base_.as<int64_t>(),
                                                   row_nnz_.as<int32_t>(), staging_.as<uint32_t>(),
-                                                  split_sum_.as<int64_t>(), rowsum_.as<int64_t>());
+                                                  split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
+                                                  dense_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
-    if (n_split > 0) {
+    if (dense && n_split > 0) {
+      k_dense_split_check<<<unsigned(std::min<int64_t>(n_split, 4 * int64_t(n_cu_))), kAccThreads, 0, s>>>(
+          split_row_.as<int32_t>(), tot, M, dense_.as<uint32_t>(), split_sum_.as<int64_t>(), row_nnz_.as<int32_t>());
+      COOC_HIP_TRY(hipGetLastError());
+    } else if (n_split > 0) {
       const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
       k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(
           tot, split_row_.as<int32_t>(), M, 0, staging_.as<uint32_t>(), row_base_.as<int64_t>(),
@@ -1660,14 +1892,23 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   }
   k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
   COOC_HIP_TRY(hipGetLastError());
-  out->row_base = row_base_.as<int64_t>();
+  out->row_base = dense ? nullptr : row_base_.as<int64_t>();
   out->row_nnz = row_nnz_.as<int32_t>();
-  out->col = col_.as<int32_t>();
-  out->cnt = cnt_.as<uint32_t>();
+  out->col = dense ? nullptr : col_.as<int32_t>();
+  out->cnt = dense ? nullptr : cnt_.as<uint32_t>();
+  out->dense = dense ? dense_.as<uint32_t>() : nullptr;
   out->rowsum = rowsum_.as<int64_t>();
   out->work = work_total;
   out->observed = pairs;
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
+  return Status::Ok();
+}
+
+// Dense output: rows that no chunk writes (items without interactions) must read as zero.
+Status Counter::zero_unplanned_rows(hipStream_t s) {
+  k_zero_empty_rows<<<std::min<unsigned>(blocks_for(M_, 4), 4096), 256, 0, s>>>(rcnt_.as<int32_t>(), M_,
+                                                                                  dense_.as<uint32_t>());
+  COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }
 

@@ -32,7 +32,9 @@ Status cooc_ctx::init(const cooc_config &c) {
   COOC_HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   COOC_HIP_TRY(hipEventCreate(&timer.acc_begin));
   COOC_HIP_TRY(hipEventCreate(&timer.acc_end));
-  return counter.init(c.n_items);
+  COOC_TRY(counter.init(c.n_items));
+  counter.set_output_layout((c.flags & COOC_FLAG_OUTPUT_DENSE) ? 2 : (c.flags & COOC_FLAG_OUTPUT_CSR) ? 1 : 0);
+  return Status::Ok();
 }
 
 cooc_ctx::~cooc_ctx() {
@@ -104,6 +106,7 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
   out->col = r.col;
   out->cnt = r.cnt;
   out->rowsum = r.rowsum;
+  out->dense = r.dense;
   have_batch = true;
   batch_result = r;
   batch_result.nnz = nnz;
@@ -180,7 +183,7 @@ Status cooc_ctx::topk_batch(int32_t topk, int32_t flags, hipStream_t s) {
   COOC_TRY(b_obs3.reserve(sizeof(int64_t) * 4));
   if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
   const cooc::CountResult &r = batch_result;
-  COOC_TRY(cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum,
+  COOC_TRY(cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense, r.rowsum,
                                       (flags & COOC_FLAG_EXACT_SCORES) != 0, topk, b_obs3.as<int64_t>(),
                                       b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(), b_tk_score.as<double>()));
   COOC_HIP_TRY(hipStreamSynchronize(s));

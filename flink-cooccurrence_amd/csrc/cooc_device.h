@@ -90,7 +90,7 @@ struct PlanTotals {
   int64_t sum_l2;     // sum_u n_u^2  (= ordered pairs + self terms)
   int64_t sum_lpl;    // sum_u n_u * pad8(n_u): padded partner ids read
   int64_t max_len;    // longest history
-  int64_t pad;
+  int64_t n_long;     // histories longer than kFillThread (filled by a workgroup each)
 };
 
 // Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
@@ -100,6 +100,7 @@ struct CountResult {
   int32_t *col = nullptr;
   uint32_t *cnt = nullptr;
   int64_t *rowsum = nullptr;
+  uint32_t *dense = nullptr;  // dense output: row-major [M x M] counts (row_base / col / cnt unused)
   int64_t nnz = 0;
   int64_t observed = 0;  // ordered pairs of the run
   int64_t work = 0;
@@ -123,14 +124,19 @@ class Counter {
 
   // One window over empty histories straight from a device CSR (user_ptr int64[U+1], items
   // int32[N]): the batch planner (per-block item histograms -> transpose of A by counting sort) and
-  // k_acc_batch.  Needs n_items <= 40,703 (one LDS row plus the pad sink); returns the same padded
+  // k_acc_batch.  Needs n_items < kBatchMaxItems (one LDS row + pad sink + descriptors); returns the same padded
   // CSR as run().  Synchronises `stream` once (to size chunks and the output region).
   Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                    CountResult *out, KernelTimer *timer = nullptr);
   bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems; }
-  static constexpr int32_t kBatchMaxItems = 40704;
+  static constexpr int32_t kBatchMaxItems = 40320;
 
-  // Pack the padded CSR of the last run into contiguous CSR (device), for copy-out.
+  // Output layout of run_batch: 0 = auto (dense when P >= M^2 / 2), 1 = sparse CSR, 2 = dense.
+  void set_output_layout(int pref) { output_pref_ = pref; }
+  bool last_dense() const { return dense_mode_; }
+  const uint32_t *last_dense_counts() const { return dense_mode_ ? dense_.as<uint32_t>() : nullptr; }
+
+  // Pack the result of the last run into contiguous CSR (device), for copy-out.
   Status pack(hipStream_t stream, int64_t **row_ptr, int32_t **col, uint32_t **cnt);
 
   // Copy the device totals of the last run (the stream must have drained).
@@ -144,6 +150,7 @@ class Counter {
 
  private:
   Status run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
+  Status zero_unplanned_rows(hipStream_t s);
 
   int32_t M_ = 0;
   int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)
@@ -166,8 +173,14 @@ class Counter {
   int xmode_ = 0;                          // COOC_ACC_X: experiment modes of k_accumulate2 (bench only)
   int vunroll_ = 4;                        // COOC_ACC_VUNROLL: 16-B loads in flight per lane (2, 4, 8)
   DevBuf plen_, poff_, vpre_;
-  DevBuf bh_, ub_, rcnt_, desc_;      // batch planner: block histograms, user bounds, row counts, descriptors
-  int bstride_ = 8, bunroll_ = 4;     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
+  DevBuf bh_, uidx_, long_, rcnt_, desc_;  // batch planner: block histograms, user of each interaction,
+                                           // long lists, row counts, descriptors
+  int bstride_ = 8, bunroll_ = 4;
+  int store_mode_ = 1;                // COOC_ACC_STORE: output stores 1 plain, 2 sc1, 3 nt (A/B)
+  int output_pref_ = 0;               // set_output_layout
+  bool dense_mode_ = false;           // the last run's output is dense_
+  DevBuf dense_;
+  int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

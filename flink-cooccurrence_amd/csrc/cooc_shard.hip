@@ -58,6 +58,37 @@ __global__ void k_pack_entries(const int64_t *__restrict__ row_base, const int32
   }
 }
 
+// Dense result: one workgroup per row compacts the row's nonzeros (column order) into the packed
+// (col << 32 | cnt) entries of its owner segment.
+__global__ __launch_bounds__(kThreads) void k_pack_entries_dense(const uint32_t *__restrict__ dense,
+                                                                const int64_t *__restrict__ perm_off, int32_t M,
+                                                                int32_t n, uint64_t *__restrict__ out) {
+  __shared__ uint32_t s_wave[kWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t per = ((M + kWaves - 1) / kWaves + 63) & ~63;
+  const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t a = blockIdx.x; a < M; a += gridDim.x) {
+    const uint32_t *d = dense + int64_t(a) * M;
+    uint32_t c = 0;
+    for (int32_t b = lo + lane; b < hi; b += 64) c += uint32_t(__popcll(__ballot(d[b] != 0u)));
+    c = __shfl(c, 0, 64);
+    if (lane == 0) s_wave[wave] = c;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; w++) off += s_wave[w];
+    const int64_t base = perm_off[perm_index(a, M, n)];
+    for (int32_t b0 = lo; b0 < hi; b0 += 64) {
+      const int32_t b = b0 + lane;
+      const uint32_t v = b < hi ? d[b] : 0u;
+      const uint64_t m = __ballot(v != 0u);
+      if (v) out[base + off + uint32_t(__popcll(m & lt))] = (uint64_t(uint32_t(b)) << 32) | uint64_t(v);
+      off += uint32_t(__popcll(m));
+    }
+    __syncthreads();
+  }
+}
+
 // Per owned row r: total received entries (sum over sources) -> output capacity.
 __global__ void k_merge_plan(const int32_t *__restrict__ recv_nnz, int32_t n_src, int32_t R, int32_t M,
                              int64_t *__restrict__ cap) {
@@ -163,7 +194,14 @@ Status Sharder::pack(const CountResult &r, int32_t M, int32_t n_parts, hipStream
   if (n_parts != planned_parts_) return Status{2, "cooc_partition_plan must precede cooc_partition_pack"};
   if (d_row_nnz)
     COOC_HIP_TRY(hipMemcpyAsync(d_row_nnz, perm_nnz_.p, sizeof(int32_t) * M, hipMemcpyDeviceToDevice, s));
-  if (d_entries) {
+  if (d_entries && r.dense) {
+    int dev = 0, n_cu = 256;
+    COOC_HIP_TRY(hipGetDevice(&dev));
+    COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    k_pack_entries_dense<<<unsigned(std::max<int32_t>(1, std::min<int32_t>(M, 4 * n_cu))), kThreads, 0, s>>>(
+        r.dense, perm_off_.as<int64_t>(), M, n_parts, d_entries);
+    COOC_HIP_TRY(hipGetLastError());
+  } else if (d_entries) {
     k_pack_entries<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
         r.row_base, r.row_nnz, r.col, r.cnt, perm_off_.as<int64_t>(), M, n_parts, d_entries);
     COOC_HIP_TRY(hipGetLastError());

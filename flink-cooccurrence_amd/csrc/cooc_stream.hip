@@ -303,11 +303,15 @@ Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal
 }
 
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
-                            const int32_t *col, const uint32_t *cnt, const int64_t *rowsum, bool exact, int32_t topk,
-                            int64_t *obs3, int32_t *out_size, int32_t *out_val, double *out_score) {
+                            const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
+                            bool exact, int32_t topk, int64_t *obs3, int32_t *out_size, int32_t *out_val,
+                            double *out_score) {
   k_observed<<<1, 256, 0, s>>>(rowsum, M, obs3);
   COOC_HIP_TRY(hipGetLastError());
   // obs3: [0] rescorer observed, [1] exact, [2] n_rows (= M)
+  if (dense)
+    return launch_rescore_rows(s, nullptr, obs3 + 2, M, DenseRows{dense, M}, rowsum, obs3, exact, topk, out_size,
+                               out_val, out_score);
   return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, rowsum, obs3, exact,
                              topk, out_size, out_val, out_score);
 }

@@ -23,7 +23,8 @@ Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal
 // LLR top-k of every row of a batch result (padded CSR) -- the C5 stage over one window.
 // obs3 (device int64[3]) receives the rescorer's observed, the exact observed and n_items.
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
-                            const int32_t *col, const uint32_t *cnt, const int64_t *rowsum, bool exact, int32_t topk,
+                            const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
+                            bool exact, int32_t topk,
                             int64_t *obs3, int32_t *out_size, int32_t *out_val, double *out_score);
 
 }  // namespace cooc

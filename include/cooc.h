@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 1
+#define COOC_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -63,8 +63,12 @@ enum cooc_status {
   COOC_ERR_OVERFLOW = 5  /* an exact uint32 count overflowed */
 };
 
-/* Rescoring flavour for cooc_config.flags. */
+/* cooc_config.flags. */
 #define COOC_FLAG_EXACT_SCORES 1 /* LLR on exact counts instead of the reference's wrapped int16/int32 */
+/* Layout of a cooc_count_device result (default: automatic, dense when the ordered pairs cover at
+ * least half of the n_items^2 matrix and it fits in HBM, else the padded CSR). */
+#define COOC_FLAG_OUTPUT_CSR 2   /* always the padded CSR (row_base, row_nnz, col, cnt) */
+#define COOC_FLAG_OUTPUT_DENSE 4 /* always the dense matrix (dense, row_nnz) */
 
 typedef struct cooc_ctx cooc_ctx;
 
@@ -89,16 +93,20 @@ typedef struct cooc_window_info {
   int32_t reserved;
 } cooc_window_info;
 
-/* Borrowed device views of a cooc_count_device result (valid until the next call on ctx). */
+/* Borrowed device views of a cooc_count_device result (valid until the next call on ctx).  Exactly
+ * one layout is set: the padded CSR (row_base, col, cnt non-NULL, dense NULL) or the dense matrix
+ * (dense non-NULL, row_base / col / cnt NULL).  Both key sets are the reference's touched keys: a
+ * key exists iff its count is > 0 (every increment is +1, ItemRowAggregator.java:29). */
 typedef struct cooc_device_result {
   int64_t n_items;
-  int64_t nnz;            /* total entries */
+  int64_t nnz;            /* total entries (keys with a count > 0) */
   int64_t observed;       /* exact ordered pairs sum_u n_u (n_u - 1) */
   const int64_t *row_base;  /* [n_items]: first entry of row a in col/cnt (rows padded, not packed) */
-  const int32_t *row_nnz;   /* [n_items]: entries of row a */
+  const int32_t *row_nnz;   /* [n_items]: entries of row a (both layouts) */
   const int32_t *col;       /* ascending within a row */
   const uint32_t *cnt;      /* exact counts */
   const int64_t *rowsum;    /* [n_items]: exact row sums sum_b C[a,b] */
+  const uint32_t *dense;    /* [n_items * n_items] row-major exact counts, 0 = key absent */
 } cooc_device_result;
 
 /* ---- lifecycle ------------------------------------------------------------------------------ */

@@ -23,8 +23,15 @@ def torch_cuda():
     return torch
 
 
-def _batch_vs_closed_form(pkg, oracle, up, it, M):
-    with pkg.CooccurrenceCore(n_items=M) as core:
+def _batch_vs_closed_form(pkg, oracle, up, it, M, layouts=("csr", "dense")):
+    """Both result layouts of the batch path (padded CSR and dense matrix) against the closed form."""
+    for output in layouts:
+        got = _batch_layout_vs_closed_form(pkg, oracle, up, it, M, output)
+    return got
+
+
+def _batch_layout_vs_closed_form(pkg, oracle, up, it, M, output):
+    with pkg.CooccurrenceCore(n_items=M, output=output) as core:
         got = core.count(up, it)
     rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
     assert got.observed == observed
@@ -42,7 +49,7 @@ def _batch_vs_closed_form(pkg, oracle, up, it, M):
     (2, 3000, 1000, 20.0, True),      # C1 shape, scaled
     (3, 2000, 4096, 40.0, False),     # rating-log shape
     (4, 300, 40704, 60.0, True),      # the largest single-tile LDS row (general planner)
-    (6, 300, 40703, 60.0, True),      # the largest batch-planner row (+ pad sink)
+    (6, 300, 40319, 60.0, True),     # the largest batch-planner row (+ pad sink + descriptors)
     (7, 5000, 2000, 150.0, False),    # long lists, many batches per chunk
 ])
 def test_batch_random_logs(pkg, oracle, torch_cuda, seed, U, M, mean, repl):
@@ -62,7 +69,8 @@ def test_batch_matches_literal_expansion(pkg, oracle, torch_cuda):
     assert np.array_equal(C, dense) and np.array_equal(got.rowsum, rs) and got.observed == obs
 
 
-@pytest.mark.parametrize("case", ["empty", "empty_users", "singletons", "one_item_universe", "max_id", "one_user"])
+@pytest.mark.parametrize("case", ["empty", "empty_users", "singletons", "one_item_universe", "max_id", "one_user",
+                                  "long_lists"])
 def test_batch_edge_cases(pkg, oracle, torch_cuda, case):
     M = 50
     if case == "empty":
@@ -76,6 +84,11 @@ def test_batch_edge_cases(pkg, oracle, torch_cuda, case):
         up, it = np.array([0, 3, 4, 8], np.int64), np.zeros(8, np.int32)
     elif case == "max_id":
         up, it = np.array([0, 4], np.int64), np.array([M - 1, 0, M - 1, 7], np.int32)
+    elif case == "long_lists":  # lists beyond one planner thread (2048), between short ones
+        rng = np.random.default_rng(11)
+        lens = np.array([5, 3000, 0, 2049, 7, 9000, 1], np.int64)
+        up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        it = rng.integers(0, M, int(up[-1])).astype(np.int32)
     else:
         up, it = np.array([0, 30], np.int64), np.arange(30, dtype=np.int32) % 7
     _batch_vs_closed_form(pkg, oracle, up, it, M)
@@ -144,6 +157,34 @@ def test_bad_item_id_is_illegal_argument(pkg, torch_cuda):
         assert got.observed == 2
 
 
+def test_dense_view_on_a_reused_context(pkg, oracle, torch_cuda):
+    """The dense device view: rows of items absent from a later batch read as zero although the
+    context's matrix held counts from an earlier batch; split rows are summed across chunks."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    M = 600
+    dev = torch.device("cuda")
+    up1, it1 = datagen.small_log(23, 2000, M, 30.0)
+    rng = np.random.default_rng(24)
+    U2, L2 = 2600, 1700   # rows 0 and 1 carry U2 * (L2 - 1) > 2^22 pairs: split over chunks
+    it2 = np.concatenate([np.concatenate([[0, 1], rng.choice(np.arange(2, M // 2), L2 - 2, replace=True)])
+                          for _ in range(U2)]).astype(np.int32)
+    up2 = (np.arange(U2 + 1) * L2).astype(np.int64)
+    with pkg.CooccurrenceCore(n_items=M, device=0, output="dense") as core:
+        for up, it in [(up1, it1), (up2, it2)]:
+            res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+            torch.cuda.synchronize()
+            assert res.dense and not res.col and not res.row_base
+            D = _d2h(res.dense, M * M, np.uint32).reshape(M, M).astype(np.int64)
+            rp, cols, data, rs, obs = oracle.closed_form(up, it, M)
+            want = sp.csr_matrix((data, cols, rp), shape=(M, M)).toarray()
+            assert np.array_equal(D, want) and res.observed == obs
+            assert np.array_equal(_d2h(res.row_nnz, M, np.int32), (want != 0).sum(1))
+            assert np.array_equal(_d2h(res.rowsum, M, np.int64), rs)
+            assert res.nnz == int((want != 0).sum())
+
+
 def test_count_device_padded_layout(pkg, oracle, torch_cuda):
     import ctypes
 
@@ -152,7 +193,7 @@ def test_count_device_padded_layout(pkg, oracle, torch_cuda):
 
     up, it = datagen.small_log(21, 1000, 300, 15.0)
     dev = torch.device("cuda")
-    with pkg.CooccurrenceCore(n_items=300, device=0) as core:
+    with pkg.CooccurrenceCore(n_items=300, device=0, output="csr") as core:
         core.set_kernel_timing(True)
         res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
         assert core.last_kernel_ms() > 0
@@ -281,8 +322,8 @@ def _d2h(ptr, n, dtype):
     return out
 
 
-@pytest.mark.parametrize("n_parts", [2, 3])
-def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts):
+@pytest.mark.parametrize("n_parts,output", [(2, "csr"), (3, "csr"), (2, "dense"), (3, "dense")])
+def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts, output):
     """The sharding kernels on one GPU: n_parts user shards reduced separately, packed by owner,
     'all-to-all' done by slicing, merged per owner == C of all users together."""
     torch = torch_cuda
@@ -297,7 +338,7 @@ def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts):
         lo, hi = s * U // n_parts, (s + 1) * U // n_parts
         sup = torch.from_numpy(up[lo:hi + 1] - up[lo]).to(dev)
         sit = torch.from_numpy(it[up[lo]:up[hi]]).to(dev)
-        core = pkg.CooccurrenceCore(n_items=M, device=0)
+        core = pkg.CooccurrenceCore(n_items=M, device=0, output=output)
         core.count_device(sup, sit)
         counts = core.partition_plan(n_parts)
         row_nnz = torch.empty(M, dtype=torch.int32, device=dev)
