@@ -68,8 +68,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_accumulate.json"),
-                    help="rocprofv3 PMC summary of k_accumulate (HBM traffic per launch), if collected")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_k_acc_batch.json"),
+                    help="rocprofv3 PMC summary of k_acc_batch (HBM traffic per launch), if collected")
     args = ap.parse_args()
 
     import torch
@@ -143,14 +143,14 @@ def main():
     k_ms = float(np.mean(kernel_ms))
     b_alg = algorithmic_bytes(P, N, U, D)
     achieved = b_alg / (k_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, pmc = None, {}
     if os.path.exists(args.pmc_file):
         try:
             with open(args.pmc_file) as f:
                 pmc = json.load(f)
             traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic = None
+            traffic, pmc = None, {}
     out = {
         "metric": "item-pair co-occurrences counted/sec (node)",
         "value": value,
@@ -169,22 +169,29 @@ def main():
                         "Zipf(0.9) without replacement, one window, numpy PCG64 seed 2 (+rank)",
             "users_per_gpu": U, "items": M, "interactions_per_gpu": N, "ordered_pairs_per_gpu": P,
             "distinct_keys_per_gpu": D,
+            "output": "dense uint32 [items x items] in HBM" if world == 1 and res.dense else "padded CSR in HBM",
             "parallelism": f"users sharded over {world} GPU(s)" + (
                 "; partial rows all-to-all'd to owner(a) = a mod N over RCCL and merged; row sums all-reduced"
                 if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_accumulate2",
+            "kernel": "k_acc_batch",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            "traffic_gbps": (traffic / (k_ms * 1e-3) / 1e9) if traffic else None,
+            "lds_util": pmc.get("lds_util"),
+            "lds_bank_conflict_frac": pmc.get("lds_bank_conflict_frac"),
             "kernel_ms": k_ms,
             "algorithmic_bytes_per_launch": b_alg,
-            "note": "B_alg = 4P + 4N + 8(U+1) + 12D (SURVEY.md §8(d)); partner ids are re-read from "
-                    "MALL/L2, so frac > 1 would mean cache reuse, not HBM bandwidth",
+            "note": "B_alg = 4P + 4N + 8(U+1) + 12D (SURVEY.md §8(d)). frac > 1 flags cache reuse: every "
+                    "partner-id list is re-read once per item in it from L2 / Infinity Cache (2 B per id "
+                    "here). traffic = HBM-side bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + "
+                    "WRITE_SIZE, profiles/pmc_k_acc_batch.json); the kernel is bound by LDS atomics "
+                    "(lds_util, lds_bank_conflict_frac), see DESIGN.md §4",
         },
         "cpu_baseline": None,
     }

@@ -13,7 +13,7 @@ import os
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_accumulate.json"
+out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_k_acc_batch.json"
 vals = collections.defaultdict(list)
 kernel = None
 for f in sorted(glob.glob(os.path.join(root, "p*", "pmc_counter_collection.csv"))):
@@ -29,9 +29,8 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     res["write_bytes"] = write
     res["hbm_bytes_per_launch"] = 2 * fetch + write
     res["note"] = ("hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (KB -> B). The x2 read correction is the guide's for "
-                   "coalesced streaming reads; this kernel's partner-id reads are 4 B per lane, so the read side is "
-                   "bracketed by [fetch_bytes_raw, 2*fetch_bytes_raw]. FETCH_SIZE counts memory-side requests "
-                   "(Infinity-Cache hits included).")
+                   "wide coalesced reads (k_acc_batch reads partner ids 16 B per lane). FETCH_SIZE counts "
+                   "memory-side requests (Infinity-Cache hits included): an upper bound on DRAM bytes.")
 if "TCC_HIT_sum" in avg:
     res["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
 if "SQ_LDS_IDX_ACTIVE" in avg and "GRBM_GUI_ACTIVE" in avg:
