@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=["records", "partials"], default="records",
+                    help="N > 1: route pair records to owner(a) (default) or partial counts (sharding.py)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_k_acc_batch.json"),
                     help="rocprofv3 PMC summary of k_acc_batch (HBM traffic per launch), if collected")
     args = ap.parse_args()
@@ -103,7 +105,9 @@ def main():
     def step():
         if world == 1:
             return core.count_device(up, it)  # returns after the stream drained (errors are checked)
-        # users sharded over ranks; partial rows all-to-all'd to owner(a) = a mod world and merged
+        # users sharded over ranks; rows owned by a mod world (keyBy(itemA), FlinkCooccurrences.java:152)
+        if args.exchange == "records":
+            return sharding.count_records(core, up, it)
         return sharding.count_sharded(core, up, it)
 
     for _ in range(args.warmup):
@@ -126,7 +130,7 @@ def main():
         D = int(res.nnz)
     else:
         assert res.local_observed == P, "pair count mismatch"
-        D = int(core_last_nnz(core))
+        D = int(res.owned.nnz) if args.exchange == "records" else int(core_last_nnz(core))
 
     stats = torch.tensor([elapsed, float(P), float(algorithmic_bytes(P, N, U, D))], dtype=torch.float64, device=dev)
     if world > 1:
@@ -171,8 +175,7 @@ def main():
             "distinct_keys_per_gpu": D,
             "output": "dense uint32 [items x items] in HBM" if world == 1 and res.dense else "padded CSR in HBM",
             "parallelism": f"users sharded over {world} GPU(s)" + (
-                "; partial rows all-to-all'd to owner(a) = a mod N over RCCL and merged; row sums all-reduced"
-                if world > 1 else ""),
+                f"; rows owned by a mod N, exchange over RCCL: {args.exchange}" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -195,8 +198,15 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if world > 1:
-        out["config"]["exchange"] = {"entries_sent_rank0": res.sent_entries, "entries_recv_rank0": res.recv_entries,
+    if world > 1 and args.exchange == "records":
+        out["config"]["exchange"] = {
+            "mode": "pair records to owner(a) = a mod N: all-gather of u16 histories + all-to-all of 8-B "
+                    "descriptors; owners reduce complete rows (no partial counts, no merge)",
+            "records_sent_rank0": res.sent_records, "records_recv_rank0": res.recv_records,
+            "arena_bytes_per_rank": 2 * res.arena_stride, "global_ordered_pairs_per_step": res.observed}
+    elif world > 1:
+        out["config"]["exchange"] = {"mode": "partial rows to owner(a) = a mod N, owner merge",
+                                     "entries_sent_rank0": res.sent_entries, "entries_recv_rank0": res.recv_entries,
                                      "bytes_per_entry": 8, "global_ordered_pairs_per_step": res.observed}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(up_h, it_h)

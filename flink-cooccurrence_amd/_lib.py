@@ -97,6 +97,10 @@ _SIGS = {
     "cooc_copy_rowsum_device": (ctypes.c_int, [vp, vp, vp]),
     "cooc_merge_partitions": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
                                              ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_shard_plan": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp,
+                                       ctypes.c_int64, vp, i64p, i64p]),
+    "cooc_shard_count": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int64, vp,
+                                        ctypes.c_int64, vp, ctypes.POINTER(CoocDeviceResult)]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }

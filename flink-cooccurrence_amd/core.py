@@ -174,6 +174,37 @@ class CooccurrenceCore:
             None if stream is None else ctypes.c_void_p(int(stream)), ctypes.byref(res)), self._h)
         return res
 
+    # ---- sharded records (multi-GPU owner routing of pair records) -------------------------------
+    @staticmethod
+    def shard_arena_cap(n_users: int, n_interactions: int) -> int:
+        """u16 arena ids cooc_shard_plan needs for a part (a multiple of 8)."""
+        return (n_interactions + 7 * max(n_users, 1) + 16 + 7) // 8 * 8
+
+    def shard_plan(self, user_ptr, items, n_parts: int, desc, row_counts, arena, stream=None):
+        """This part's users -> desc (int64 device [n_interactions]), row_counts (int32 device
+        [n_items], owner-major), arena (int16 device [>= shard_arena_cap]).  Returns (descriptors per
+        owner (np.int64 [n_parts]), arena ids used, this part's ordered pairs)."""
+        send = np.zeros(n_parts, np.int64)
+        info = np.zeros(2, np.int64)
+        n_users = int(user_ptr.numel()) - 1
+        check(_lib.load().cooc_shard_plan(
+            self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()), ctypes.c_void_p(items.data_ptr()),
+            int(items.numel()), n_parts, ctypes.c_void_p(desc.data_ptr()) if desc.numel() else None,
+            ctypes.c_void_p(row_counts.data_ptr()), ctypes.c_void_p(arena.data_ptr()), int(arena.numel()),
+            None if stream is None else ctypes.c_void_p(int(stream)), _p(send, i64p), _p(info, i64p)), self._h)
+        return send, int(info[0]), int(info[1])
+
+    def shard_count(self, n_parts: int, part: int, recv_row_counts, recv_desc, arena_all, arena_stride: int,
+                    stream=None) -> CoocDeviceResult:
+        """Owner `part`: complete rows part + r * n_parts from every source's records."""
+        res = CoocDeviceResult()
+        check(_lib.load().cooc_shard_count(
+            self._h, n_parts, part, ctypes.c_void_p(recv_row_counts.data_ptr()),
+            ctypes.c_void_p(recv_desc.data_ptr()) if recv_desc.numel() else None, int(recv_desc.numel()),
+            ctypes.c_void_p(arena_all.data_ptr()), int(arena_stride),
+            None if stream is None else ctypes.c_void_p(int(stream)), ctypes.byref(res)), self._h)
+        return res
+
     def set_kernel_timing(self, enable: bool = True) -> None:
         check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)
 

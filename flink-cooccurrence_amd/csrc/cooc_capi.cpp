@@ -228,6 +228,52 @@ int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part, const in
   return COOC_OK;
 }
 
+int cooc_shard_plan(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                    int64_t n_interactions, int32_t n_parts, uint64_t *d_desc, int32_t *d_row_counts,
+                    uint16_t *d_arena, int64_t arena_cap, void *hip_stream, int64_t *h_send, int64_t *h_info) {
+  if (!ctx || !h_send || !h_info || !d_row_counts || !d_arena) return COOC_ERR_ARG;
+  if (n_users < 0 || n_interactions < 0) return fail(ctx, COOC_ERR_ARG, "negative size");
+  if (n_interactions > 0 && (!d_user_ptr || !d_items || !d_desc)) return fail(ctx, COOC_ERR_ARG, "NULL input");
+  if (n_parts < 1) return fail(ctx, COOC_ERR_ARG, "n_parts must be >= 1");
+  (void)hipSetDevice(ctx->device);
+  ctx->have_batch = false;
+  Status s = ctx->counter.shard_plan(n_users, d_user_ptr, d_items, n_interactions, n_parts,
+                                     stream_of(ctx, hip_stream), d_desc, d_row_counts, d_arena, arena_cap, h_send,
+                                     h_info, h_info + 1);
+  return s.ok() ? COOC_OK : fail(ctx, s);
+}
+
+int cooc_shard_count(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t *d_recv_row_counts,
+                     const uint64_t *d_recv_desc, int64_t n_recv, const uint16_t *d_arena_all, int64_t arena_stride,
+                     void *hip_stream, cooc_device_result *out) {
+  if (!ctx || !out || !d_recv_row_counts || !d_arena_all) return COOC_ERR_ARG;
+  if (n_recv > 0 && !d_recv_desc) return fail(ctx, COOC_ERR_ARG, "NULL descriptors");
+  if (n_parts < 1) return fail(ctx, COOC_ERR_ARG, "n_parts must be >= 1");
+  (void)hipSetDevice(ctx->device);
+  ctx->have_batch = false;
+  hipStream_t s = stream_of(ctx, hip_stream);
+  cooc::CountResult r;
+  Status st = ctx->counter.shard_count(n_parts, part, d_recv_row_counts, d_recv_desc, n_recv, d_arena_all,
+                                       arena_stride, s, &r, ctx->timer.enabled ? &ctx->timer : nullptr);
+  if (!st.ok()) return fail(ctx, st);
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ctx, COOC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+  cooc::PlanTotals t;
+  st = ctx->counter.read_totals(&t);
+  if (!st.ok()) return fail(ctx, st);
+  if (t.err & 2) return fail(ctx, COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32");
+  out->n_items = ctx->counter.last_rows();
+  out->nnz = t.nnz_total;
+  out->observed = r.observed;
+  out->row_base = r.row_base;
+  out->row_nnz = r.row_nnz;
+  out->col = r.col;
+  out->cnt = r.cnt;
+  out->rowsum = r.rowsum;
+  out->dense = r.dense;
+  return COOC_OK;
+}
+
 int cooc_set_kernel_timing(cooc_ctx *ctx, int32_t enable) {
   if (!ctx) return COOC_ERR_ARG;
   ctx->timer.enabled = enable != 0;

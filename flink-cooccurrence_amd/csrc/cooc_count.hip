@@ -846,17 +846,112 @@ __global__ void k_batch_colscan(int32_t B, int32_t M, int32_t *__restrict__ bh, 
   rcnt[a] = run;
 }
 
+// ---- owner-major row order of the sharded records path (owner(a) = a mod W) --------------------
+// Row a sits at perm_rows(a) = (rows of owners < a mod W) + a / W; W == 1 is the identity.
+__host__ __device__ inline int32_t owner_rows_before(int32_t o, int32_t M, int32_t W) {
+  const int32_t q = M / W, rem = M % W;
+  return o * q + (o < rem ? o : rem);
+}
+
+__host__ __device__ inline int32_t perm_rows(int32_t a, int32_t M, int32_t W) {
+  return owner_rows_before(a % W, M, W) + a / W;
+}
+
+__host__ __device__ inline int32_t inv_perm_rows(int32_t k, int32_t M, int32_t W) {
+  const int32_t q = M / W, rem = M % W;
+  const int32_t big = rem * (q + 1);  // owners < rem hold q + 1 rows
+  const int32_t o = k < big ? k / (q + 1) : rem + (k - big) / q;
+  return o + (k - owner_rows_before(o, M, W)) * W;
+}
+
+struct PermCount {  // row count of the k-th row in owner-major order
+  const int32_t *rcnt;
+  int32_t M, W;
+  __host__ __device__ int64_t operator()(int32_t k) const {
+    return int64_t(rcnt[W == 1 ? k : inv_perm_rows(k, M, W)]);
+  }
+};
+
+__global__ void k_perm_counts(const int32_t *__restrict__ rcnt, int32_t M, int32_t W, int32_t *__restrict__ out) {
+  const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < M) out[k] = rcnt[inv_perm_rows(k, M, W)];
+}
+
+// send[o] = descriptors bound for owner o; send[W] = the padded arena size (ids).
+__global__ void k_send_counts(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ arena_ids, int32_t M,
+                              int32_t W, int64_t *__restrict__ send) {
+  const int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < W) send[o] = row_ptr[owner_rows_before(o + 1, M, W)] - row_ptr[owner_rows_before(o, M, W)];
+  if (o == 0) send[W] = *arena_ids;
+}
+
+// Owner side: contributions of owned row r over all sources.
+__global__ void k_sources_sum(const int32_t *__restrict__ recv_counts, int32_t W, int32_t R,
+                              int32_t *__restrict__ rcnt) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  int32_t t = 0;
+  for (int32_t s = 0; s < W; s++) t += recv_counts[int64_t(s) * R + r];
+  rcnt[r] = t;
+}
+
+// Owner side: one wave per owned row concatenates its sources' descriptor segments (source order)
+// into the row-contiguous list, moving each offset into the all-gathered arena (source s at
+// s * stride), and accumulates the contributions' statistics for the chunk plan.
+__global__ __launch_bounds__(256) void k_reorder_sources(const int32_t *__restrict__ recv_counts,
+                                                         const int64_t *__restrict__ seg_off,
+                                                         const uint64_t *__restrict__ recv_desc,
+                                                         const int64_t *__restrict__ row_ptr, int32_t W, int32_t R,
+                                                         int64_t stride, uint64_t *__restrict__ desc,
+                                                         PlanTotals *__restrict__ tot) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  uint64_t l_sum = 0, lpl_sum = 0, l_max = 0;
+  for (int64_t r = wave; r < R; r += n_waves) {
+    int64_t dst = row_ptr[r];
+    for (int32_t s = 0; s < W; s++) {
+      const int64_t k = int64_t(s) * R + r;
+      const int32_t c = recv_counts[k];
+      const int64_t src = seg_off[k];
+      const uint64_t shift = uint64_t(s) * uint64_t(stride);
+      for (int32_t i = lane; i < c; i += 64) {
+        const uint64_t d = recv_desc[src + i] + shift;  // offset field: low 40 bits, no carry
+        desc[dst + i] = d;
+        const uint64_t l = d >> 40;
+        l_sum += l;
+        lpl_sum += l * ((l + 7) & ~uint64_t(7));
+        l_max = l > l_max ? l : l_max;
+      }
+      dst += c;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    l_sum += __shfl_xor(l_sum, o, 64);
+    lpl_sum += __shfl_xor(lpl_sum, o, 64);
+    const uint64_t m = __shfl_xor(l_max, o, 64);
+    l_max = m > l_max ? m : l_max;
+  }
+  if (lane == 0 && l_sum) {
+    atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_l2), (unsigned long long)l_sum);
+    atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_lpl), (unsigned long long)lpl_sum);
+    atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_len), (unsigned long long)l_max);
+  }
+}
+
 __global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(int64_t n, int32_t B, const int64_t *__restrict__ up,
                                                                 const int32_t *__restrict__ items,
                                                                 const int32_t *__restrict__ uidx,
                                                                 const int64_t *__restrict__ poff,
                                                                 const int64_t *__restrict__ row_ptr, int32_t M,
-                                                                const int32_t *__restrict__ bh,
+                                                                int32_t W, const int32_t *__restrict__ bh,
                                                                 uint64_t *__restrict__ desc) {
   extern __shared__ uint32_t next_pos[];  // [M] next free position of each row inside this block's share
   const int tid = threadIdx.x, b = blockIdx.x;
   const int32_t *row = bh + int64_t(b) * M;
-  for (int32_t a = tid; a < M; a += kPlanThreads) next_pos[a] = uint32_t(row_ptr[a] + row[a]);
+  // row_ptr is in owner-major row order (perm_rows; the identity when W == 1)
+  for (int32_t a = tid; a < M; a += kPlanThreads)
+    next_pos[a] = uint32_t(row_ptr[W == 1 ? a : perm_rows(a, M, W)] + row[a]);
   __syncthreads();
   int64_t p0, p1;
   block_range(n, B, b, &p0, &p1);
@@ -938,8 +1033,8 @@ __device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
 template <int U, int S, bool DENSE, int X = 0, int ST = 1>
 __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
     const Chunk *__restrict__ chunks, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
-    const uint64_t *__restrict__ desc, const uint16_t *__restrict__ arena, int32_t M, int32_t db,
-    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump,
+    const uint64_t *__restrict__ desc, const uint16_t *__restrict__ arena, int32_t M, int32_t db, int32_t W,
+    int32_t part, int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump,
     int64_t bump_cap, int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, uint32_t *__restrict__ staging,
     int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, uint32_t *__restrict__ dense) {
   constexpr uint32_t kWalkers = kAccThreads / S;
@@ -1058,7 +1153,8 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       __syncthreads();
     }
     if (tid == 0) s_chunk = nxt;
-    // every contribution is a new position of item c.row: the -1 self term at column c.row
+    // every contribution is a new position of the row's item: the -1 self term at its column.  Rows
+    // are local (output) indices; the row's item is part + row * W (W parts of the sharded path).
     const int64_t n_c = c.end - c.begin;
     const uint64_t len_sum = block_sum_u64(my_len, s_red);  // (its barriers publish s_chunk)
     const int64_t chunk_rowsum = int64_t(len_sum) - n_c;
@@ -1067,7 +1163,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
     const uint64_t d2 = (tid < db && c2.begin + tid < c2.end) ? desc[c2.begin + tid] : 0;
     if (tid == 0) {
       acc[M] = 0;
-      acc[c.row] -= uint32_t(n_c);
+      acc[part + c.row * W] -= uint32_t(n_c);
       atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
       if (c.split >= 0)
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
@@ -1130,11 +1226,12 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
 }
 
 // Dense output: rows of items without interactions (no chunk) are zero; one wave per row.
-__global__ void k_zero_empty_rows(const int32_t *__restrict__ rcnt, int32_t M, uint32_t *__restrict__ dense) {
+__global__ void k_zero_empty_rows(const int32_t *__restrict__ rcnt, int32_t R, int32_t M,
+                                  uint32_t *__restrict__ dense) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t a = wave; a < M; a += n_waves) {
+  for (int64_t a = wave; a < R; a += n_waves) {
     if (rcnt[a] != 0) continue;
     uint32_t *d = dense + a * M;
     for (int32_t b = lane; b < M; b += 64) d[b] = 0;
@@ -1690,15 +1787,20 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
   return Status::Ok();
 }
 
-Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
-                          CountResult *out, KernelTimer *timer) {
+// ---- batch path, phase 1: local plan (arena, row counts, descriptors in owner-major row order) ----
+// W > 1 (sharded records): rows are laid out owner by owner (owner(a) = a mod W, perm_rows), so the
+// descriptors bound for one owner are contiguous.  W == 1: natural row order.
+Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
+                           uint64_t *desc, uint16_t *arena, int64_t arena_cap) {
   const int32_t M = M_;
-  if (!batch_ok()) return Status{1, "run_batch needs n_items < " + std::to_string(kBatchMaxItems)};
+  if (!batch_ok()) return Status{1, "the batch path needs n_items < " + std::to_string(kBatchMaxItems)};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
   if (U > int64_t(INT32_MAX)) return Status{1, "more than 2^31 users in one window"};
+  if (W < 1 || W > M) return Status{1, "n_parts must be in [1, n_items]"};
   // partition blocks of the hist / scatter passes: one per CU, fewer for tiny inputs
   const int32_t B = int32_t(std::max<int64_t>(1, std::min<int64_t>(n_cu_, n / 4096 + 1)));
   const int64_t U1 = std::max<int64_t>(U, 1);
+  if (arena_cap < n + 7 * U1 + 16) return Status{1, "arena buffer smaller than n + 7 n_users + 16 ids"};
   COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
   COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
   COOC_TRY(plen_.reserve(sizeof(int64_t) * U1));
@@ -1708,47 +1810,24 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   COOC_TRY(bh_.reserve(sizeof(int32_t) * size_t(B) * M));
   COOC_TRY(rcnt_.reserve(sizeof(int32_t) * M));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
-  COOC_TRY(desc_.reserve(sizeof(uint64_t) * (n + 1)));
-  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
-  COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
-  COOC_TRY(order_.reserve(sizeof(int32_t) * M * 2));
-  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(row_split_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (M + 1)));
-  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * (M + 1)));
-  COOC_TRY(split_row_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
-  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
-  COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
   PlanTotals *tot = tot_.as<PlanTotals>();
   int64_t *plen = plen_.as<int64_t>(), *poff = poff_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
   int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *uidx = uidx_.as<int32_t>();
   COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
-  COOC_HIP_TRY(hipMemsetAsync(queue_.p, 0, sizeof(int32_t) * 4, s));
-  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * M, s));
-  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * M, s));
-  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t) * (M + 1), s));
-  COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
   COOC_HIP_TRY(hipMemsetAsync(poff, 0, sizeof(int64_t), s));
   COOC_HIP_TRY(hipMemsetAsync(row_ptr, 0, sizeof(int64_t), s));
   if (U > 0) {
     k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, plen, tot);
     COOC_HIP_TRY(hipGetLastError());
   }
-  // hipCUB temp storage for every scan / sort of the plan
-  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> cnt64(rcnt, WidenI64{});
+  // row counts in owner-major order -> row_ptr (prefix); the identity order when W == 1
+  hipcub::CountingInputIterator<int32_t> rows(0);
+  hipcub::TransformInputIterator<int64_t, PermCount, hipcub::CountingInputIterator<int32_t>> cnt_perm(
+      rows, PermCount{rcnt, M, W});
   size_t tmp = 0, q = 0;
   COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, poff + 1, int(U1), s));
   tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, cnt64, row_ptr + 1, M, s));
-  tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint32_t>(),
-                                                            order_keys_.as<uint32_t>(), order_.as<int32_t>() + M,
-                                                            order_.as<int32_t>(), M, 0, 32, s));
-  tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, M, s));
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, cnt_perm, row_ptr + 1, M, s));
   tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
   if (U > 0) {
@@ -1757,14 +1836,11 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   }
   // padded arena: every list 16-B aligned and padded to 8 ids with the sink id M; one pad group
   // at the end (never referenced by a segment, keeps the last 16-B load in bounds)
-  const int64_t arena_cap = n + 7 * U1 + 16;
-  COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
   const size_t lds_m = sizeof(uint32_t) * size_t(M);
   if (U > 0) {
-    k_batch_fill<<<blocks_for(U, 256), 256, 0, s>>>(U, up, poff, M, uidx, tarena_.as<uint16_t>(), long_.as<int32_t>(),
-                                                   tot);
+    k_batch_fill<<<blocks_for(U, 256), 256, 0, s>>>(U, up, poff, M, uidx, arena, long_.as<int32_t>(), tot);
     k_batch_fill_long<<<256, 256, 0, s>>>(up, long_.as<int32_t>(), tot, uidx);
-    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, M, tarena_.as<uint16_t>(), bh, tot);
+    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, M, arena, bh, tot);
     k_batch_colscan<<<blocks_for(M, 256), 256, 0, s>>>(B, M, bh, rcnt);
   } else {
     COOC_HIP_TRY(hipMemsetAsync(rcnt, 0, sizeof(int32_t) * M, s));
@@ -1772,36 +1848,73 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   COOC_HIP_TRY(hipGetLastError());
   {
     size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt64, row_ptr + 1, M, s));
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt_perm, row_ptr + 1, M, s));
   }
   if (U > 0) {
-    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, bh, desc_.as<uint64_t>());
+    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, W, bh, desc);
     COOC_HIP_TRY(hipGetLastError());
   }
+  return Status::Ok();
+}
+
+// ---- batch path, phase 2: accumulate R rows (row r = global item part + r * W) whose contributions
+// are desc[row_ptr[r] .. row_ptr[r + 1]); tot already holds the contributions' statistics
+// (sum_l2 = sum of list lengths, sum_lpl, max_len, err).  Synchronises `s` once.
+Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_t *row_ptr, const int32_t *rcnt,
+                                const uint64_t *desc, const uint16_t *arena, int64_t n, hipStream_t s,
+                                CountResult *out, KernelTimer *timer) {
+  const int32_t M = M_;
+  const int32_t R1 = std::max<int32_t>(R, 1);
+  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * R1));
+  COOC_TRY(row_work_.reserve(sizeof(uint64_t) * R1));
+  COOC_TRY(order_.reserve(sizeof(int32_t) * R1 * 2));
+  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * R1));
+  COOC_TRY(row_split_.reserve(sizeof(int32_t) * R1));
+  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * R1));
+  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (R1 + 1)));
+  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * (R1 + 1)));
+  COOC_TRY(split_row_.reserve(sizeof(int32_t) * R1));
+  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (R1 + 1)));
+  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * R1));
+  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * R1));
+  COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
+  PlanTotals *tot = tot_.as<PlanTotals>();
+  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * R1, s));
+  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * R1, s));
+  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t) * (R1 + 1), s));
+  COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
+  size_t tmp = 0, q = 0;
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint32_t>(),
+                                                            order_keys_.as<uint32_t>(), order_.as<int32_t>() + R1,
+                                                            order_.as<int32_t>(), R1, 0, 32, s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, R1, s));
+  tmp = std::max(tmp, q);
+  COOC_TRY(sort_tmp_.reserve(tmp));
   // chunk plan: rows by contribution count, heaviest first
   int32_t *order = order_.as<int32_t>();
-  k_batch_plan<<<blocks_for(M, 256), 256, 0, s>>>(rcnt, M, tot, n, row_work_.as<uint32_t>(), order + M,
-                                                  row_nch_.as<int32_t>(), row_split_.as<int32_t>());
-  {
+  if (R > 0) {
+    k_batch_plan<<<blocks_for(R, 256), 256, 0, s>>>(rcnt, R, tot, n, row_work_.as<uint32_t>(), order + R,
+                                                    row_nch_.as<int32_t>(), row_split_.as<int32_t>());
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint32_t>(),
-                                                              order_keys_.as<uint32_t>(), order + M, order, M, 0,
-                                                              32, s));
+                                                              order_keys_.as<uint32_t>(), order + R, order, R, 0, 32,
+                                                              s));
+    k_gather_i32<<<blocks_for(R, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), R, ord_nch_.as<int32_t>());
   }
-  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
   COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
   COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
-  {
+  if (R > 0) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
-                                                  M, s));
+                                                  R, s));
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
-                                                  split_slot_.as<int32_t>() + 1, M, s));
+                                                  split_slot_.as<int32_t>() + 1, R, s));
+    k_split_rows<<<blocks_for(R, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), R,
+                                                    split_row_.as<int32_t>());
   }
-  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
-                                                  split_row_.as<int32_t>());
-  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>(), M, tot, queue_.as<int32_t>());
+  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>(), R, tot, queue_.as<int32_t>());
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
@@ -1810,46 +1923,46 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
   const int64_t work_total = h_tot_->sum_l2;
   const int64_t pairs = work_total - n;
-  // Output layout.  Dense uint32 [M x M] when the pairs cover the matrix (P >= M^2 / 2: dense is then
+  // Output layout.  Dense uint32 [R x M] when the pairs cover the matrix (P >= R M / 2: dense is then
   // no larger than the sparse (col, cnt) entries it replaces, and written with plain coalesced row
   // stores) and it fits in 40% of free HBM; else the sparse bump-allocated padded CSR, whose entries
-  // are at most min(M^2, P).
-  const int64_t MM = int64_t(M) * M;
+  // are at most min(R M, P).
+  const int64_t RM = int64_t(R) * M;
   bool dense = output_pref_ == 2;
-  if (output_pref_ == 0 && 2 * pairs >= MM) {
+  if (output_pref_ == 0 && 2 * pairs >= RM) {
     size_t free_b = 0, total_b = 0;
     COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    dense = size_t(MM) * sizeof(uint32_t) <= free_b / 10 * 4 + dense_.cap;
+    dense = size_t(RM) * sizeof(uint32_t) <= free_b / 10 * 4 + dense_.cap;
   }
   dense_mode_ = dense;
+  last_rows_ = R;
   bump_mode_ = false;  // the bump region IS the sparse output (one column tile): no gather
   if (dense) {
-    COOC_TRY(dense_.reserve(sizeof(uint32_t) * size_t(std::max<int64_t>(MM, 1))));
+    COOC_TRY(dense_.reserve(sizeof(uint32_t) * size_t(std::max<int64_t>(RM, 1))));
   } else {
-    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(MM, pairs));
+    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(RM, pairs));
     COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
     COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
   }
-  if (dense && n_chunks == 0 && MM > 0) COOC_HIP_TRY(hipMemsetAsync(dense_.p, 0, sizeof(uint32_t) * size_t(MM), s));
+  if (dense && n_chunks == 0 && RM > 0) COOC_HIP_TRY(hipMemsetAsync(dense_.p, 0, sizeof(uint32_t) * size_t(RM), s));
   if (n_chunks > 0) {
     COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
     COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
     COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
     if (dense) {
       // rows without contributions stay all-zero; rows of several chunks are zeroed, then added into
-      COOC_TRY(zero_unplanned_rows(s));
-      if (n_split > 0) {
+      k_zero_empty_rows<<<std::min<unsigned>(blocks_for(R, 4), 4096), 256, 0, s>>>(rcnt, R, M, dense_.as<uint32_t>());
+      if (n_split > 0)
         k_zero_rows<<<unsigned(std::min<int64_t>(n_split, 4 * int64_t(n_cu_))), 1024, 0, s>>>(
             split_row_.as<int32_t>(), tot, M, dense_.as<uint32_t>());
-        COOC_HIP_TRY(hipGetLastError());
-      }
+      COOC_HIP_TRY(hipGetLastError());
     } else if (n_split > 0) {
       const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
       COOC_TRY(staging_.reserve(need));
       COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
     }
-    k_batch_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
-                                                      row_ptr, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
+    k_batch_chunks<<<blocks_for(R, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
+                                                      row_ptr, split_slot_.as<int32_t>(), R, chunks_.as<Chunk>());
     COOC_HIP_TRY(hipGetLastError());
     const size_t acc_bytes = sizeof(uint32_t) * size_t((M + 2) & ~1);
     const int db = int(std::min<int64_t>(1024, (int64_t(kBatchLdsBudget) - int64_t(acc_bytes) - 4) / 12));
@@ -1864,9 +1977,8 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
               : xmode_ == 4 ? k_acc_batch<4, 8, false, 4> : xmode_ == 8 ? k_acc_batch<4, 8, false, 8>
               : store_mode_ == 3 ? k_acc_batch<4, 8, false, 0, 3> : k_acc_batch<4, 8, false>;
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-    kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(),
-                                                  desc_.as<uint64_t>(), tarena_.as<uint16_t>(), M, db,
-                                                  col_.as<int32_t>(), cnt_.as<uint32_t>(),
+    kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), desc, arena, M, db,
+                                                  W, part, col_.as<int32_t>(), cnt_.as<uint32_t>(),
                                                   bump_.as<unsigned long long>(), bump_cap_, row_base_.as<int64_t>(),
                                                   row_nnz_.as<int32_t>(), staging_.as<uint32_t>(),
                                                   split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
@@ -1890,7 +2002,7 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
     COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
   }
-  k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
+  if (R > 0) k_nnz_total<<<std::min<unsigned>(blocks_for(R, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), R, tot);
   COOC_HIP_TRY(hipGetLastError());
   out->row_base = dense ? nullptr : row_base_.as<int64_t>();
   out->row_nnz = row_nnz_.as<int32_t>();
@@ -1904,12 +2016,81 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   return Status::Ok();
 }
 
-// Dense output: rows that no chunk writes (items without interactions) must read as zero.
-Status Counter::zero_unplanned_rows(hipStream_t s) {
-  k_zero_empty_rows<<<std::min<unsigned>(blocks_for(M_, 4), 4096), 256, 0, s>>>(rcnt_.as<int32_t>(), M_,
-                                                                                  dense_.as<uint32_t>());
+Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
+                          CountResult *out, KernelTimer *timer) {
+  const int64_t U1 = std::max<int64_t>(U, 1);
+  const int64_t arena_cap = n + 7 * U1 + 16;
+  COOC_TRY(desc_.reserve(sizeof(uint64_t) * (n + 1)));
+  COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
+  COOC_TRY(plan_local(U, up, items, n, 1, s, desc_.as<uint64_t>(), tarena_.as<uint16_t>(), arena_cap));
+  return accumulate_rows(M_, 1, 0, row_ptr_.as<int64_t>(), rcnt_.as<int32_t>(), desc_.as<uint64_t>(),
+                         tarena_.as<uint16_t>(), n, s, out, timer);
+}
+
+// ---- sharded records (W parts): local plan of this part's users -------------------------------
+Status Counter::shard_plan(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
+                           uint64_t *desc, int32_t *row_counts, uint16_t *arena, int64_t arena_cap, int64_t *h_send,
+                           int64_t *h_arena_ids, int64_t *h_observed) {
+  COOC_TRY(plan_local(U, up, items, n, W, s, desc, arena, arena_cap));
+  COOC_TRY(send_.reserve(sizeof(int64_t) * (W + 1)));
+  k_perm_counts<<<blocks_for(M_, 256), 256, 0, s>>>(rcnt_.as<int32_t>(), M_, W, row_counts);
+  k_send_counts<<<blocks_for(W, 256), 256, 0, s>>>(row_ptr_.as<int64_t>(), poff_.as<int64_t>() + U, M_, W,
+                                                   send_.as<int64_t>());
   COOC_HIP_TRY(hipGetLastError());
+  std::vector<int64_t> h(W + 1);
+  COOC_HIP_TRY(hipMemcpyAsync(h.data(), send_.p, sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot_.p, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+  for (int32_t o = 0; o < W; o++) h_send[o] = h[o];
+  *h_arena_ids = U > 0 ? h[W] : 0;
+  *h_observed = h_tot_->sum_l2 - n;
   return Status::Ok();
 }
+
+// ---- sharded records: owner side.  recv_counts [W x R] (source-major row counts), recv_desc the
+// sources' descriptor segments in source order (offsets into each source's own arena), arena_all
+// the all-gathered arenas (source s at s * arena_stride ids).
+Status Counter::shard_count(int32_t W, int32_t part, const int32_t *recv_counts, const uint64_t *recv_desc,
+                            int64_t n_recv, const uint16_t *arena_all, int64_t arena_stride, hipStream_t s,
+                            CountResult *out, KernelTimer *timer) {
+  const int32_t M = M_;
+  if (!batch_ok()) return Status{1, "the batch path needs n_items < " + std::to_string(kBatchMaxItems)};
+  if (W < 1 || part < 0 || part >= W) return Status{1, "part outside [0, n_parts)"};
+  if (n_recv > int64_t(INT32_MAX)) return Status{1, "more than 2^31 contributions for one owner"};
+  if (arena_stride % 8 != 0) return Status{1, "arena_stride must be a multiple of 8 ids"};
+  const int32_t R = M > part ? (M - part + W - 1) / W : 0;
+  const int64_t K = int64_t(W) * R;
+  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
+  COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
+  COOC_TRY(rcnt_.reserve(sizeof(int32_t) * (R + 1)));
+  COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (R + 1)));
+  COOC_TRY(seg_off_.reserve(sizeof(int64_t) * (K + 1)));
+  COOC_TRY(desc_.reserve(sizeof(uint64_t) * (n_recv + 1)));
+  PlanTotals *tot = tot_.as<PlanTotals>();
+  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
+  COOC_HIP_TRY(hipMemsetAsync(row_ptr_.p, 0, sizeof(int64_t), s));
+  if (R > 0) k_sources_sum<<<blocks_for(R, 256), 256, 0, s>>>(recv_counts, W, R, rcnt_.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> own64(rcnt_.as<int32_t>(), WidenI64{});
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> seg64(recv_counts, WidenI64{});
+  size_t b1 = 0, b2 = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b1, own64, row_ptr_.as<int64_t>() + 1, std::max(R, 1), s));
+  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, seg64, seg_off_.as<int64_t>(), int(std::max<int64_t>(K, 1)), s));
+  COOC_TRY(sort_tmp_.reserve(std::max(b1, b2)));
+  if (R > 0) {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, own64, row_ptr_.as<int64_t>() + 1, R, s));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, seg64, seg_off_.as<int64_t>(), int(K), s));
+    k_reorder_sources<<<std::min<unsigned>(blocks_for(int64_t(R) * 64, 256), 8192), 256, 0, s>>>(
+        recv_counts, seg_off_.as<int64_t>(), recv_desc, row_ptr_.as<int64_t>(), W, R, arena_stride,
+        desc_.as<uint64_t>(), tot);
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  return accumulate_rows(R, W, part, row_ptr_.as<int64_t>(), rcnt_.as<int32_t>(), desc_.as<uint64_t>(), arena_all,
+                         n_recv, s, out, timer);
+}
+
 
 }  // namespace cooc

@@ -129,6 +129,20 @@ class Counter {
   Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                    CountResult *out, KernelTimer *timer = nullptr);
   bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems; }
+
+  // Sharded records (W parts, owner(a) = a mod W).  shard_plan: this part's users -> its padded
+  // u16 arena (arena[arena_cap >= n + 7 U + 16]), descriptors grouped by owner (desc[n]) and row
+  // counts in owner-major order (row_counts[n_items]); h_send[W] descriptors per owner, the arena's
+  // ids and this part's ordered pairs.  Synchronises `stream`.
+  Status shard_plan(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, int32_t W,
+                    hipStream_t stream, uint64_t *desc, int32_t *row_counts, uint16_t *arena, int64_t arena_cap,
+                    int64_t *h_send, int64_t *h_arena_ids, int64_t *h_observed);
+  // shard_count: the owned rows (part + r W) from every source's row counts [W x R] and descriptor
+  // segments (source order) over the all-gathered arenas (source s at s * arena_stride ids).
+  Status shard_count(int32_t W, int32_t part, const int32_t *recv_counts, const uint64_t *recv_desc, int64_t n_recv,
+                     const uint16_t *arena_all, int64_t arena_stride, hipStream_t stream, CountResult *out,
+                     KernelTimer *timer = nullptr);
+  int32_t last_rows() const { return last_rows_; }
   static constexpr int32_t kBatchMaxItems = 40320;
 
   // Output layout of run_batch: 0 = auto (dense when P >= M^2 / 2), 1 = sparse CSR, 2 = dense.
@@ -150,7 +164,11 @@ class Counter {
 
  private:
   Status run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
-  Status zero_unplanned_rows(hipStream_t s);
+  Status plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
+                    uint64_t *desc, uint16_t *arena, int64_t arena_cap);
+  Status accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_t *row_ptr, const int32_t *rcnt,
+                         const uint64_t *desc, const uint16_t *arena, int64_t n, hipStream_t s, CountResult *out,
+                         KernelTimer *timer);
 
   int32_t M_ = 0;
   int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)
@@ -179,7 +197,8 @@ class Counter {
   int store_mode_ = 1;                // COOC_ACC_STORE: output stores 1 plain, 2 sc1, 3 nt (A/B)
   int output_pref_ = 0;               // set_output_layout
   bool dense_mode_ = false;           // the last run's output is dense_
-  DevBuf dense_;
+  DevBuf dense_, send_;
+  int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
   int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
   PlanTotals *h_tot_ = nullptr;  // pinned
 };

@@ -1,5 +1,15 @@
 """Multi-GPU sharding layer: users sharded over ranks, rows owned by a mod world.
 
+Two exchanges are implemented, both keyed by owner(a) = a mod world (the reference's
+keyBy(ItemCooccurrences::getItem), FlinkCooccurrences.java:152):
+
+* ``count_records`` (default) routes the pair RECORDS: every rank all-gathers the users' u16
+  histories once (input sized) and all-to-alls one 8-B descriptor per (row, user) record to the
+  row's owner, which then reduces complete rows.  Exchanged bytes ~ 2 N + 8 N per rank.
+* ``count_sharded`` routes PARTIAL COUNTS: every rank reduces its own users, packs its partial
+  rows by owner and the owner merges them.  Exchanged bytes ~ 8 D per rank (D = distinct keys of
+  a rank's partial result, up to n_items^2), which dominates on dense co-occurrence data.
+
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Mirrors the
 reference's keyed data-parallelism:
 
@@ -74,3 +84,52 @@ def count_sharded(core, user_ptr, items, group=None, stream=None) -> ShardResult
 def _sync(dev, stream):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+@dataclass
+class RecordsResult:
+    part: int
+    n_parts: int
+    owned: object           # CoocDeviceResult of the owned rows (rows r -> items part + r * n_parts), complete
+    observed: int           # global ordered pairs (sum over ranks)
+    local_observed: int     # this rank's users' ordered pairs
+    sent_records: int
+    recv_records: int
+    arena_stride: int
+
+
+def count_records(core, user_ptr, items, group=None, stream=None) -> RecordsResult:
+    """One window over this rank's users; pair records routed to owner(a) and reduced there."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = items.device
+    M = core.n_items
+    n_users, n = int(user_ptr.numel()) - 1, int(items.numel())
+    # every rank's arena slot has the same size (all_gather_into_tensor): the largest part's need
+    cap = torch.tensor([core.shard_arena_cap(n_users, n)], dtype=torch.int64, device=dev)
+    dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)
+    stride = int(cap.item())
+    arena = torch.empty(stride, dtype=torch.int16, device=dev)
+    desc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    row_counts = torch.empty(M, dtype=torch.int32, device=dev)
+    send, _arena_ids, local_obs = core.shard_plan(user_ptr, items, world, desc, row_counts, arena, stream)
+    arena_all = torch.empty(world * stride, dtype=torch.int16, device=dev)
+    # u16 ids travel as int32 pairs (RCCL has no 16-bit integer type; the stride is a multiple of 8 ids)
+    work = dist.all_gather_into_tensor(arena_all.view(torch.int32), arena.view(torch.int32), group=group,
+                                       async_op=True)
+    counts = torch.as_tensor(send, dtype=torch.int64, device=dev)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    R = rows_owned(M, world, rank)
+    recv_rc = torch.empty(world * R, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(recv_rc, row_counts, [R] * world, [rows_owned(M, world, o) for o in range(world)],
+                           group=group)
+    recv_h = recv_counts.cpu().tolist()
+    recv_desc = torch.empty(sum(recv_h), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_desc, desc, recv_h, send.tolist(), group=group)
+    obs = torch.tensor([local_obs], dtype=torch.int64, device=dev)
+    dist.all_reduce(obs, group=group)
+    work.wait()
+    _sync(dev, stream)
+    owned = core.shard_count(world, rank, recv_rc, recv_desc, arena_all, stride, stream)
+    return RecordsResult(rank, world, owned, int(obs.item()), int(local_obs), n, int(sum(recv_h)), stride)

@@ -205,6 +205,31 @@ COOC_API int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part,
                                    const uint64_t *d_recv_entries, const int64_t *d_rowsum_global, void *hip_stream,
                                    cooc_device_result *out);
 
+/* ---- sharded records (multi-GPU: the keyBy(itemA) of FlinkCooccurrences.java:152 on pair RECORDS) -
+ * Users are sharded over n_parts GPUs (keyBy(user), :70); row a is owned by part a mod n_parts.  The
+ * reference ships each pair record (itemA, the user's history) to the owner of itemA; here every
+ * part ships its users' histories once (the caller all-gathers the u16 arenas) and one 8-B
+ * descriptor per record (the caller all-to-alls them by owner), and each owner reduces complete
+ * rows: no partial counts are exchanged and nothing is merged.
+ *   cooc_shard_plan   this part's users -> into caller DEVICE buffers: d_desc uint64[n_interactions]
+ *                     (descriptors grouped by owner, then by owned row), d_row_counts int32[n_items]
+ *                     (row counts in the same owner-major order: owner o's rows_owned(o) counts are
+ *                     contiguous), d_arena uint16[arena_cap >= n_interactions + 7 n_users + 16];
+ *                     h_send[n_parts] = descriptors per owner, h_info[0] = arena ids used (a multiple
+ *                     of 8), h_info[1] = this part's ordered pairs.
+ *   cooc_shard_count  owner `part`: d_recv_row_counts int32[n_parts * rows_owned] and d_recv_desc
+ *                     (source-major, as delivered by the all-to-all), d_arena_all the all-gathered
+ *                     arenas with source s at s * arena_stride ids.  Result rows r = 0..n_rows-1 are
+ *                     items part + r * n_parts (borrowed device views in *out; out->n_items = rows
+ *                     owned), complete: counts, row sums and the overflow check are final. */
+COOC_API int cooc_shard_plan(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                             int64_t n_interactions, int32_t n_parts, uint64_t *d_desc, int32_t *d_row_counts,
+                             uint16_t *d_arena, int64_t arena_cap, void *hip_stream, int64_t *h_send,
+                             int64_t *h_info);
+COOC_API int cooc_shard_count(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t *d_recv_row_counts,
+                              const uint64_t *d_recv_desc, int64_t n_recv, const uint16_t *d_arena_all,
+                              int64_t arena_stride, void *hip_stream, cooc_device_result *out);
+
 /* ---- diagnostics (not part of the reference surface) ------------------------------------------
  * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the
  * stream it is launched on; read back after a call that ran it. */

@@ -486,3 +486,71 @@ def test_c2_scale_topk_rows(pkg, oracle, torch_cuda):
         assert np.allclose(gs[fin], ws[fin], rtol=1e-6, atol=1e-9)
         if np.allclose(gs[fin], ws[fin], rtol=0, atol=0):
             assert np.array_equal(vals[a, :sizes[a]], wv)  # identical scores -> identical heap layout
+
+
+@pytest.mark.parametrize("W,output", [(2, "dense"), (3, "csr"), (4, "dense"), (3, "dense")])
+def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output):
+    """The sharded-records entry points on one GPU: W user shards planned separately, the collectives
+    done by slicing (all-gather of the arenas, all-to-all of row counts and descriptors), each owner's
+    rows complete and equal to C of all users together."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen, sharding
+
+    up, it = datagen.small_log(33, 1800, 700, 25.0)
+    M, U = 700, len(up) - 1
+    dev = torch.device("cuda")
+    shards = []
+    for p in range(W):
+        lo, hi = p * U // W, (p + 1) * U // W
+        shards.append((up[lo:hi + 1] - up[lo], it[up[lo]:up[hi]]))
+    stride = max(pkg.CooccurrenceCore.shard_arena_cap(len(s[0]) - 1, len(s[1])) for s in shards)
+    cores, parts = [], []
+    for sup, sit in shards:
+        core = pkg.CooccurrenceCore(n_items=M, device=0, output=output)
+        n = len(sit)
+        desc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+        rc = torch.empty(M, dtype=torch.int32, device=dev)
+        arena = torch.full((stride,), -1, dtype=torch.int16, device=dev)
+        send, ids, obs = core.shard_plan(torch.from_numpy(sup).to(dev), torch.from_numpy(sit).to(dev), W, desc, rc,
+                                         arena)
+        assert ids % 8 == 0 and ids <= stride and int(send.sum()) == n
+        cores.append(core)
+        parts.append((send, rc, desc, arena, obs))
+    torch.cuda.synchronize()
+    arena_all = torch.cat([p[3] for p in parts])
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert sum(p[4] for p in parts) == observed
+    for o in range(W):
+        R = sharding.rows_owned(M, W, o)
+        before = sum(sharding.rows_owned(M, W, q) for q in range(o))
+        recv_rc = torch.cat([p[1][before:before + R] for p in parts])
+        recv_desc = torch.cat([p[2][int(p[0][:o].sum()):int(p[0][:o + 1].sum())] for p in parts])
+        res = cores[o].shard_count(W, o, recv_rc, recv_desc, arena_all, stride)
+        torch.cuda.synchronize()
+        assert res.n_items == R
+        nnz = _d2h(res.row_nnz, R, np.int32)
+        rs = _d2h(res.rowsum, R, np.int64)
+        if output == "dense":
+            assert res.dense and not res.col
+            dense = _d2h(res.dense, R * M, np.uint32).reshape(R, M).astype(np.int64)
+        else:
+            assert res.col and not res.dense
+            base = _d2h(res.row_base, R, np.int64)
+            cap = int((base + nnz).max()) if R else 0
+            mc, mn = _d2h(res.col, cap, np.int32), _d2h(res.cnt, cap, np.uint32).astype(np.int64)
+        total = 0
+        for r in range(R):
+            a = o + r * W
+            s, e = rp[a], rp[a + 1]
+            assert nnz[r] == e - s and rs[r] == rowsums[a]
+            if output == "dense":
+                row = np.zeros(M, np.int64)
+                row[cols[s:e]] = data[s:e]
+                assert np.array_equal(dense[r], row)
+            else:
+                assert np.array_equal(mc[base[r]:base[r] + nnz[r]], cols[s:e])
+                assert np.array_equal(mn[base[r]:base[r] + nnz[r]], data[s:e])
+            total += e - s
+        assert res.nnz == total
+    for c in cores:
+        c.close()

@@ -70,7 +70,66 @@ class FakeCore:
         return rows
 
 
-def _worker(rank, world, port, up_all, it_all, M, out_q):
+class FakeRecordsCore:
+    """numpy double of the sharded-records entry points, restating their buffer contract
+    (include/cooc.h: cooc_shard_plan / cooc_shard_count): padded u16 arena with sink id M, 8-B
+    descriptors (n_u << 40 | arena offset) grouped by owner then owned row, owner-major row counts."""
+
+    def __init__(self, n_items):
+        self.n_items = n_items
+
+    @staticmethod
+    def shard_arena_cap(n_users, n):
+        return (n + 7 * max(n_users, 1) + 16 + 7) // 8 * 8
+
+    def shard_plan(self, user_ptr, items, W, desc, row_counts, arena, stream=None):
+        M = self.n_items
+        up, it = user_ptr.numpy(), items.numpy()
+        lens = np.diff(up)
+        plen = (lens + 7) // 8 * 8
+        poff = np.concatenate([[0], np.cumsum(plen)])
+        ar = np.full(len(arena), M, np.int64)
+        for j in range(len(lens)):
+            ar[poff[j]:poff[j] + lens[j]] = it[up[j]:up[j + 1]]
+        arena.copy_(torch.from_numpy(ar.astype(np.uint16).view(np.int16)))
+        users = np.repeat(np.arange(len(lens)), lens)
+        owner_rows = [list(range(o, M, W)) for o in range(W)]
+        order = [a for rows in owner_rows for a in rows]
+        d, rc = [], []
+        for a in order:
+            js = users[it == a]
+            rc.append(len(js))
+            d.extend(int((lens[j] << 40) | poff[j]) for j in js)
+        if len(d):
+            desc.copy_(torch.tensor(d, dtype=torch.int64))
+        row_counts.copy_(torch.tensor(rc, dtype=torch.int32))
+        send = np.array([sum(rc[len(sum(owner_rows[:o], [])):len(sum(owner_rows[:o + 1], []))]) for o in range(W)],
+                        np.int64)
+        return send, int(poff[-1]), int(np.sum(lens * (lens - 1)))
+
+    def shard_count(self, W, part, recv_rc, recv_desc, arena_all, stride, stream=None):
+        M = self.n_items
+        R = len(range(part, M, W))
+        rc = recv_rc.numpy().reshape(W, R)
+        d = recv_desc.numpy().astype(np.uint64)
+        ar = arena_all.numpy().view(np.uint16).astype(np.int64)
+        src = np.concatenate([[0], np.cumsum(rc.ravel())])
+        rows = {}
+        for r in range(R):
+            acc = np.zeros(M + 1, np.int64)
+            n_c = 0
+            for s_ in range(W):
+                for k in range(src[s_ * R + r], src[s_ * R + r + 1]):
+                    l, off = int(d[k] >> np.uint64(40)), int(d[k] & np.uint64((1 << 40) - 1)) + s_ * stride
+                    np.add.at(acc, ar[off:off + l], 1)
+                    n_c += 1
+            a = part + r * W
+            acc[a] -= n_c
+            rows[a] = acc[:M]
+        return rows
+
+
+def _worker(rank, world, port, up_all, it_all, M, out_q, mode="partials"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -87,9 +146,13 @@ def _worker(rank, world, port, up_all, it_all, M, out_q):
     lo, hi = rank * U // world, (rank + 1) * U // world
     up = up_all[lo:hi + 1] - up_all[lo]
     it = it_all[up_all[lo]:up_all[hi]]
-    core = FakeCore(M)
-    res = sharding.count_sharded(core, torch.from_numpy(up), torch.from_numpy(it))
-    out_q.put((rank, {a: v.tolist() for a, v in res.merged.items()}, res.rowsum.numpy().tolist(), res.observed))
+    if mode == "records":
+        res = sharding.count_records(FakeRecordsCore(M), torch.from_numpy(up), torch.from_numpy(it))
+        rows, rs = res.owned, None
+    else:
+        res = sharding.count_sharded(FakeCore(M), torch.from_numpy(up), torch.from_numpy(it))
+        rows, rs = res.merged, res.rowsum.numpy().tolist()
+    out_q.put((rank, {a: v.tolist() for a, v in rows.items()}, rs, res.observed))
     dist.destroy_process_group()
 
 
@@ -101,8 +164,8 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_count_sharded_gloo(oracle, pkg, world):
+@pytest.mark.parametrize("world,mode", [(2, "partials"), (3, "partials"), (2, "records"), (3, "records")])
+def test_count_sharded_gloo(oracle, pkg, world, mode):
     rng = np.random.default_rng(3)
     U, M = 90, 23
     lens = rng.integers(1, 12, U)
@@ -111,7 +174,7 @@ def test_count_sharded_gloo(oracle, pkg, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, up, it, M, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, up, it, M, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]
@@ -125,7 +188,8 @@ def test_count_sharded_gloo(oracle, pkg, world):
     seen = set()
     for rank, rows, rs, obs in outs:
         assert obs == observed
-        assert np.array_equal(np.array(rs), rowsums)
+        if rs is not None:
+            assert np.array_equal(np.array(rs), rowsums)
         for a, v in rows.items():
             assert a % world == rank
             assert np.array_equal(np.array(v), C[a])
