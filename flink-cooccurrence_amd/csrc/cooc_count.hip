@@ -895,36 +895,42 @@ __global__ void k_sources_sum(const int32_t *__restrict__ recv_counts, int32_t W
   rcnt[r] = t;
 }
 
-// Owner side: one wave per owned row concatenates its sources' descriptor segments (source order)
-// into the row-contiguous list, moving each offset into the all-gathered arena (source s at
-// s * stride), and accumulates the contributions' statistics for the chunk plan.
-__global__ __launch_bounds__(256) void k_reorder_sources(const int32_t *__restrict__ recv_counts,
-                                                         const int64_t *__restrict__ seg_off,
-                                                         const uint64_t *__restrict__ recv_desc,
-                                                         const int64_t *__restrict__ row_ptr, int32_t W, int32_t R,
-                                                         int64_t stride, uint64_t *__restrict__ desc,
-                                                         PlanTotals *__restrict__ tot) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+// Owner side: one workgroup per (source, owned row) segment copies it to its place in the row's
+// concatenated list (sources in order), moving each offset into the all-gathered arena (source s at
+// s * stride), and accumulates the contributions' statistics for the chunk plan.  A workgroup per
+// segment keeps the hot rows' segments (up to ~1e5 records each) from serialising on one wave.
+__global__ __launch_bounds__(1024) void k_reorder_sources(const int32_t *__restrict__ recv_counts,
+                                                          const int64_t *__restrict__ seg_off,
+                                                          const uint64_t *__restrict__ recv_desc,
+                                                          const int64_t *__restrict__ row_ptr, int32_t W, int32_t R,
+                                                          int64_t stride, uint64_t *__restrict__ desc,
+                                                          PlanTotals *__restrict__ tot) {
+  __shared__ uint64_t s_red[3][16];
+  __shared__ int64_t s_dst;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t K = int64_t(W) * R;
   uint64_t l_sum = 0, lpl_sum = 0, l_max = 0;
-  for (int64_t r = wave; r < R; r += n_waves) {
-    int64_t dst = row_ptr[r];
-    for (int32_t s = 0; s < W; s++) {
-      const int64_t k = int64_t(s) * R + r;
-      const int32_t c = recv_counts[k];
-      const int64_t src = seg_off[k];
-      const uint64_t shift = uint64_t(s) * uint64_t(stride);
-      for (int32_t i = lane; i < c; i += 64) {
-        const uint64_t d = recv_desc[src + i] + shift;  // offset field: low 40 bits, no carry
-        desc[dst + i] = d;
-        const uint64_t l = d >> 40;
-        l_sum += l;
-        lpl_sum += l * ((l + 7) & ~uint64_t(7));
-        l_max = l > l_max ? l : l_max;
-      }
-      dst += c;
+  for (int64_t k = blockIdx.x; k < K; k += gridDim.x) {
+    const int32_t s = int32_t(k / R), r = int32_t(k % R);
+    const int32_t c = recv_counts[k];
+    if (c == 0) continue;  // uniform over the workgroup
+    if (tid == 0) {
+      int64_t dst = row_ptr[r];
+      for (int32_t q = 0; q < s; q++) dst += recv_counts[int64_t(q) * R + r];
+      s_dst = dst;
     }
+    __syncthreads();
+    const int64_t dst = s_dst, src = seg_off[k];
+    const uint64_t shift = uint64_t(s) * uint64_t(stride);
+    for (int32_t i = tid; i < c; i += 1024) {
+      const uint64_t d = recv_desc[src + i] + shift;  // offset field: low 40 bits, no carry
+      desc[dst + i] = d;
+      const uint64_t l = d >> 40;
+      l_sum += l;
+      lpl_sum += (l + 7) & ~uint64_t(7);  // sum over contributions of pad8(n_u) = sum_u n_u pad8(n_u)
+      l_max = l > l_max ? l : l_max;
+    }
+    __syncthreads();  // s_dst is rewritten for the next segment
   }
   for (int o = 32; o > 0; o >>= 1) {
     l_sum += __shfl_xor(l_sum, o, 64);
@@ -932,10 +938,23 @@ __global__ __launch_bounds__(256) void k_reorder_sources(const int32_t *__restri
     const uint64_t m = __shfl_xor(l_max, o, 64);
     l_max = m > l_max ? m : l_max;
   }
-  if (lane == 0 && l_sum) {
-    atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_l2), (unsigned long long)l_sum);
-    atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_lpl), (unsigned long long)lpl_sum);
-    atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_len), (unsigned long long)l_max);
+  if (lane == 0) {
+    s_red[0][wave] = l_sum;
+    s_red[1][wave] = lpl_sum;
+    s_red[2][wave] = l_max;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 16; w++) {
+      l_sum += s_red[0][w];
+      lpl_sum += s_red[1][w];
+      l_max = s_red[2][w] > l_max ? s_red[2][w] : l_max;
+    }
+    if (l_sum) {
+      atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_l2), (unsigned long long)l_sum);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&tot->sum_lpl), (unsigned long long)lpl_sum);
+      atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_len), (unsigned long long)l_max);
+    }
   }
 }
 
@@ -2083,7 +2102,7 @@ Status Counter::shard_count(int32_t W, int32_t part, const int32_t *recv_counts,
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, own64, row_ptr_.as<int64_t>() + 1, R, s));
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, seg64, seg_off_.as<int64_t>(), int(K), s));
-    k_reorder_sources<<<std::min<unsigned>(blocks_for(int64_t(R) * 64, 256), 8192), 256, 0, s>>>(
+    k_reorder_sources<<<unsigned(std::min<int64_t>(K, 8 * int64_t(n_cu_))), 1024, 0, s>>>(
         recv_counts, seg_off_.as<int64_t>(), recv_desc, row_ptr_.as<int64_t>(), W, R, arena_stride,
         desc_.as<uint64_t>(), tot);
     COOC_HIP_TRY(hipGetLastError());
