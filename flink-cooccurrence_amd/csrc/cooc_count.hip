@@ -992,6 +992,32 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(int64_t n, int32
   }
 }
 
+// One launch instead of a memset per small buffer (each fill is a launch on the critical path).
+__global__ void k_plan_reset(PlanTotals *__restrict__ tot, int64_t *__restrict__ a0, int64_t *__restrict__ b0) {
+  if (threadIdx.x == 0) {
+    *tot = PlanTotals{};
+    *a0 = 0;
+    *b0 = 0;
+  }
+}
+
+__global__ void k_rows_reset(int32_t R, int64_t *__restrict__ rowsum, int32_t *__restrict__ row_nnz,
+                             int64_t *__restrict__ row_base, unsigned long long *__restrict__ bump,
+                             int32_t *__restrict__ ord_cbase, int32_t *__restrict__ split_slot) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < R) {
+    rowsum[i] = 0;
+    row_nnz[i] = 0;
+  }
+  if (i <= R) row_base[i] = 0;
+  if (i == 0) {
+    bump[0] = 0;
+    bump[1] = 0;
+    ord_cbase[0] = 0;
+    split_slot[0] = 0;
+  }
+}
+
 // Chunks of a row: equal shares of its contributions, as many as its estimated pair work needs
 // (contributions x mean padded list length per contribution).  Heaviest rows first (sort by count).
 __global__ void k_batch_plan(const int32_t *__restrict__ rcnt, int32_t M, const PlanTotals *__restrict__ tot,
@@ -1832,9 +1858,7 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
   PlanTotals *tot = tot_.as<PlanTotals>();
   int64_t *plen = plen_.as<int64_t>(), *poff = poff_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
   int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *uidx = uidx_.as<int32_t>();
-  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
-  COOC_HIP_TRY(hipMemsetAsync(poff, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipMemsetAsync(row_ptr, 0, sizeof(int64_t), s));
+  k_plan_reset<<<1, 64, 0, s>>>(tot, poff, row_ptr);
   if (U > 0) {
     k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, plen, tot);
     COOC_HIP_TRY(hipGetLastError());
@@ -1898,10 +1922,9 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
   COOC_TRY(rowsum_.reserve(sizeof(int64_t) * R1));
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
   PlanTotals *tot = tot_.as<PlanTotals>();
-  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * R1, s));
-  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * R1, s));
-  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t) * (R1 + 1), s));
-  COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
+  k_rows_reset<<<blocks_for(int64_t(R1) + 1, 256), 256, 0, s>>>(R1, rowsum_.as<int64_t>(), row_nnz_.as<int32_t>(),
+                                                                row_base_.as<int64_t>(), bump_.as<unsigned long long>(),
+                                                                ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>());
   size_t tmp = 0, q = 0;
   COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint32_t>(),
                                                             order_keys_.as<uint32_t>(), order_.as<int32_t>() + R1,
@@ -1921,8 +1944,6 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
                                                               s));
     k_gather_i32<<<blocks_for(R, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), R, ord_nch_.as<int32_t>());
   }
-  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
-  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
   if (R > 0) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
