@@ -1021,7 +1021,7 @@ __global__ void k_rows_reset(int32_t R, int64_t *__restrict__ rowsum, int32_t *_
 // Chunks of a row: equal shares of its contributions, as many as its estimated pair work needs
 // (contributions x mean padded list length per contribution).  Heaviest rows first (sort by count).
 __global__ void k_batch_plan(const int32_t *__restrict__ rcnt, int32_t M, const PlanTotals *__restrict__ tot,
-                             int64_t n, uint32_t *__restrict__ key, int32_t *__restrict__ order,
+                             int64_t n, int64_t chunk_work, uint32_t *__restrict__ key, int32_t *__restrict__ order,
                              int32_t *__restrict__ row_nch, int32_t *__restrict__ row_split) {
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= M) return;
@@ -1030,7 +1030,7 @@ __global__ void k_batch_plan(const int32_t *__restrict__ rcnt, int32_t M, const 
   int32_t nch = 0;
   if (c > 0) {
     const double w = double(c) * lbar;
-    nch = int32_t(min(double(c), max(1.0, ceil(w / double(kChunkWork)))));
+    nch = int32_t(min(double(c), max(1.0, ceil(w / double(chunk_work)))));
   }
   key[a] = uint32_t(c);
   order[a] = a;
@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
     int64_t bump_cap, int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, uint32_t *__restrict__ staging,
     int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, uint32_t *__restrict__ dense) {
   constexpr uint32_t kWalkers = kAccThreads / S;
-  extern __shared__ uint32_t acc[];                                   // [M + 1]: counters, sink at M
+  extern __shared__ __attribute__((aligned(16))) uint32_t acc[];     // [M + 1]: counters, sink at M
   int64_t *s_seg = reinterpret_cast<int64_t *>(acc + ((M + 2) & ~1));  // [db] arena group - group start
   uint32_t *s_vst = reinterpret_cast<uint32_t *>(s_seg + db);          // [db + 1] group starts
   __shared__ int32_t s_chunk;
@@ -1218,12 +1218,24 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       uint32_t *dst = dense + int64_t(c.row) * M;
       uint64_t sum = 0;
       uint32_t nnz = 0;
-      for (int32_t b = tid; b < M; b += kAccThreads) {
-        const uint32_t v = acc[b];
-        if (!(X & 8)) dst[b] = v;
-        acc[b] = 0;
-        sum += v;
-        nnz += v != 0u;
+      if ((M & 3) == 0) {  // 16-B LDS reads and HBM stores (rows 16-B aligned)
+        uint4 *a4 = reinterpret_cast<uint4 *>(acc);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (int32_t q = tid; q < (M >> 2); q += kAccThreads) {
+          const uint4 v = a4[q];
+          if (!(X & 8)) d4[q] = v;
+          a4[q] = make_uint4(0u, 0u, 0u, 0u);
+          sum += uint64_t(v.x) + v.y + v.z + v.w;
+          nnz += (v.x != 0u) + (v.y != 0u) + (v.z != 0u) + (v.w != 0u);
+        }
+      } else {
+        for (int32_t b = tid; b < M; b += kAccThreads) {
+          const uint32_t v = acc[b];
+          if (!(X & 8)) dst[b] = v;
+          acc[b] = 0;
+          sum += v;
+          nnz += v != 0u;
+        }
       }
       // a row sum fits 40 bits (uint32 counts over < 2^8 columns per thread), nnz < 2^16 per thread
       const uint64_t both = block_sum_u64((sum << 24) | uint64_t(nnz), s_red);
@@ -1446,6 +1458,8 @@ Status Counter::init(int32_t n_items) {
   store_mode_ = sm ? atoi(sm) : 1;
   const char *aw = getenv("COOC_ACC_WGS");
   acc_wgs_ = aw ? atoi(aw) : 1;
+  const char *cw = getenv("COOC_CHUNK_WORK");
+  chunk_work_ = cw ? std::max<int64_t>(4096, atoll(cw)) : kChunkWork;
   const char *bs = getenv("COOC_BATCH_STRIDE");
   bstride_ = bs ? atoi(bs) : 16;
   const char *bu = getenv("COOC_BATCH_UNROLL");
@@ -1936,7 +1950,7 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
   // chunk plan: rows by contribution count, heaviest first
   int32_t *order = order_.as<int32_t>();
   if (R > 0) {
-    k_batch_plan<<<blocks_for(R, 256), 256, 0, s>>>(rcnt, R, tot, n, row_work_.as<uint32_t>(), order + R,
+    k_batch_plan<<<blocks_for(R, 256), 256, 0, s>>>(rcnt, R, tot, n, chunk_work_, row_work_.as<uint32_t>(), order + R,
                                                     row_nch_.as<int32_t>(), row_split_.as<int32_t>());
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint32_t>(),

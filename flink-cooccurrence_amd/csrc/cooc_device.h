@@ -199,6 +199,7 @@ class Counter {
   bool dense_mode_ = false;           // the last run's output is dense_
   DevBuf dense_, send_;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
+  int64_t chunk_work_ = 0;            // COOC_CHUNK_WORK: pairs per chunk of the batch planner (A/B)
   int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
