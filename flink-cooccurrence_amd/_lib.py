@@ -23,6 +23,7 @@ COOC_ERR_OVERFLOW = 5
 COOC_FLAG_EXACT_SCORES = 1
 COOC_FLAG_OUTPUT_CSR = 2
 COOC_FLAG_OUTPUT_DENSE = 4
+COOC_FLAG_GENERAL_PLANNER = 8
 
 i16p = ctypes.POINTER(ctypes.c_int16)
 i32p = ctypes.POINTER(ctypes.c_int32)

@@ -76,13 +76,17 @@ class CooccurrenceCore:
     """One context of the C-ABI (one Flink subtask)."""
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
-                 exact_scores: bool = False, output: str = "auto"):
-        """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2)."""
+                 exact_scores: bool = False, output: str = "auto", planner: str = "auto"):
+        """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
+        planner: "auto" (the batch planner below 40,320 items) or "general" (the sort-based planner)."""
         L = _lib.load()
         flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
         if output not in ("auto", "csr", "dense"):
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown output layout {output!r}")
         flags |= {"auto": 0, "csr": _lib.COOC_FLAG_OUTPUT_CSR, "dense": _lib.COOC_FLAG_OUTPUT_DENSE}[output]
+        if planner not in ("auto", "general"):
+            raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown planner {planner!r}")
+        flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner == "general" else 0
         cfg = CoocConfig(device, n_items, topk, flags, window_size_ms)
         h = ctypes.c_void_p()
         check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
@@ -328,10 +332,11 @@ class NonSampledUserInteractionCounterOneInputStreamOperator:
     ROW_SUM_TAG = "rowSums"         # NonSampled...java:45-46
 
     def __init__(self, window_size: int, window_unit: str = "MILLISECONDS", *, n_items: int, top_k: int = 10,
-                 device: int = -1, exact_scores: bool = False):
+                 device: int = -1, exact_scores: bool = False, planner: str = "auto"):
         if top_k <= 0:  # ItemRowRescorer...java:52-54
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"{top_k} is <= 0")
-        self.core = CooccurrenceCore(n_items, top_k, window_size_ms(window_size, window_unit), device, exact_scores)
+        self.core = CooccurrenceCore(n_items, top_k, window_size_ms(window_size, window_unit), device, exact_scores,
+                                     planner=planner)
 
     def process_element(self, user: int, item: int, timestamp: int) -> bool:
         """Returns True when the record was late and dropped (NonSampled...java:89-91)."""

@@ -18,6 +18,7 @@
 //   8. k_finalize_split   compacts staging rows of split rows
 // HBM model per window: the ordered pairs P stream 4 B partner ids (mostly served by MALL/L2:
 // every user list is re-read once per item in it), 12 B per output entry; see DESIGN.md.
+#include <cstdio>
 #include <hipcub/hipcub.hpp>
 
 #include "cooc_device.h"
@@ -293,6 +294,28 @@ __device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t *s_red) {
   return t;
 }
 
+// Two sums with the barriers of one (s_red: 2 kAccWaves).
+__device__ inline uint64_t block_sum2_u64(uint64_t v, uint64_t u, uint64_t *s_red, uint64_t *u_sum) {
+  for (int o = 32; o > 0; o >>= 1) {
+    v += __shfl_xor(v, o, 64);
+    u += __shfl_xor(u, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_red[wave] = v;
+    s_red[kAccWaves + wave] = u;
+  }
+  __syncthreads();
+  uint64_t t = 0, w2 = 0;
+  for (int w = 0; w < kAccWaves; w++) {
+    t += s_red[w];
+    w2 += s_red[kAccWaves + w];
+  }
+  __syncthreads();
+  *u_sum = w2;
+  return t;
+}
+
 // Two-pass compaction: every wave owns a contiguous column range; pass 1 counts its nonzeros,
 // one block scan gives each wave its output offset, pass 2 writes (col, cnt) in column order.
 // Two barriers per row instead of two per 1024-column tile.
@@ -303,6 +326,10 @@ struct Place {
   int64_t fixed_base;        // used when bump == nullptr
   unsigned long long *bump;  // device cursor of the bump region, or nullptr
   int64_t bump_cap;          // entries in the bump region
+  int64_t *slab = nullptr;   // compact_row_ranges4: the workgroup's slab [cur, end) in LDS (one
+                             // global atomic per slab instead of one per row), or nullptr
+  int64_t slab_size = 0;     // entries taken per slab (>= the row's nnz)
+  unsigned long long *err = nullptr;  // bit 2 set when the region is exhausted
 };
 
 // kStore: 0 = no stores (experiments), 1 = plain stores, 2 = sc1 stores (written through, the lines
@@ -362,6 +389,111 @@ __device__ inline uint32_t compact_row_ranges(Src *row, int32_t M, int32_t col_o
       my_sum += v;
     }
     off += uint32_t(__popcll(m));
+  }
+  __syncthreads();
+  *sum = my_sum;
+  return tot;
+}
+
+// compact_row_ranges over a 16-B aligned uint32 LDS row with 16-B LDS reads: every lane holds 4
+// consecutive columns, waves own 256-column-aligned ranges, a lane's output slot is the popcount
+// prefix of three ballots (its nonzero count in 0..4, bit by bit).  A quarter of the LDS
+// instructions and loop trips of the scalar version.  Columns >= M are never read as counters.
+template <int kStore = 1>
+__device__ inline uint32_t compact_row_ranges4(uint32_t *row, int32_t M, int32_t *__restrict__ col_out,
+                                               uint32_t *__restrict__ cnt_out, Place place, int64_t *base_used,
+                                               uint64_t *sum, uint32_t *s_wave, int64_t *s_base) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t per = ((M + kAccWaves - 1) / kAccWaves + 255) & ~255;
+  const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
+  const uint4 *row4 = reinterpret_cast<const uint4 *>(row);
+  auto load = [&](int32_t b, uint32_t v[4]) {
+    if (b < hi) {
+      const uint4 q = row4[b >> 2];
+      v[0] = q.x;
+      v[1] = b + 1 < hi ? q.y : 0u;
+      v[2] = b + 2 < hi ? q.z : 0u;
+      v[3] = b + 3 < hi ? q.w : 0u;
+    } else {
+      v[0] = v[1] = v[2] = v[3] = 0u;
+    }
+  };
+  uint32_t cnt = 0;
+  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
+    uint32_t v[4];
+    load(b0 + 4 * lane, v);
+    cnt += (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) s_wave[wave] = cnt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kAccWaves; w++) {
+    const uint32_t x = s_wave[w];
+    off += (w < wave) ? x : 0u;
+    tot += x;
+  }
+  if (place.bump) {
+    if (tid == 0) {
+      int64_t b = 0;
+      if (place.slab && tot) {
+        if (place.slab[0] + int64_t(tot) > place.slab[1]) {  // the rest of the slab is abandoned
+          const int64_t take = max(int64_t(tot), place.slab_size);
+          place.slab[0] = int64_t(atomicAdd(place.bump, (unsigned long long)take));
+          place.slab[1] = place.slab[0] + take;
+        }
+        b = place.slab[0];
+        place.slab[0] += tot;
+      } else if (tot) {
+        b = int64_t(atomicAdd(place.bump, (unsigned long long)tot));
+      }
+      if (b + int64_t(tot) > place.bump_cap) {  // region exhausted: write nothing, the host reports OOM
+        b = -1;
+        if (place.err) atomicOr(place.err, 4ull);
+      }
+      *s_base = b;
+    }
+    __syncthreads();
+  }
+  const int64_t out_base = place.bump ? *s_base : place.fixed_base;
+  *base_used = out_base;
+  const bool write = out_base >= 0;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint64_t my_sum = 0;
+  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
+    const int32_t b = b0 + 4 * lane;
+    uint32_t v[4];
+    load(b, v);
+    const uint32_t c = (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+    const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
+    const uint32_t pre = uint32_t(__popcll(m0 & lt_mask)) + 2u * uint32_t(__popcll(m1 & lt_mask)) +
+                         4u * uint32_t(__popcll(m2 & lt_mask));
+    if (c) {
+      int64_t pos = out_base + off + pre;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (!v[k]) continue;
+        if (kStore && write) {
+          if (kStore == 3) {
+            __builtin_nontemporal_store(b + k, col_out + pos);
+            __builtin_nontemporal_store(v[k], cnt_out + pos);
+          } else {
+            col_out[pos] = b + k;
+            cnt_out[pos] = v[k];
+          }
+        }
+        pos++;
+        my_sum += v[k];
+      }
+      // zero the 4 counters (those >= hi belong to the next wave's range or lie past M: untouched)
+      if (b + 3 < hi) {
+        reinterpret_cast<uint4 *>(row)[b >> 2] = make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        for (int k = 0; k < 4 && b + k < hi; k++) row[b + k] = 0u;
+      }
+    }
+    off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2));
   }
   __syncthreads();
   *sum = my_sum;
@@ -695,9 +827,19 @@ __global__ void k_iota_users(int64_t n, const int64_t *__restrict__ user_ptr, in
 constexpr int kPlanThreads = 1024;
 constexpr int kPlanUnroll = 4;       // interactions per thread per step of hist / scatter
 constexpr int32_t kFillThread = 2048;  // longer lists get a workgroup each in k_batch_fill_long
+// Descriptor of a contribution: arena offset (bits 0-39), segment length (bits 40-62), bit 63 set
+// for an old position of a streaming window (its segment is the new part; no -1 self term).
 constexpr uint64_t kOffMask = (uint64_t(1) << 40) - 1;
+constexpr uint64_t kOldPos = uint64_t(1) << 63;
+constexpr uint32_t kLenMask = (1u << 23) - 1;
 
+// Per user: padded arena footprint and the contributions' statistics.  old == nullptr: one window
+// over empty histories (every position contributes the whole list).  Streaming windows (old[j] =
+// resident history length before the window): a user's arena holds the whole list, then (old > 0)
+// its new part [old, l) as a second padded segment; new positions contribute the whole list and
+// old positions the new part.
 __global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *__restrict__ up,
+                                                     const int32_t *__restrict__ old,
                                                      int64_t *__restrict__ plen, PlanTotals *__restrict__ tot) {
   __shared__ uint64_t s2[4], spl[4];
   __shared__ int64_t smax[4];
@@ -707,9 +849,11 @@ __global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *_
   if (j < U) {
     const int64_t l = up[j + 1] - up[j];
     const int64_t pl = (l + 7) & ~int64_t(7);
-    plen[j] = pl;
-    l2 = uint64_t(l) * uint64_t(l);
-    lpl = uint64_t(l) * uint64_t(pl);
+    const int64_t o = old ? int64_t(old[j]) : 0;
+    const int64_t pn = o > 0 ? ((l - o + 7) & ~int64_t(7)) : 0;  // padded new part (its own segment)
+    plen[j] = pl + pn;
+    l2 = uint64_t(l - o) * uint64_t(l) + uint64_t(o) * uint64_t(l - o);
+    lpl = uint64_t(l - o) * uint64_t(pl) + uint64_t(o) * uint64_t(pn);
     mx = l;
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -739,13 +883,18 @@ __global__ __launch_bounds__(256) void k_batch_users(int64_t U, const int64_t *_
 // One thread per user: uidx[up[j] .. up[j+1]) = j (16-B stores where aligned) and the arena pads
 // [n_j, pad8(n_j)).  Lists longer than kFillThread are queued for k_batch_fill_long.
 __global__ __launch_bounds__(256) void k_batch_fill(int64_t U, const int64_t *__restrict__ up,
+                                                    const int32_t *__restrict__ old,
                                                     const int64_t *__restrict__ poff, int32_t M,
                                                     int32_t *__restrict__ uidx, uint16_t *__restrict__ arena,
                                                     int32_t *__restrict__ long_list, PlanTotals *__restrict__ tot) {
   const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (j >= U) return;
   const int64_t s = up[j], l = up[j + 1] - s, o = poff[j];
-  for (int64_t i = l; i < ((l + 7) & ~int64_t(7)); i++) arena[o + i] = uint16_t(M);
+  const int64_t pl = (l + 7) & ~int64_t(7);
+  for (int64_t i = l; i < pl; i++) arena[o + i] = uint16_t(M);
+  const int64_t h = old ? int64_t(old[j]) : 0;
+  if (h > 0)
+    for (int64_t i = l - h; i < ((l - h + 7) & ~int64_t(7)); i++) arena[o + pl + i] = uint16_t(M);
   if (l > kFillThread) {
     long_list[atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_long), 1ull)] = int32_t(j);
     return;
@@ -770,6 +919,19 @@ __global__ __launch_bounds__(256) void k_batch_fill_long(const int64_t *__restri
   }
 }
 
+// Streaming windows: the active users' histories (resident int32 arena, user j at hoff[j]) as
+// one CSR over the contribution slots.
+__global__ __launch_bounds__(256) void k_window_items(int64_t n, const int64_t *__restrict__ up,
+                                                      const int32_t *__restrict__ uidx,
+                                                      const int64_t *__restrict__ hoff,
+                                                      const int32_t *__restrict__ harena,
+                                                      int32_t *__restrict__ items) {
+  const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t j = uidx[p];
+  items[p] = harena[hoff[j] + (p - up[j])];
+}
+
 // Interaction range of partition block b (the same in hist and scatter).
 __device__ inline void block_range(int64_t n, int32_t B, int32_t b, int64_t *p0, int64_t *p1) {
   *p0 = n * b / B;
@@ -780,6 +942,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_hist(int64_t n, int32_t 
                                                              const int32_t *__restrict__ items,
                                                              const int32_t *__restrict__ uidx,
                                                              const int64_t *__restrict__ poff, int32_t M,
+                                                             const int32_t *__restrict__ old,
                                                              uint16_t *__restrict__ arena, int32_t *__restrict__ bh,
                                                              PlanTotals *__restrict__ tot) {
   extern __shared__ uint32_t hist[];  // [M]
@@ -797,11 +960,20 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_hist(int64_t n, int32_t 
       it[k] = p < p1 ? items[p] : -1;
       j[k] = p < p1 ? uidx[p] : -1;
     }
-    int64_t dst[kPlanUnroll];
+    int64_t dst[kPlanUnroll], dst2[kPlanUnroll];
 #pragma unroll
     for (int k = 0; k < kPlanUnroll; k++) {
       const int64_t p = pb + k * kPlanThreads + tid;
-      dst[k] = j[k] >= 0 ? poff[j[k]] + (p - up[j[k]]) : -1;
+      dst[k] = -1;
+      dst2[k] = -1;
+      if (j[k] >= 0) {
+        const int64_t s0 = up[j[k]], i = p - s0;
+        dst[k] = poff[j[k]] + i;
+        if (old) {  // a new position is also the (i - h)-th id of the user's new-part segment
+          const int64_t h = old[j[k]];
+          if (h > 0 && i >= h) dst2[k] = dst[k] - i + ((up[j[k] + 1] - s0 + 7) & ~int64_t(7)) + (i - h);
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < kPlanUnroll; k++) {
@@ -814,6 +986,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_hist(int64_t n, int32_t 
         bad = true;
       }
       arena[dst[k]] = v;
+      if (dst2[k] >= 0) arena[dst2[k]] = v;
     }
   }
   if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
@@ -925,7 +1098,7 @@ __global__ __launch_bounds__(1024) void k_reorder_sources(const int32_t *__restr
     for (int32_t i = tid; i < c; i += 1024) {
       const uint64_t d = recv_desc[src + i] + shift;  // offset field: low 40 bits, no carry
       desc[dst + i] = d;
-      const uint64_t l = d >> 40;
+      const uint64_t l = (d >> 40) & kLenMask;
       l_sum += l;
       lpl_sum += (l + 7) & ~uint64_t(7);  // sum over contributions of pad8(n_u) = sum_u n_u pad8(n_u)
       l_max = l > l_max ? l : l_max;
@@ -964,6 +1137,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(int64_t n, int32
                                                                 const int64_t *__restrict__ poff,
                                                                 const int64_t *__restrict__ row_ptr, int32_t M,
                                                                 int32_t W, const int32_t *__restrict__ bh,
+                                                                const int32_t *__restrict__ old,
                                                                 uint64_t *__restrict__ desc) {
   extern __shared__ uint32_t next_pos[];  // [M] next free position of each row inside this block's share
   const int tid = threadIdx.x, b = blockIdx.x;
@@ -984,8 +1158,16 @@ __global__ __launch_bounds__(kPlanThreads) void k_batch_scatter(int64_t n, int32
     }
     uint64_t d[kPlanUnroll];
 #pragma unroll
-    for (int k = 0; k < kPlanUnroll; k++)
-      d[k] = j[k] >= 0 ? (uint64_t(up[j[k] + 1] - up[j[k]]) << 40) | uint64_t(poff[j[k]]) : 0;
+    for (int k = 0; k < kPlanUnroll; k++) {
+      d[k] = 0;
+      if (j[k] < 0) continue;
+      const int64_t s0 = up[j[k]], l = up[j[k] + 1] - s0;
+      const int64_t h = old ? int64_t(old[j[k]]) : 0;
+      if (pb + k * kPlanThreads + tid - s0 < h)  // old position: the new part, no self term
+        d[k] = kOldPos | (uint64_t(l - h) << 40) | uint64_t(poff[j[k]] + ((l + 7) & ~int64_t(7)));
+      else
+        d[k] = (uint64_t(l) << 40) | uint64_t(poff[j[k]]);
+    }
 #pragma unroll
     for (int k = 0; k < kPlanUnroll; k++)
       if (uint32_t(it[k]) < uint32_t(M)) desc[atomicAdd(&next_pos[it[k]], 1u)] = d[k];
@@ -1062,6 +1244,9 @@ __device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
   return v;
 }
 
+// Sparse output of k_acc_batch: a workgroup takes kSlabRows * M entries of the bump region at a time.
+constexpr int kSlabRows = 4;
+
 // ★ batch accumulate.  Per chunk (row a, contribution range): up to `db` descriptors per batch;
 // their group counts (8 ids per 16-B group) are block-scanned into LDS segment starts; walkers of S
 // lanes own equal contiguous group ranges (start segment from a table written by the scan) and
@@ -1089,30 +1274,44 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
   __shared__ int32_t s_chunk;
   __shared__ uint32_t s_wtot[kAccWaves];
   __shared__ uint32_t s_wave[kAccWaves];
-  __shared__ uint64_t s_red[kAccWaves];
+  __shared__ uint64_t s_red[2 * kAccWaves];
   __shared__ int64_t s_base;
+  __shared__ int64_t s_slab[2];
   __shared__ int32_t s_qstart[kWalkers];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_chunks = tot->n_chunks;
   const uint4 *A = reinterpret_cast<const uint4 *>(arena);
   const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
   for (int32_t b = tid; b <= M; b += kAccThreads) acc[b] = 0;
-  if (tid == 0) s_chunk = atomicAdd(queue, 1);
+  if (tid == 0) {
+    s_chunk = atomicAdd(queue, 1);
+    s_slab[0] = s_slab[1] = 0;
+  }
   __syncthreads();
   int32_t ch = s_chunk;
   Chunk c = ch < n_chunks ? chunks[ch] : Chunk{0, -1, 0, 0, 0};
   uint64_t d = (tid < db && c.begin + tid < c.end) ? desc[c.begin + tid] : 0;
+  uint64_t ph[5] = {0, 0, 0, 0, 0};  // X & 64: phase times (wall clock, thread 0)
+  uint64_t t_last = (X & 64) ? wall_clock64() : 0;
+  auto stamp = [&](int k) {
+    if (X & 64) {
+      const uint64_t t = wall_clock64();
+      ph[k] += t - t_last;
+      t_last = t;
+    }
+  };
   while (ch < n_chunks) {
     int32_t nxt = 0;
     if (tid == 0) nxt = atomicAdd(queue, 1);  // lands while this chunk is walked
-    uint64_t my_len = 0;
+    uint64_t my_len = 0, my_self = 0;
     for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
       const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
       uint32_t ng = 0;
       int64_t gsrc = 0;
       if (tid < nb) {
-        const uint32_t l = uint32_t(d >> 40);
+        const uint32_t l = uint32_t(d >> 40) & kLenMask;
         my_len += l;
+        my_self += (d & kOldPos) ? 0u : 1u;
         ng = (l + 7) >> 3;
         gsrc = int64_t(d & kOffMask) >> 3;
       }
@@ -1197,11 +1396,13 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       }
       __syncthreads();
     }
+    stamp(0);
     if (tid == 0) s_chunk = nxt;
-    // every contribution is a new position of the row's item: the -1 self term at its column.  Rows
-    // are local (output) indices; the row's item is part + row * W (W parts of the sharded path).
-    const int64_t n_c = c.end - c.begin;
-    const uint64_t len_sum = block_sum_u64(my_len, s_red);  // (its barriers publish s_chunk)
+    // every contribution at a new position of the row's item has the -1 self term at its column.
+    // Rows are local (output) indices; the row's item is part + row * W (W parts of the sharded path).
+    uint64_t self_sum;
+    const uint64_t len_sum = block_sum2_u64(my_len, my_self, s_red, &self_sum);  // (publishes s_chunk)
+    const int64_t n_c = int64_t(self_sum);
     const int64_t chunk_rowsum = int64_t(len_sum) - n_c;
     const int32_t ch2 = s_chunk;
     const Chunk c2 = ch2 < n_chunks ? chunks[ch2] : Chunk{0, -1, 0, 0, 0};
@@ -1214,6 +1415,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
     }
     __syncthreads();
+    stamp(1);
     if (DENSE && c.split < 0) {
       uint32_t *dst = dense + int64_t(c.row) * M;
       uint64_t sum = 0;
@@ -1253,11 +1455,13 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
           acc[b] = 0;
         }
       }
+    } else if (X & 16) {  // timing experiment: no compaction (counters left in LDS)
     } else if (c.split < 0) {
       uint64_t sum;
       int64_t used;
-      const uint32_t nnz = compact_row_ranges<uint32_t, (X & 8) ? 0 : ST>(
-          acc, M, 0, col_out, cnt_out, Place{0, bump, bump_cap}, &used, &sum, s_wave, &s_base);
+      const Place pl{0, bump, bump_cap, s_slab, int64_t(kSlabRows) * M, reinterpret_cast<unsigned long long *>(&tot->err)};
+      const uint32_t nnz = compact_row_ranges4<(X & 8) ? 0 : ST>(acc, M, col_out, cnt_out, pl, &used, &sum, s_wave,
+                                                                  &s_base);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
         row_base[c.row] = used;
@@ -1275,11 +1479,17 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         }
       }
     }
+    stamp(2);
     __syncthreads();
+    stamp(3);
+    ph[4]++;
     ch = ch2;
     c = c2;
     d = d2;
   }
+  if ((X & 64) && tid == 0)
+    for (int k = 0; k < 5; k++)  // after the split rows' sums (the host reserves 8 more)
+      atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + tot->n_split + 1 + k), (unsigned long long)ph[k]);
 }
 
 // Dense output: rows of items without interactions (no chunk) are zero; one wave per row.
@@ -1849,8 +2059,12 @@ Status Counter::pack(hipStream_t s, int64_t **row_ptr, int32_t **col, uint32_t *
 // ---- batch path, phase 1: local plan (arena, row counts, descriptors in owner-major row order) ----
 // W > 1 (sharded records): rows are laid out owner by owner (owner(a) = a mod W, perm_rows), so the
 // descriptors bound for one owner are contiguous.  W == 1: natural row order.
+// Streaming windows (old != nullptr): up = the active users' contribution prefix (history lengths
+// after the window), old = their lengths before it, items = the resident int32 history arena with
+// user j at hoff[j].
 Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
-                           uint64_t *desc, uint16_t *arena, int64_t arena_cap) {
+                           uint64_t *desc, uint16_t *arena, int64_t arena_cap, const int32_t *old,
+                           const int64_t *hoff) {
   const int32_t M = M_;
   if (!batch_ok()) return Status{1, "the batch path needs n_items < " + std::to_string(kBatchMaxItems)};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
@@ -1859,7 +2073,9 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
   // partition blocks of the hist / scatter passes: one per CU, fewer for tiny inputs
   const int32_t B = int32_t(std::max<int64_t>(1, std::min<int64_t>(n_cu_, n / 4096 + 1)));
   const int64_t U1 = std::max<int64_t>(U, 1);
-  if (arena_cap < n + 7 * U1 + 16) return Status{1, "arena buffer smaller than n + 7 n_users + 16 ids"};
+  if (arena_cap < (old ? 2 * n + 14 * U1 + 16 : n + 7 * U1 + 16))
+    return Status{1, "arena buffer smaller than n + 7 n_users + 16 ids"};
+  if ((old == nullptr) != (hoff == nullptr)) return Status{1, "old and hoff go together"};
   COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
   COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
   COOC_TRY(plen_.reserve(sizeof(int64_t) * U1));
@@ -1874,7 +2090,7 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
   int32_t *bh = bh_.as<int32_t>(), *rcnt = rcnt_.as<int32_t>(), *uidx = uidx_.as<int32_t>();
   k_plan_reset<<<1, 64, 0, s>>>(tot, poff, row_ptr);
   if (U > 0) {
-    k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, plen, tot);
+    k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, old, plen, tot);
     COOC_HIP_TRY(hipGetLastError());
   }
   // row counts in owner-major order -> row_ptr (prefix); the identity order when W == 1
@@ -1895,9 +2111,14 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
   // at the end (never referenced by a segment, keeps the last 16-B load in bounds)
   const size_t lds_m = sizeof(uint32_t) * size_t(M);
   if (U > 0) {
-    k_batch_fill<<<blocks_for(U, 256), 256, 0, s>>>(U, up, poff, M, uidx, arena, long_.as<int32_t>(), tot);
+    k_batch_fill<<<blocks_for(U, 256), 256, 0, s>>>(U, up, old, poff, M, uidx, arena, long_.as<int32_t>(), tot);
     k_batch_fill_long<<<256, 256, 0, s>>>(up, long_.as<int32_t>(), tot, uidx);
-    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, M, arena, bh, tot);
+    if (hoff) {  // the window's histories as one CSR
+      COOC_TRY(witems_.reserve(sizeof(int32_t) * (n + 1)));
+      if (n > 0) k_window_items<<<blocks_for(n, 256), 256, 0, s>>>(n, up, uidx, hoff, items, witems_.as<int32_t>());
+      items = witems_.as<int32_t>();
+    }
+    k_batch_hist<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, M, old, arena, bh, tot);
     k_batch_colscan<<<blocks_for(M, 256), 256, 0, s>>>(B, M, bh, rcnt);
   } else {
     COOC_HIP_TRY(hipMemsetAsync(rcnt, 0, sizeof(int32_t) * M, s));
@@ -1908,7 +2129,7 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt_perm, row_ptr + 1, M, s));
   }
   if (U > 0) {
-    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, W, bh, desc);
+    k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, W, bh, old, desc);
     COOC_HIP_TRY(hipGetLastError());
   }
   return Status::Ok();
@@ -1917,9 +2138,11 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
 // ---- batch path, phase 2: accumulate R rows (row r = global item part + r * W) whose contributions
 // are desc[row_ptr[r] .. row_ptr[r + 1]); tot already holds the contributions' statistics
 // (sum_l2 = sum of list lengths, sum_lpl, max_len, err).  Synchronises `s` once.
+// n = contributions, n_self = those at a new position (each carries the -1 self term); sparse_only
+// forces the padded CSR output (streaming windows: the delta rows are merged from it).
 Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_t *row_ptr, const int32_t *rcnt,
-                                const uint64_t *desc, const uint16_t *arena, int64_t n, hipStream_t s,
-                                CountResult *out, KernelTimer *timer) {
+                                const uint64_t *desc, const uint16_t *arena, int64_t n, int64_t n_self,
+                                bool sparse_only, hipStream_t s, CountResult *out, KernelTimer *timer) {
   const int32_t M = M_;
   const int32_t R1 = std::max<int32_t>(R, 1);
   COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * R1));
@@ -1973,17 +2196,17 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
-  if (h_tot_->max_len >= (int64_t(1) << 24)) return Status{1, "a user history longer than 2^24 items"};
+  if (h_tot_->max_len > int64_t(kLenMask)) return Status{1, "a user history longer than 2^23 - 1 items"};
   const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
   const int64_t work_total = h_tot_->sum_l2;
-  const int64_t pairs = work_total - n;
+  const int64_t pairs = work_total - n_self;
   // Output layout.  Dense uint32 [R x M] when the pairs cover the matrix (P >= R M / 2: dense is then
   // no larger than the sparse (col, cnt) entries it replaces, and written with plain coalesced row
   // stores) and it fits in 40% of free HBM; else the sparse bump-allocated padded CSR, whose entries
   // are at most min(R M, P).
   const int64_t RM = int64_t(R) * M;
-  bool dense = output_pref_ == 2;
-  if (output_pref_ == 0 && 2 * pairs >= RM) {
+  bool dense = !sparse_only && output_pref_ == 2;
+  if (!sparse_only && output_pref_ == 0 && 2 * pairs >= RM) {
     size_t free_b = 0, total_b = 0;
     COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     dense = size_t(RM) * sizeof(uint32_t) <= free_b / 10 * 4 + dense_.cap;
@@ -1994,15 +2217,18 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
   if (dense) {
     COOC_TRY(dense_.reserve(sizeof(uint32_t) * size_t(std::max<int64_t>(RM, 1))));
   } else {
-    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(RM, pairs));
+    // rows are placed in per-workgroup slabs of kSlabRows * M entries; a slab switch abandons less
+    // than one row (< M entries, a quarter of a slab) and every workgroup ends inside one slab
+    const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(RM, pairs));
+    bump_cap_ = bound + bound / 3 + int64_t(n_cu_) * std::max<int64_t>(1, acc_wgs_) * (kSlabRows + 1) * int64_t(M);
     COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
     COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
   }
   if (dense && n_chunks == 0 && RM > 0) COOC_HIP_TRY(hipMemsetAsync(dense_.p, 0, sizeof(uint32_t) * size_t(RM), s));
   if (n_chunks > 0) {
     COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
-    COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
-    COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
+    COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 9)));
+    COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 9), s));
     if (dense) {
       // rows without contributions stay all-zero; rows of several chunks are zeroed, then added into
       k_zero_empty_rows<<<std::min<unsigned>(blocks_for(R, 4), 4096), 256, 0, s>>>(rcnt, R, M, dense_.as<uint32_t>());
@@ -2029,6 +2255,7 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
                                : bstride_ == 16 ? k_acc_batch<4, 16, true> : bunroll_ == 2 ? k_acc_batch<2, 8, true>
                                                                                          : k_acc_batch<4, 8, true>)
               : xmode_ == 4 ? k_acc_batch<4, 8, false, 4> : xmode_ == 8 ? k_acc_batch<4, 8, false, 8>
+              : xmode_ == 20 ? k_acc_batch<4, 8, false, 20> : xmode_ == 64 ? k_acc_batch<4, 8, false, 64>
               : store_mode_ == 3 ? k_acc_batch<4, 8, false, 0, 3> : k_acc_batch<4, 8, false>;
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), desc, arena, M, db,
@@ -2039,6 +2266,14 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
                                                   dense_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+    if (xmode_ == 64) {  // phase times of k_acc_batch (experiments)
+      int64_t ph[5];
+      COOC_HIP_TRY(hipMemcpyAsync(ph, split_sum_.as<int64_t>() + n_split + 1, sizeof(ph), hipMemcpyDeviceToHost, s));
+      COOC_HIP_TRY(hipStreamSynchronize(s));
+      fprintf(stderr, "[k_acc_batch phases] chunks %lld grid %lld  walk %.1f  sum+fetch %.1f  out %.1f  barrier %.1f us per WG\n",
+              (long long)ph[4], (long long)grid, ph[0] / 100.0 / grid, ph[1] / 100.0 / grid, ph[2] / 100.0 / grid,
+              ph[3] / 100.0 / grid);
+    }
     if (dense && n_split > 0) {
       k_dense_split_check<<<unsigned(std::min<int64_t>(n_split, 4 * int64_t(n_cu_))), kAccThreads, 0, s>>>(
           split_row_.as<int32_t>(), tot, M, dense_.as<uint32_t>(), split_sum_.as<int64_t>(), row_nnz_.as<int32_t>());
@@ -2078,7 +2313,21 @@ Status Counter::run_batch(int64_t U, const int64_t *up, const int32_t *items, in
   COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
   COOC_TRY(plan_local(U, up, items, n, 1, s, desc_.as<uint64_t>(), tarena_.as<uint16_t>(), arena_cap));
   return accumulate_rows(M_, 1, 0, row_ptr_.as<int64_t>(), rcnt_.as<int32_t>(), desc_.as<uint64_t>(),
-                         tarena_.as<uint16_t>(), n, s, out, timer);
+                         tarena_.as<uint16_t>(), n, n, false, s, out, timer);
+}
+
+// ---- streaming window through the batch planner: the active users' whole histories and new parts
+// in a padded u16 arena, one descriptor per history position (new positions: the whole list with
+// the self term; old positions: the new part), then the same chunk plan and k_acc_batch.
+Status Counter::run_window(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
+  const int64_t U = au.n_active, n = au.n_contrib, U1 = std::max<int64_t>(U, 1);
+  const int64_t arena_cap = 2 * n + 14 * U1 + 16;
+  COOC_TRY(desc_.reserve(sizeof(uint64_t) * (n + 1)));
+  COOC_TRY(tarena_.reserve(sizeof(uint16_t) * arena_cap));
+  COOC_TRY(plan_local(U, au.cbase, au.arena, n, 1, s, desc_.as<uint64_t>(), tarena_.as<uint16_t>(), arena_cap,
+                      au.old, au.off));
+  return accumulate_rows(M_, 1, 0, row_ptr_.as<int64_t>(), rcnt_.as<int32_t>(), desc_.as<uint64_t>(),
+                         tarena_.as<uint16_t>(), n, au.n_new, true, s, out, timer);
 }
 
 // ---- sharded records (W parts): local plan of this part's users -------------------------------
@@ -2143,7 +2392,7 @@ Status Counter::shard_count(int32_t W, int32_t part, const int32_t *recv_counts,
     COOC_HIP_TRY(hipGetLastError());
   }
   return accumulate_rows(R, W, part, row_ptr_.as<int64_t>(), rcnt_.as<int32_t>(), desc_.as<uint64_t>(), arena_all,
-                         n_recv, s, out, timer);
+                         n_recv, n_recv, false, s, out, timer);
 }
 
 

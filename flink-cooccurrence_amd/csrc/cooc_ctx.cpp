@@ -34,6 +34,8 @@ Status cooc_ctx::init(const cooc_config &c) {
   COOC_HIP_TRY(hipEventCreate(&timer.acc_end));
   COOC_TRY(counter.init(c.n_items));
   counter.set_output_layout((c.flags & COOC_FLAG_OUTPUT_DENSE) ? 2 : (c.flags & COOC_FLAG_OUTPUT_CSR) ? 1 : 0);
+  const char *env = getenv("COOC_BATCH");  // COOC_BATCH=0: the general planner for every context (A/B)
+  counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0 || (env && env[0] == '0'));
   return Status::Ok();
 }
 
@@ -56,8 +58,7 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   have_batch = false;
   batch_topk = 0;
   cooc::CountResult r;
-  static const bool legacy = getenv("COOC_BATCH") && getenv("COOC_BATCH")[0] == '0';  // A/B: the general planner
-  if (counter.batch_ok() && !legacy) {
+  if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
   } else {
     COOC_TRY(count_general(n_users, d_user_ptr, d_items, n_interactions, s, &r));
@@ -98,6 +99,7 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
   }
   static const bool x_mode = getenv("COOC_ACC_X") && atoi(getenv("COOC_ACC_X")) != 0;  // experiments: counts invalid
   if ((err & 2) && !x_mode) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  if (err & 4) return Status{COOC_ERR_OOM, "the sparse output region is exhausted"};
   out->n_items = cfg.n_items;
   out->nnz = nnz;
   out->observed = r.observed;

@@ -128,7 +128,12 @@ class Counter {
   // CSR as run().  Synchronises `stream` once (to size chunks and the output region).
   Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                    CountResult *out, KernelTimer *timer = nullptr);
-  bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems; }
+  bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems && !general_only_; }
+  // A streaming window (resident histories) through the batch planner and k_acc_batch; needs
+  // batch_ok().  Same padded CSR result as run().  Synchronises `stream` once.
+  Status run_window(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
+  // COOC_FLAG_GENERAL_PLANNER: every window through run() (the sort-based general planner).
+  void set_general_only(bool g) { general_only_ = g; }
 
   // Sharded records (W parts, owner(a) = a mod W).  shard_plan: this part's users -> its padded
   // u16 arena (arena[arena_cap >= n + 7 U + 16]), descriptors grouped by owner (desc[n]) and row
@@ -165,10 +170,11 @@ class Counter {
  private:
   Status run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
   Status plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
-                    uint64_t *desc, uint16_t *arena, int64_t arena_cap);
+                    uint64_t *desc, uint16_t *arena, int64_t arena_cap, const int32_t *old = nullptr,
+                    const int64_t *hoff = nullptr);
   Status accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_t *row_ptr, const int32_t *rcnt,
-                         const uint64_t *desc, const uint16_t *arena, int64_t n, hipStream_t s, CountResult *out,
-                         KernelTimer *timer);
+                         const uint64_t *desc, const uint16_t *arena, int64_t n, int64_t n_self, bool sparse_only,
+                         hipStream_t s, CountResult *out, KernelTimer *timer);
 
   int32_t M_ = 0;
   int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)
@@ -197,10 +203,11 @@ class Counter {
   int store_mode_ = 1;                // COOC_ACC_STORE: output stores 1 plain, 2 sc1, 3 nt (A/B)
   int output_pref_ = 0;               // set_output_layout
   bool dense_mode_ = false;           // the last run's output is dense_
-  DevBuf dense_, send_;
+  DevBuf dense_, send_, witems_;
+  bool general_only_ = false;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
   int64_t chunk_work_ = 0;            // COOC_CHUNK_WORK: pairs per chunk of the batch planner (A/B)
-  int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU     // COOC_BATCH_STRIDE / COOC_BATCH_UNROLL: k_acc_batch walker shape
+  int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

@@ -228,7 +228,10 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   au.arena_span = arena_used_;
   CountResult r;
   tr.mark("upload_append", s);
-  COOC_TRY(ctx.counter.run(au, s, &r));
+  if (ctx.counter.batch_ok())  // n_items < 40,320: the batch planner + k_acc_batch
+    COOC_TRY(ctx.counter.run_window(au, s, &r));
+  else
+    COOC_TRY(ctx.counter.run(au, s, &r));
   tr.mark("count", s);
 
   // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
@@ -254,6 +257,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   PlanTotals t;
   COOC_TRY(ctx.counter.read_totals(&t));
   if (t.err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  if (t.err & 4) return Status{COOC_ERR_OOM, "the sparse output region is exhausted"};
 
   n_touched_ = int32_t(h_scal[0]);
   observed_exact += observed_window;

@@ -39,14 +39,19 @@ __global__ void k_append(int64_t n, const int64_t *__restrict__ new_ptr, const i
   }
 }
 
-// One wave per row with a non-empty delta.
-__global__ void k_merge_global(int32_t M, const int64_t *__restrict__ row_base, const int32_t *__restrict__ row_nnz,
-                               const int32_t *__restrict__ col, const uint32_t *__restrict__ cnt,
-                               const int64_t *__restrict__ rowsum_delta, uint32_t *__restrict__ G,
-                               int64_t *__restrict__ grs, int64_t *__restrict__ scal) {
+// One wave per row with a non-empty delta; the int views of the row-sum deltas are summed per
+// workgroup (one global atomic per workgroup, not per row).
+__global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *__restrict__ row_base,
+                                                      const int32_t *__restrict__ row_nnz,
+                                                      const int32_t *__restrict__ col, const uint32_t *__restrict__ cnt,
+                                                      const int64_t *__restrict__ rowsum_delta,
+                                                      uint32_t *__restrict__ G, int64_t *__restrict__ grs,
+                                                      int64_t *__restrict__ scal) {
+  __shared__ int64_t s_d32[4];
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  int64_t d32 = 0;
   for (int64_t a = wave; a < M; a += n_waves) {
     const int32_t n = row_nnz[a];
     if (n == 0) continue;
@@ -56,10 +61,14 @@ __global__ void k_merge_global(int32_t M, const int64_t *__restrict__ row_base, 
     if (lane == 0) {
       const int64_t d = rowsum_delta[a];
       grs[a] += d;
-      // RowSumAggregator's int value of this window's update, ItemRowRescorer...java:154
-      atomicAdd(reinterpret_cast<unsigned long long *>(scal + 1),
-                (unsigned long long)int64_t(int32_t(uint32_t(uint64_t(d)))));
+      d32 += int64_t(int32_t(uint32_t(uint64_t(d))));  // RowSumAggregator's int value, ItemRowRescorer...java:154
     }
+  }
+  if (lane == 0) s_d32[threadIdx.x >> 6] = d32;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t t = s_d32[0] + s_d32[1] + s_d32[2] + s_d32[3];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long *>(scal + 1), (unsigned long long)t);
   }
 }
 

@@ -69,6 +69,9 @@ enum cooc_status {
  * least half of the n_items^2 matrix and it fits in HBM, else the padded CSR). */
 #define COOC_FLAG_OUTPUT_CSR 2   /* always the padded CSR (row_base, row_nnz, col, cnt) */
 #define COOC_FLAG_OUTPUT_DENSE 4 /* always the dense matrix (dense, row_nnz) */
+/* Route every window through the sort-based general planner (the path for n_items >= 40,320) even
+ * when the batch planner applies; same results (A/B and tests). */
+#define COOC_FLAG_GENERAL_PLANNER 8
 
 typedef struct cooc_ctx cooc_ctx;
 

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--copy", action="store_true", help="also copy every window's outputs to the host")
     ap.add_argument("--users", type=int, default=138_493)
+    ap.add_argument("--planner", default="auto", choices=["auto", "general"])
     args = ap.parse_args()
 
     import torch
@@ -62,7 +63,7 @@ def main():
         user_ptr = np.concatenate([starts, [e - s]]).astype(np.int64)
         batches.append((w * 1000 + 999, user_ids.astype(np.int32), user_ptr, i_sorted[s:e].astype(np.int32)))
 
-    core = pkg.CooccurrenceCore(n_items=M, topk=args.topk, window_size_ms=1000, device=0)
+    core = pkg.CooccurrenceCore(n_items=M, topk=args.topk, window_size_ms=1000, device=0, planner=args.planner)
     lat, copy_s, pairs = [], [], []
     for ts_w, uid, uptr, items in batches:
         torch.cuda.synchronize()
@@ -82,7 +83,7 @@ def main():
         "config": "C4 streaming: C2-shaped log over %d x 1 s windows (seed 4)%s" % (
             args.windows, f", LLR top-{args.topk} rescoring of touched rows" if args.topk else ""),
         "users": int(len(lens)), "interactions": int(up[-1]), "n_items": M,
-        "windows": args.windows, "topk": args.topk,
+        "windows": args.windows, "topk": args.topk, "planner": args.planner,
         "window_latency_ms": {"median": float(np.median(lat_ms)), "p90": float(np.percentile(lat_ms, 90)),
                               "max": float(lat_ms.max()), "first": float(lat_ms[0]), "last": float(lat_ms[-1])},
         "total_s": float(np.sum(lat)), "ordered_pairs": total_pairs,

@@ -128,12 +128,15 @@ def test_micro_logs_batch(pkg, oracle, torch_cuda, log):
     assert got.observed == w["observed"]
 
 
+@pytest.mark.parametrize("planner", ["auto", "general"])
 @pytest.mark.parametrize("log", [l for l in micro_logs() if not l.get("closed_form_only")], ids=lambda l: l["name"])
-def test_micro_logs_operator(pkg, oracle, torch_cuda, log):
-    """The operator mirror (processElement / watermark firing / late drop) on the micro-logs."""
+def test_micro_logs_operator(pkg, oracle, torch_cuda, log, planner):
+    """The operator mirror (processElement / watermark firing / late drop) on the micro-logs, through
+    the batch planner (streaming windows over resident histories) and the general planner."""
     ev = micro_events(log)
     M = 1 + max(e[2] for e in ev if e[0] == "e")
-    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(log["window_ms"], n_items=M, top_k=3)
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(log["window_ms"], n_items=M, top_k=3,
+                                                                    planner=planner)
     got = run_events(ev, op.process_elements, op.process_watermark)
     ref = oracle.OracleStream(log["window_ms"], topk=3)
     want = run_events(ev, ref.process_elements, ref.process_watermark)
@@ -209,14 +212,16 @@ def test_count_device_padded_layout(pkg, oracle, torch_cuda):
         assert np.array_equal(nnz, np.diff(rp))
 
 
-def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("planner", ["auto", "general"])
+def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda, planner):
     """C1-shaped click log over 1 s windows: every window's delta rows, row sums, observed, the
     rescorer's top-k, and the final global state."""
     from flink_cooccurrence_amd import datagen
 
     d = datagen.config_c1(seed=1, U=2000, M=300, mean=20.0)
     users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
-    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=300, top_k=10)
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=300, top_k=10,
+                                                                    planner=planner)
     ref = oracle.OracleStream(1000, topk=10)
     got, want = [], []
     for lo in range(0, len(users), 7000):  # watermarks between chunks, like periodic watermarks
@@ -242,6 +247,44 @@ def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda):
     ex, v32 = op.core.global_rowsums()
     assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
     op.close()
+
+
+@pytest.mark.parametrize("planner", ["auto", "general"])
+def test_streaming_long_histories_vs_closed_form(pkg, oracle, torch_cuda, planner):
+    """Windows over resident histories longer than one fill thread's share (2,048 ids), with
+    repeats, users absent from some windows, and a row (item 0) split over several chunks: every
+    window's delta rows, row sums and observed equal the closed-form difference
+    C(A through window w) - C(A through window w - 1)."""
+    rng = np.random.default_rng(31)
+    M, n_win = 500, 3
+    heavy = [np.where(rng.random(3000) < 0.1, 0, rng.integers(1, M, 3000)) for _ in range(40)]
+    light = [rng.integers(0, M, int(rng.integers(1, 40))) for _ in range(2000)]
+    lists = heavy + light
+    parts = [[l[len(l) * w // n_win:len(l) * (w + 1) // n_win] for l in lists] for w in range(n_win)]
+    C_prev = sp.csr_matrix((M, M), dtype=np.int64)
+    rs_prev, obs_prev = np.zeros(M, np.int64), 0
+    with pkg.CooccurrenceCore(n_items=M, planner=planner) as core:
+        for w in range(n_win):
+            uids = [u for u in range(len(lists)) if len(parts[w][u])]
+            up = np.concatenate([[0], np.cumsum([len(parts[w][u]) for u in uids])]).astype(np.int64)
+            it = np.concatenate([parts[w][u] for u in uids]).astype(np.int32)
+            core.submit_batch(w * 1000 + 999, np.array(uids, np.int32), up, it)
+            got = core.finish_window(w * 1000 + 999)
+            cum = [np.concatenate([parts[v][u] for v in range(w + 1)]) for u in range(len(lists))]
+            cup = np.concatenate([[0], np.cumsum([len(c) for c in cum])]).astype(np.int64)
+            rp, cols, data, rs, obs = oracle.closed_form(cup, np.concatenate(cum).astype(np.int32), M)
+            C = sp.csr_matrix((data, cols, rp), shape=(M, M))
+            D = (C - C_prev).tocsr()
+            D.eliminate_zeros()
+            D.sort_indices()
+            rows = np.nonzero(np.diff(D.indptr))[0]
+            assert np.array_equal(got.rows, rows)
+            assert np.array_equal(np.diff(got.row_ptr), np.diff(D.indptr)[rows])
+            assert np.array_equal(got.cols, D.indices)
+            assert np.array_equal(np.asarray(got.exact, np.int64), D.data)
+            assert np.array_equal(got.rs_exact, (rs - rs_prev)[got.rs_items])
+            assert got.observed == obs - obs_prev
+            C_prev, rs_prev, obs_prev = C, rs, obs
 
 
 def test_streaming_exact_scores_flag(pkg, oracle, torch_cuda):
