@@ -40,6 +40,8 @@ class CoocConfig(ctypes.Structure):
         ("topk", ctypes.c_int32),
         ("flags", ctypes.c_int32),
         ("window_size_ms", ctypes.c_int64),
+        ("user_cut", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

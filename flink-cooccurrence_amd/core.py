@@ -76,9 +76,11 @@ class CooccurrenceCore:
     """One context of the C-ABI (one Flink subtask)."""
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
-                 exact_scores: bool = False, output: str = "auto", planner: str = "auto"):
+                 exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0):
         """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
-        planner: "auto" (the batch planner below 40,320 items) or "general" (the sort-based planner)."""
+        planner: "auto" (the batch planner below 40,320 items) or "general" (the sort-based planner).
+        user_cut: kMax, 0 = off; else only the first user_cut interactions of every user are expanded
+        (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped)."""
         L = _lib.load()
         flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
         if output not in ("auto", "csr", "dense"):
@@ -87,7 +89,7 @@ class CooccurrenceCore:
         if planner not in ("auto", "general"):
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown planner {planner!r}")
         flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner == "general" else 0
-        cfg = CoocConfig(device, n_items, topk, flags, window_size_ms)
+        cfg = CoocConfig(device, n_items, topk, flags, window_size_ms, user_cut, 0)
         h = ctypes.c_void_p()
         check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
         self._h = h
@@ -332,11 +334,13 @@ class NonSampledUserInteractionCounterOneInputStreamOperator:
     ROW_SUM_TAG = "rowSums"         # NonSampled...java:45-46
 
     def __init__(self, window_size: int, window_unit: str = "MILLISECONDS", *, n_items: int, top_k: int = 10,
-                 device: int = -1, exact_scores: bool = False, planner: str = "auto"):
+                 device: int = -1, exact_scores: bool = False, planner: str = "auto", user_cut: int = 0):
+        """user_cut (kMax, 0 = off): expand only the first user_cut interactions of every user
+        (UserInteractionCounter...java:168-205 without its random reservoir branch)."""
         if top_k <= 0:  # ItemRowRescorer...java:52-54
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"{top_k} is <= 0")
         self.core = CooccurrenceCore(n_items, top_k, window_size_ms(window_size, window_unit), device, exact_scores,
-                                     planner=planner)
+                                     planner=planner, user_cut=user_cut)
 
     def process_element(self, user: int, item: int, timestamp: int) -> bool:
         """Returns True when the record was late and dropped (NonSampled...java:89-91)."""

@@ -20,6 +20,8 @@ Status cooc_ctx::init(const cooc_config &c) {
   if (c.topk < 0 || c.topk > 32767)  // topK is a Java short (Configuration.java:153, ItemRowRescorer...java:31)
     return Status{COOC_ERR_ARG, std::to_string(c.topk) + " is not a valid topK"};
   if (c.window_size_ms <= 0) return Status{COOC_ERR_ARG, "window size must be > 0"};
+  if (c.user_cut < 0 || c.user_cut > 32767)  // userCut is a Java short (UserInteractionCounter...java:54,76)
+    return Status{COOC_ERR_ARG, std::to_string(c.user_cut) + " is not a valid userCut"};
   int n_dev = 0;
   hipError_t e = hipGetDeviceCount(&n_dev);
   if (e != hipSuccess || n_dev == 0) {
@@ -45,7 +47,8 @@ cooc_ctx::~cooc_ctx() {
   stream_state.release();
   sharder.release();
   counter.release();
-  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3};
+  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
+                          &b_cut_ptr, &b_cut_items, &b_cut_tmp};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
   if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);
@@ -57,6 +60,18 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   COOC_HIP_TRY(hipSetDevice(device));
   have_batch = false;
   batch_topk = 0;
+  if (cfg.user_cut > 0) {
+    // kMax (UserInteractionCounter...java:168): only the first user_cut items of every user are
+    // expanded; one capping pass over the CSR, then the same path on the capped copy
+    COOC_TRY(b_cut_ptr.reserve(sizeof(int64_t) * size_t(n_users + 1)));
+    COOC_TRY(b_cut_items.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(n_interactions, 1))));
+    int64_t n_cut = 0;
+    COOC_TRY(cooc::launch_user_cut(s, n_users, d_user_ptr, d_items, cfg.user_cut, b_cut_ptr.as<int64_t>(),
+                                   b_cut_items.as<int32_t>(), b_cut_tmp, &n_cut));
+    d_user_ptr = b_cut_ptr.as<int64_t>();
+    d_items = b_cut_items.as<int32_t>();
+    n_interactions = n_cut;
+  }
   cooc::CountResult r;
   if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));

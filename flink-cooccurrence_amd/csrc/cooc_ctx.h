@@ -66,6 +66,7 @@ class StreamState {
   DevBuf d_global_, d_grs_, d_touched_, d_scan_tmp_, d_scal_, d_topk_val_, d_topk_score_, d_topk_size_;
   // last window
   bool have_window_ = false;
+  bool empty_window_ = false;  // the last window had no interaction left after user_cut
   cooc_window_info last_{};
   int32_t n_touched_ = 0;
 };
@@ -121,6 +122,8 @@ struct cooc_ctx {
 
   // stateless batch buffers
   cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3;
+  // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
+  cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
   int32_t batch_topk = 0;
   bool have_batch = false;
   int64_t batch_observed = 0;

@@ -100,10 +100,20 @@ Status StreamState::submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int
       if (items[i] < 0 || items[i] >= M)
         return Status{COOC_ERR_ARG, "item id " + std::to_string(items[i]) + " outside [0, n_items)"};
   }
+  const int64_t cut = ctx.cfg.user_cut;
   for (int32_t u = 0; u < n_users; u++) {
     const int32_t slot = slot_for(user_ids[u]);
+    const bool staged = staged_stamp_[slot] == window_seq_;
+    int64_t take = user_ptr[u + 1] - user_ptr[u];
+    if (cut > 0) {
+      // kMax: `userInteractions < userCut` (UserInteractionCounter...java:168) -- every accepted
+      // interaction appends once to the history, so the accepted count is the history length
+      const int64_t seen = int64_t(h_len_[slot]) + (staged ? int64_t(staged_items_[staged_pos_[slot]].size()) : 0);
+      take = std::max<int64_t>(0, std::min<int64_t>(take, cut - seen));
+      if (take == 0) continue;  // nothing of this user enters the window
+    }
     int32_t j;
-    if (staged_stamp_[slot] != window_seq_) {  // first appearance of this user in the window
+    if (!staged) {  // first appearance of this user in the window
       staged_stamp_[slot] = window_seq_;
       j = n_staged_++;
       staged_pos_[slot] = j;
@@ -118,7 +128,7 @@ Status StreamState::submit(cooc_ctx &ctx, int64_t ts, int32_t n_users, const int
       j = staged_pos_[slot];
     }
     auto &dst = staged_items_[j];
-    dst.insert(dst.end(), items + user_ptr[u], items + user_ptr[u + 1]);
+    dst.insert(dst.end(), items + user_ptr[u], items + user_ptr[u] + take);
   }
   staged_ = true;
   staged_ts_ = ts;
@@ -169,6 +179,20 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   const int32_t M = ctx.cfg.n_items;
   const int64_t n_act = n_staged_;
   PhaseTrace tr;
+  empty_window_ = n_act == 0;
+  if (empty_window_) {
+    // every interaction of the window was cut (user_cut): onEventTime emits nothing, no row is
+    // touched and the global state is unchanged
+    std::memset(&last_, 0, sizeof(last_));
+    last_.ts = ts;
+    last_.topk = ctx.cfg.topk;
+    *info = last_;
+    n_touched_ = 0;
+    have_window_ = true;
+    staged_ = false;
+    window_seq_++;
+    return Status::Ok();
+  }
 
   // ---- host plan: history capacity (relocation on growth), append destinations, contributions
   std::vector<int64_t> act_off(n_act), cbase(n_act + 1, 0), new_ptr(n_act + 1, 0), new_dst(n_act), reloc;
@@ -286,6 +310,10 @@ Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, i
                                int16_t *cnt16) {
   if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
   COOC_HIP_TRY(hipSetDevice(ctx.device));
+  if (empty_window_) {
+    if (row_ptr) row_ptr[0] = 0;
+    return Status::Ok();
+  }
   const int32_t M = ctx.cfg.n_items;
   int64_t *d_rp;
   int32_t *d_col;
@@ -322,6 +350,7 @@ Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, i
 
 Status StreamState::copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32) {
   if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
+  if (empty_window_) return Status::Ok();
   COOC_HIP_TRY(hipSetDevice(ctx.device));
   const int32_t M = ctx.cfg.n_items;
   std::vector<int32_t> nnz(M);

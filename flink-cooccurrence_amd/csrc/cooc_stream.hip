@@ -39,6 +39,25 @@ __global__ void k_append(int64_t n, const int64_t *__restrict__ new_ptr, const i
   }
 }
 
+// kMax cap (UserInteractionCounter...java:168): capped length min(n_u, cut) of every user at
+// lens[u + 1]; an inclusive scan of lens[1..U] gives the capped offsets.
+__global__ void k_cut_lens(int64_t U, const int64_t *__restrict__ up, int32_t cut, int64_t *__restrict__ lens) {
+  const int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (u < U) lens[u + 1] = min(up[u + 1] - up[u], int64_t(cut));
+}
+
+// One wave per user copies its first (capped) items; the source rows are read coalesced.
+__global__ void k_cut_copy(int64_t U, const int64_t *__restrict__ up, const int32_t *__restrict__ items,
+                           const int64_t *__restrict__ cut_ptr, int32_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t u = wave; u < U; u += n_waves) {
+    const int64_t s = up[u], d = cut_ptr[u], n = cut_ptr[u + 1] - d;
+    for (int64_t i = lane; i < n; i += 64) out[d + i] = items[s + i];
+  }
+}
+
 // One wave per row with a non-empty delta; the int views of the row-sum deltas are summed per
 // workgroup (one global atomic per workgroup, not per row).
 __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *__restrict__ row_base,
@@ -262,6 +281,33 @@ Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, co
       M, row_base, row_nnz, col, cnt, rowsum_delta, G, grs, scal);
   k_finish_scalars<<<1, 1, 0, s>>>(scal, observed_window);
   COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_user_cut(hipStream_t s, int64_t n_users, const int64_t *up, const int32_t *items, int32_t cut,
+                       int64_t *cut_ptr, int32_t *cut_items, DevBuf &tmp, int64_t *n_cut) {
+  *n_cut = 0;
+  if (n_users <= 0) {
+    COOC_HIP_TRY(hipMemsetAsync(cut_ptr, 0, sizeof(int64_t), s));
+    return Status::Ok();
+  }
+  // tmp = [capped lengths int64[n_users + 1] | scan workspace] (the scan is not in place)
+  const size_t lens_bytes = (sizeof(int64_t) * size_t(n_users + 1) + 255) / 256 * 256;
+  size_t bytes = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, cut_ptr, cut_ptr + 1, int(n_users), s));
+  COOC_TRY(tmp.reserve(lens_bytes + bytes));
+  int64_t *lens = tmp.as<int64_t>();
+  k_cut_lens<<<blocks_for(n_users, 256), 256, 0, s>>>(n_users, up, cut, lens);
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemsetAsync(cut_ptr, 0, sizeof(int64_t), s));
+  bytes = tmp.cap - lens_bytes;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(static_cast<char *>(tmp.p) + lens_bytes, bytes, lens + 1,
+                                                cut_ptr + 1, int(n_users), s));
+  const int64_t waves = std::min<int64_t>(n_users, int64_t(1) << 16);
+  k_cut_copy<<<blocks_for(waves * 64, 256), 256, 0, s>>>(n_users, up, items, cut_ptr, cut_items);
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemcpyAsync(n_cut, cut_ptr + n_users, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
   return Status::Ok();
 }
 

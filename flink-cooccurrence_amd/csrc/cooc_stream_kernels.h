@@ -13,6 +13,10 @@ Status launch_append(hipStream_t s, int64_t n, const int64_t *new_ptr, const int
 Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                            const int32_t *col, const uint32_t *cnt, const int64_t *rowsum_delta, uint32_t *G,
                            int64_t *grs, int64_t *scal, int64_t observed_window);
+// kMax cap of a device CSR: cut_ptr int64[n_users+1], cut_items int32[<= n]; *n_cut = cut_ptr[n_users]
+// (read back: the caller sizes the next pass with it).
+Status launch_user_cut(hipStream_t s, int64_t n_users, const int64_t *up, const int32_t *items, int32_t cut,
+                       int64_t *cut_ptr, int32_t *cut_items, DevBuf &tmp, int64_t *n_cut);
 Status launch_touched(hipStream_t s, int32_t M, const int32_t *row_nnz, int32_t *touched, int64_t *n_touched,
                       DevBuf &tmp);
 size_t rescore_lds_bytes(int32_t topk);

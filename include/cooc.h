@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 2
+#define COOC_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -83,6 +83,13 @@ typedef struct cooc_config {
   int32_t flags;          /* COOC_FLAG_* */
   int64_t window_size_ms; /* TumblingEventTimeWindows.of(Time.of(windowSize, windowUnit)),
                              NonSampled...java:61-62, in milliseconds */
+  int32_t user_cut;       /* kMax: 0 = off (the non-sampled path).  1..32767 (a Java short,
+                             UserInteractionCounter...java:54,76): only the first user_cut
+                             interactions of every user (arrival order, over all windows) are
+                             expanded -- the `userInteractions < userCut` branch of
+                             UserInteractionCounter...java:168-205; later interactions are dropped
+                             (the reference's random reservoir branch, :206-240, is not restated) */
+  int32_t reserved;
 } cooc_config;
 
 /* Sizes of one fired window's outputs (two-phase copy protocol). */
@@ -232,6 +239,24 @@ COOC_API int cooc_shard_plan(cooc_ctx *ctx, int64_t n_users, const int64_t *d_us
 COOC_API int cooc_shard_count(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t *d_recv_row_counts,
                               const uint64_t *d_recv_desc, int64_t n_recv, const uint16_t *d_arena_all,
                               int64_t arena_stride, void *hip_stream, cooc_device_result *out);
+
+/* ---- ItemCooccurrences wire codec (ItemCooccurrences.java:113-147, Kryo 2.24 primitives) --------
+ * Host-only (no device calls, no context).  A record is (item, increment int16, size other items):
+ * varint item, big-endian int16 increment, varint size', size' varints -- every varint is Kryo's
+ * writeInt(v, true).  For a mixed deployment that keeps the Java emitter or the Java reducer.
+ *   cooc_records_encode  n records: items int32[n], increments int16[n], ks int32[n] (slot k is
+ *                        skipped, ItemCooccurrences.java:124-131; NULL = all -1), rec_ptr
+ *                        int64[n+1] into others.  out == NULL: *n_bytes = encoded size only;
+ *                        else out must hold out_cap >= *n_bytes bytes.
+ *   cooc_records_decode  bytes -> *n_records, *n_others; pass NULL arrays to size them, then
+ *                        items int32[n_records], increments int16[n_records], rec_ptr
+ *                        int64[n_records+1], others int32[n_others] (any may be NULL).  A truncated
+ *                        record or a negative size fails with COOC_ERR_ARG. */
+COOC_API int cooc_records_encode(int64_t n_records, const int32_t *items, const int16_t *increments, const int32_t *ks,
+                                 const int64_t *rec_ptr, const int32_t *others, uint8_t *out, int64_t out_cap,
+                                 int64_t *n_bytes);
+COOC_API int cooc_records_decode(const uint8_t *bytes, int64_t n_bytes, int64_t *n_records, int64_t *n_others,
+                                 int32_t *items, int16_t *increments, int64_t *rec_ptr, int32_t *others);
 
 /* ---- diagnostics (not part of the reference surface) ------------------------------------------
  * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the

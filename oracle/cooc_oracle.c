@@ -353,6 +353,7 @@ typedef struct { /* one fired window's observable outputs */
 typedef struct {
   int64_t window_size;
   int32_t topk;
+  int32_t user_cut;  /* kMax, 0 = off: UserInteractionCounter...java:54,168 (deterministic branch only) */
   int64_t watermark; /* timerService.currentWatermark(); starts at Long.MIN_VALUE */
   /* keyed user history, NonSampled:57,129-161 */
   i32map user_idx;
@@ -390,6 +391,16 @@ EXPORT oc_state *oc_create(int64_t window_size, int32_t topk) {
   i32map_init(&s->grow_idx, 1024);
   i32map_init(&s->grs_idx, 1024);
   return s;
+}
+
+/* UserInteractionCounter(..., short userCut, ...), :76-81.  Only the `userInteractions < userCut`
+ * branch (:168-205) is restated: it is NonSampled's expansion for the first userCut sampled
+ * interactions of a user.  The reservoir branch (:206-240, a shared java.util.Random) is replaced by
+ * dropping the interaction: the deterministic subset SURVEY.md §8(f).4 names. */
+EXPORT int oc_set_user_cut(oc_state *s, int32_t user_cut) {
+  if (user_cut < 0 || user_cut > 32767) return 1; /* a Java short */
+  s->user_cut = user_cut;
+  return 0;
 }
 
 static void fired_free(fired_window *f) {
@@ -519,6 +530,8 @@ static void agg_rowsum(window_agg *g, int32_t item, int32_t update) {
  */
 static void expand_interaction(oc_state *s, window_agg *g, ivec *hist, int32_t item) {
   int64_t size = hist->n; /* :134-135 */
+  /* UserInteractionCounter...java:168: userInteractions (= history length here) < userCut */
+  if (s->user_cut > 0 && size >= s->user_cut) return;
   if (size > 0) {
     /* :138-139  ITEM (item, history[0..size), +1) -> ItemRowAggregator.add, :26-31 */
     rowmap *r = agg_row(g, item);

@@ -72,6 +72,7 @@ def lib():
         "oc_java_random_next_int32": (None, [ctypes.c_int64, ctypes.c_int32, i32p]),
         "oc_java_random_ints": (None, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, i32p]),
         "oc_create": (vp, [ctypes.c_int64, ctypes.c_int32]),
+        "oc_set_user_cut": (ctypes.c_int, [vp, ctypes.c_int32]),
         "oc_destroy": (None, [vp]),
         "oc_window_max_ts": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
         "oc_process_element": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
@@ -207,10 +208,12 @@ class WindowOutput:
 class OracleStream:
     """Record-by-record restatement of the skip-cuts job from the keyBy(user) edge onwards."""
 
-    def __init__(self, window_size_ms: int, topk: int = 0):
+    def __init__(self, window_size_ms: int, topk: int = 0, user_cut: int = 0):
         self._s = lib().oc_create(window_size_ms, topk)
         if not self._s:
             raise ValueError("bad window size / topk")
+        if lib().oc_set_user_cut(self._s, user_cut):
+            raise ValueError("userCut must be a Java short >= 0")
         self.topk = topk
         self._read = 0
 
@@ -313,6 +316,15 @@ def batch_dense(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
     return counts, rowsums, int(obs)
 
 
+def cut_csr(user_ptr: np.ndarray, items: np.ndarray, user_cut: int):
+    """The first user_cut items of every user (kMax, one window over empty histories)."""
+    user_ptr = np.asarray(user_ptr, np.int64)
+    lens = np.minimum(np.diff(user_ptr), user_cut)
+    keep = np.concatenate([np.arange(user_ptr[u], user_ptr[u] + lens[u]) for u in range(len(lens))]
+                          + [np.zeros(0, np.int64)])
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), np.asarray(items)[keep].astype(np.int32)
+
+
 def closed_form(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
     """C = A^T A - diag(colsum A) as a sorted CSR (scipy), row sums and observed."""
     import scipy.sparse as sp
@@ -335,8 +347,10 @@ def closed_form(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
     return C.indptr.astype(np.int64), C.indices.astype(np.int32), C.data.astype(np.int64), rowsums, observed
 
 
-def literal_python(histories: list[list[int]]):
-    """Pure-Python NonSampled...java:129-161 over per-user item lists (tiny inputs only)."""
+def literal_python(histories: list[list[int]], user_cut: int = 0):
+    """Pure-Python NonSampled...java:129-161 over per-user item lists (tiny inputs only).
+    user_cut > 0: UserInteractionCounter...java:168-205, an interaction is expanded only while the
+    user has fewer than user_cut accepted ones (later ones dropped, no reservoir)."""
     counts: dict[tuple[int, int], int] = {}
     rowsums: dict[int, int] = {}
     observed = 0
@@ -344,6 +358,8 @@ def literal_python(histories: list[list[int]]):
         history: list[int] = []
         for item in items:
             size = len(history)
+            if user_cut > 0 and size >= user_cut:
+                continue
             if size > 0:
                 for o in history:
                     counts[(item, o)] = counts.get((item, o), 0) + 1

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol(pkg):
     assert declared == _exported(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(L, name)
-    assert L.cooc_abi_version() == 2
+    assert L.cooc_abi_version() == 3
 
 
 def test_status_strings(pkg):
@@ -48,10 +48,14 @@ def test_argument_errors_mirror_reference(pkg):
         pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=10, top_k=0)
     with pytest.raises(pkg.IllegalArgumentException):
         pkg.window_size_ms(1, "WEEKS")  # Configuration.java:176-177
-    cfg = _lib.CoocConfig(-1, 0, 0, 0, 1000)
+    cfg = _lib.CoocConfig(-1, 0, 0, 0, 1000, 0, 0)
     h = ctypes.c_void_p()
     assert L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.COOC_ERR_ARG
     assert b"n_items" in L.cooc_last_error(None)
+    # userCut is a Java short (UserInteractionCounter...java:54): rejected before any device call
+    cfg = _lib.CoocConfig(-1, 10, 0, 0, 1000, 40000, 0)
+    assert L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.COOC_ERR_ARG
+    assert b"userCut" in L.cooc_last_error(None)
 
 
 def test_window_units(pkg):

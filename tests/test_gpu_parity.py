@@ -597,3 +597,59 @@ def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output):
         assert res.nnz == total
     for c in cores:
         c.close()
+
+
+@pytest.mark.parametrize("cut", [1, 4, 25, 32767])
+def test_batch_user_cut(pkg, oracle, torch_cuda, cut):
+    """kMax on the stateless batch: the device capping pass + the same path == the closed form of
+    every user's first `cut` items (UserInteractionCounter...java:168-205, deterministic branch)."""
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(31, 1500, 300, 20.0)
+    cup, cit = oracle.cut_csr(up, it, cut)
+    for output in ("csr", "dense"):
+        with pkg.CooccurrenceCore(n_items=300, output=output, user_cut=cut) as core:
+            got = core.count(up, it)
+        rp, cols, data, rowsums, observed = oracle.closed_form(cup, cit, 300)
+        assert got.observed == observed
+        assert np.array_equal(got.row_ptr, rp) and np.array_equal(got.cols, cols)
+        assert np.array_equal(got.cnt.astype(np.int64), data) and np.array_equal(got.rowsum, rowsums)
+
+
+@pytest.mark.parametrize("U,M,cut", [(2000, 300, 5), (20, 50, 2)])
+def test_streaming_user_cut_vs_oracle(pkg, oracle, torch_cuda, U, M, cut):
+    """kMax across windows: a user's later interactions are dropped once `cut` were accepted; windows
+    whose interactions are all dropped fire with no rows (U=20 makes most late windows empty)."""
+    from flink_cooccurrence_amd import datagen
+
+    if U > 100:
+        d = datagen.config_c1(seed=3, U=U, M=M, mean=20.0)
+        users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
+    else:  # few users over 10 s: after the first windows every user is capped
+        rng = np.random.default_rng(5)
+        users = rng.integers(0, U, 600).astype(np.int32)
+        items = rng.integers(0, M, 600).astype(np.int32)
+        ts = np.sort(rng.integers(0, 10_000, 600)).astype(np.int64)
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=M, top_k=5,
+                                                                    user_cut=cut)
+    ref = oracle.OracleStream(1000, topk=5, user_cut=cut)
+    got, want = [], []
+    for lo in range(0, len(users), 5000):
+        sl = slice(lo, lo + 5000)
+        op.process_elements(users[sl], items[sl], ts[sl])
+        ref.process_elements(users[sl], items[sl], ts[sl])
+        wm = int(ts[sl][-1]) - 1
+        got += op.process_watermark(wm)
+        want += ref.process_watermark(wm)
+    got += op.process_watermark(INT64_MAX)
+    want += ref.process_watermark(INT64_MAX)
+    assert len(got) == len(want) >= 1
+    if U <= 100:
+        assert len(got) == 10 and sum(len(w.rows) == 0 for w in want) >= 5
+    for g, w in zip(got, want):
+        assert_windows_equal(g, w)
+    assert op.accumulators() == ref.counters()
+    gi, gv32, gex = ref.global_rowsums()
+    ex, v32 = op.core.global_rowsums()
+    assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
+    op.close()

@@ -99,3 +99,38 @@ def test_window_assignment_matches_flink(oracle):
     assert oracle.window_max_ts(999, 1000) == 999
     assert oracle.window_max_ts(1000, 1000) == 1999
     assert oracle.window_max_ts(-1, 1000) == -1
+
+
+@pytest.mark.parametrize("cut", [1, 3, 7])
+def test_user_cut_restatements_agree(oracle, cut):
+    """kMax (UserInteractionCounter...java:168-205, deterministic branch): the record-by-record
+    oracle over several windows == the literal expansion of every user's first `cut` interactions ==
+    the closed form of the capped CSR."""
+    rng = np.random.default_rng(20 + cut)
+    U, M, n = 30, 12, 700
+    users = rng.integers(0, U, n).astype(np.int32)
+    items = rng.integers(0, M, n).astype(np.int32)
+    ts = np.sort(rng.integers(0, 8_000, n)).astype(np.int64)
+    s = oracle.OracleStream(1000, topk=3, user_cut=cut)
+    s.process_elements(users, items, ts)
+    wins = s.process_watermark(INT64_MAX)
+    tot = np.zeros((M, M), np.int64)
+    for w in wins:
+        for r, a in enumerate(w.rows):
+            tot[a, w.cols[w.row_ptr[r]:w.row_ptr[r + 1]]] += w.exact[w.row_ptr[r]:w.row_ptr[r + 1]]
+    order = np.lexsort((np.arange(n), users))
+    lens = np.bincount(users, minlength=U)
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    it = items[order]
+    counts, _, obs_lit = oracle.literal_python([it[up[u]:up[u + 1]].tolist() for u in range(U)], user_cut=cut)
+    D = np.zeros((M, M), np.int64)
+    for (a, b), v in counts.items():
+        D[a, b] = v
+    cup, cit = oracle.cut_csr(up, it, cut)
+    assert np.diff(cup).max() <= cut
+    rp, cols, data, rs, obs = oracle.closed_form(cup, cit, M)
+    assert np.array_equal(tot, D)
+    assert np.array_equal(D, sp.csr_matrix((data, cols, rp), shape=(M, M)).toarray())
+    assert s.counters()["UserInteractionCounterObservedCooccurrences"] == obs == obs_lit
+    with pytest.raises(ValueError):
+        oracle.OracleStream(1000, user_cut=40000)  # a Java short
