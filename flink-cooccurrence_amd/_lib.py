@@ -104,6 +104,9 @@ _SIGS = {
                                        ctypes.c_int64, vp, i64p, i64p]),
     "cooc_shard_count": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int64, vp,
                                         ctypes.c_int64, vp, ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_records_encode": (ctypes.c_int, [ctypes.c_int64, i32p, i16p, i32p, i64p, i32p, vp, ctypes.c_int64,
+                                           i64p]),
+    "cooc_records_decode": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i64p, i32p, i16p, i64p, i32p]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }

@@ -357,3 +357,38 @@ class NonSampledUserInteractionCounterOneInputStreamOperator:
 
     def close(self):
         self.core.close()
+
+
+# ---- ItemCooccurrences wire codec (ItemCooccurrences.java:113-147) --------------------------------
+def encode_item_cooccurrences(items, increments, rec_ptr, others, ks=None) -> bytes:
+    """Records (item, increment, others[rec_ptr[r]:rec_ptr[r+1]]) in the Kryo wire format of
+    ItemCooccurrences.Serializer.write; ks[r] != -1 skips slot k of record r (:124-131)."""
+    it = np.ascontiguousarray(items, np.int32)
+    inc = np.ascontiguousarray(increments, np.int16)
+    rp = np.ascontiguousarray(rec_ptr, np.int64)
+    ot = np.ascontiguousarray(others, np.int32)
+    kk = None if ks is None else np.ascontiguousarray(ks, np.int32)
+    L = _lib.load()
+    n = ctypes.c_int64()
+    args = (len(it), _p(it, i32p), _p(inc, i16p), None if kk is None else _p(kk, i32p), _p(rp, i64p), _p(ot, i32p))
+    check(L.cooc_records_encode(*args, None, 0, ctypes.byref(n)), None)
+    out = np.zeros(max(n.value, 1), np.uint8)
+    check(L.cooc_records_encode(*args, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)), None)
+    return out[: n.value].tobytes()
+
+
+def decode_item_cooccurrences(data: bytes):
+    """ItemCooccurrences.Serializer.read over a byte stream of records -> (items int32,
+    increments int16, rec_ptr int64, others int32)."""
+    buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+    L = _lib.load()
+    nr, no = ctypes.c_int64(), ctypes.c_int64()
+    bp = buf.ctypes.data_as(ctypes.c_void_p)
+    check(L.cooc_records_decode(bp, len(data), ctypes.byref(nr), ctypes.byref(no), None, None, None, None), None)
+    items = np.zeros(nr.value, np.int32)
+    inc = np.zeros(nr.value, np.int16)
+    rp = np.zeros(nr.value + 1, np.int64)
+    ot = np.zeros(no.value, np.int32)
+    check(L.cooc_records_decode(bp, len(data), ctypes.byref(nr), ctypes.byref(no), _p(items, i32p), _p(inc, i16p),
+                                _p(rp, i64p), _p(ot, i32p)), None)
+    return items, inc, rp, ot
