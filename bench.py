@@ -8,7 +8,7 @@ MovieLens-20M-shaped log (138,493 users x 26,744 items, 20,000,263 interactions)
 seed 2.  With --gpus N (one process per GPU, torchrun), every rank expands its own C2-shaped
 user shard (seed 2 + rank): users are independent units, so the per-GPU work is fixed ("weak").
 
-Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (k_accumulate, timed with
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (k_acc_batch, timed with
 HIP events on the stream it runs on) and a CPU baseline (the oracle's record-by-record
 restatement of the reference path, timed on a bounded sample of the same workload).
 """

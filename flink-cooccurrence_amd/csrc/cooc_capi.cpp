@@ -237,9 +237,10 @@ int cooc_shard_plan(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, c
   if (n_parts < 1) return fail(ctx, COOC_ERR_ARG, "n_parts must be >= 1");
   (void)hipSetDevice(ctx->device);
   ctx->have_batch = false;
-  Status s = ctx->counter.shard_plan(n_users, d_user_ptr, d_items, n_interactions, n_parts,
-                                     stream_of(ctx, hip_stream), d_desc, d_row_counts, d_arena, arena_cap, h_send,
-                                     h_info, h_info + 1);
+  Status s = ctx->apply_user_cut(n_users, &d_user_ptr, &d_items, &n_interactions, stream_of(ctx, hip_stream));
+  if (s.ok())
+    s = ctx->counter.shard_plan(n_users, d_user_ptr, d_items, n_interactions, n_parts, stream_of(ctx, hip_stream),
+                                d_desc, d_row_counts, d_arena, arena_cap, h_send, h_info, h_info + 1);
   return s.ok() ? COOC_OK : fail(ctx, s);
 }
 

@@ -1650,7 +1650,6 @@ Status Counter::init(int32_t n_items) {
                         reinterpret_cast<const void *>(k_accumulate2<4, true, 7>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
   if (n_items < kBatchMaxItems) {
-    const int acc_bytes = int(sizeof(uint32_t)) * ((n_items + 2) & ~1);
     for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 4>),
                           reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 8>),
                           reinterpret_cast<const void *>(k_acc_batch<4, 16, true>),

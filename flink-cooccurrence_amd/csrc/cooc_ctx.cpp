@@ -60,18 +60,7 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   COOC_HIP_TRY(hipSetDevice(device));
   have_batch = false;
   batch_topk = 0;
-  if (cfg.user_cut > 0) {
-    // kMax (UserInteractionCounter...java:168): only the first user_cut items of every user are
-    // expanded; one capping pass over the CSR, then the same path on the capped copy
-    COOC_TRY(b_cut_ptr.reserve(sizeof(int64_t) * size_t(n_users + 1)));
-    COOC_TRY(b_cut_items.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(n_interactions, 1))));
-    int64_t n_cut = 0;
-    COOC_TRY(cooc::launch_user_cut(s, n_users, d_user_ptr, d_items, cfg.user_cut, b_cut_ptr.as<int64_t>(),
-                                   b_cut_items.as<int32_t>(), b_cut_tmp, &n_cut));
-    d_user_ptr = b_cut_ptr.as<int64_t>();
-    d_items = b_cut_items.as<int32_t>();
-    n_interactions = n_cut;
-  }
+  COOC_TRY(apply_user_cut(n_users, &d_user_ptr, &d_items, &n_interactions, s));
   cooc::CountResult r;
   if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
@@ -79,6 +68,22 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
     COOC_TRY(count_general(n_users, d_user_ptr, d_items, n_interactions, s, &r));
   }
   return finish_batch(r, s, out);
+}
+
+Status cooc_ctx::apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, const int32_t **d_items,
+                                int64_t *n_interactions, hipStream_t s) {
+  if (cfg.user_cut <= 0) return Status::Ok();
+  // kMax (UserInteractionCounter...java:168): only the first user_cut items of every user are
+  // expanded; one capping pass over the CSR, then the same path on the capped copy
+  COOC_TRY(b_cut_ptr.reserve(sizeof(int64_t) * size_t(n_users + 1)));
+  COOC_TRY(b_cut_items.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(*n_interactions, 1))));
+  int64_t n_cut = 0;
+  COOC_TRY(cooc::launch_user_cut(s, n_users, *d_user_ptr, *d_items, cfg.user_cut, b_cut_ptr.as<int64_t>(),
+                                 b_cut_items.as<int32_t>(), b_cut_tmp, &n_cut));
+  *d_user_ptr = b_cut_ptr.as<int64_t>();
+  *d_items = b_cut_items.as<int32_t>();
+  *n_interactions = n_cut;
+  return Status::Ok();
 }
 
 cooc::Status cooc_ctx::count_general(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,

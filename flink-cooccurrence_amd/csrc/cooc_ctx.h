@@ -98,6 +98,9 @@ struct cooc_ctx {
 
   cooc::Status count_device(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
                             hipStream_t s, cooc_device_result *out);
+  // user_cut > 0: replaces the CSR by its capped copy (b_cut_*); no-op otherwise
+  cooc::Status apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, const int32_t **d_items,
+                              int64_t *n_interactions, hipStream_t s);
   cooc::Status count_general(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
                              int64_t n_interactions, hipStream_t s, cooc::CountResult *r);
   cooc::Status finish_batch(const cooc::CountResult &r, hipStream_t s, cooc_device_result *out);

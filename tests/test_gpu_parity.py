@@ -400,6 +400,7 @@ def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts, output):
         rstart = [sum(sharding.rows_owned(M, n_parts, o) for o in range(p))]
         recv_nnz = torch.cat([pk[1][rstart[0]:rstart[0] + R] for pk in packs])
         recv_ent = torch.cat([pk[2][int(pk[0][:p].sum()):int(pk[0][:p + 1].sum())] for pk in packs])
+        torch.cuda.synchronize()  # the gathers run on torch's stream, not the context's
         m = cores[p].merge_partitions(n_parts, p, recv_nnz, recv_ent, rowsum)
         torch.cuda.synchronize()
         assert m.n_items == R
@@ -531,8 +532,9 @@ def test_c2_scale_topk_rows(pkg, oracle, torch_cuda):
             assert np.array_equal(vals[a, :sizes[a]], wv)  # identical scores -> identical heap layout
 
 
-@pytest.mark.parametrize("W,output", [(2, "dense"), (3, "csr"), (4, "dense"), (3, "dense")])
-def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output):
+@pytest.mark.parametrize("W,output,cut", [(2, "dense", 0), (3, "csr", 0), (4, "dense", 0), (3, "dense", 0),
+                                          (3, "csr", 6), (2, "dense", 9)])
+def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output, cut):
     """The sharded-records entry points on one GPU: W user shards planned separately, the collectives
     done by slicing (all-gather of the arenas, all-to-all of row counts and descriptors), each owner's
     rows complete and equal to C of all users together."""
@@ -549,25 +551,29 @@ def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output):
     stride = max(pkg.CooccurrenceCore.shard_arena_cap(len(s[0]) - 1, len(s[1])) for s in shards)
     cores, parts = [], []
     for sup, sit in shards:
-        core = pkg.CooccurrenceCore(n_items=M, device=0, output=output)
+        core = pkg.CooccurrenceCore(n_items=M, device=0, output=output, user_cut=cut)  # kMax: capped per shard
         n = len(sit)
         desc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
         rc = torch.empty(M, dtype=torch.int32, device=dev)
         arena = torch.full((stride,), -1, dtype=torch.int16, device=dev)
+        torch.cuda.synchronize()  # the -1 fill must land before the plan writes the arena
         send, ids, obs = core.shard_plan(torch.from_numpy(sup).to(dev), torch.from_numpy(sit).to(dev), W, desc, rc,
                                          arena)
-        assert ids % 8 == 0 and ids <= stride and int(send.sum()) == n
+        assert ids % 8 == 0 and ids <= stride
+        assert int(send.sum()) == (int(np.minimum(np.diff(sup), cut).sum()) if cut else n)
         cores.append(core)
         parts.append((send, rc, desc, arena, obs))
     torch.cuda.synchronize()
     arena_all = torch.cat([p[3] for p in parts])
-    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    rp, cols, data, rowsums, observed = oracle.closed_form(*(oracle.cut_csr(up, it, cut) if cut else (up, it)), M)
     assert sum(p[4] for p in parts) == observed
     for o in range(W):
         R = sharding.rows_owned(M, W, o)
         before = sum(sharding.rows_owned(M, W, q) for q in range(o))
         recv_rc = torch.cat([p[1][before:before + R] for p in parts])
         recv_desc = torch.cat([p[2][int(p[0][:o].sum()):int(p[0][:o + 1].sum())] for p in parts])
+        # the gathers above run on torch's stream; the context's stream does not wait for it
+        torch.cuda.synchronize()
         res = cores[o].shard_count(W, o, recv_rc, recv_desc, arena_all, stride)
         torch.cuda.synchronize()
         assert res.n_items == R
