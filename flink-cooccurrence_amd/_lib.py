@@ -107,6 +107,8 @@ _SIGS = {
     "cooc_records_encode": (ctypes.c_int, [ctypes.c_int64, i32p, i16p, i32p, i64p, i32p, vp, ctypes.c_int64,
                                            i64p]),
     "cooc_records_decode": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i64p, i32p, i16p, i64p, i32p]),
+    "cooc_parse_interactions": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p,
+                                               i64p, i64p]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }

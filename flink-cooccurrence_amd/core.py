@@ -392,3 +392,37 @@ def decode_item_cooccurrences(data: bytes):
     check(L.cooc_records_decode(bp, len(data), ctypes.byref(nr), ctypes.byref(no), _p(items, i32p), _p(inc, i16p),
                                 _p(rp, i64p), _p(ot, i32p)), None)
     return items, inc, rp, ot
+
+
+# ---- text ingest (FlinkCooccurrences.java:55-61,207-229) -------------------------------------------
+def parse_interactions(data: bytes):
+    """'\\n'-delimited "user,item,timestamp" lines -> (users int32, items int32, ts int64), with the
+    reference's InteractionLineSplitter semantics; a rejected line raises IllegalArgumentException
+    naming its 0-based index."""
+    L = _lib.load()
+    n, bad = ctypes.c_int64(), ctypes.c_int64()
+    check(L.cooc_parse_interactions(data, len(data), 0, None, None, None, ctypes.byref(n), ctypes.byref(bad)), None)
+    users = np.zeros(n.value, np.int32)
+    items = np.zeros(n.value, np.int32)
+    ts = np.zeros(n.value, np.int64)
+    st = L.cooc_parse_interactions(data, len(data), n.value, _p(users, i32p), _p(items, i32p), _p(ts, i64p),
+                                   ctypes.byref(n), ctypes.byref(bad))
+    if st != _lib.COOC_OK:
+        raise _lib.IllegalArgumentException(st, f"line {bad.value} is not 'user,item,timestamp'")
+    return users, items, ts
+
+
+def run_text_source(op, data: bytes, records_per_watermark: int = 100_000) -> list:
+    """Drive an operator from the job's text input: records in file order, and after every
+    records_per_watermark records the AscendingTimestampExtractor watermark (largest timestamp so far
+    - 1, FlinkCooccurrences.java:221-229); Long.MAX_VALUE at the end of the input (PROCESS_ONCE)."""
+    users, items, ts = parse_interactions(data)
+    out, hi = [], None
+    for lo in range(0, len(users), records_per_watermark):
+        sl = slice(lo, lo + records_per_watermark)
+        op.process_elements(users[sl], items[sl], ts[sl])
+        m = int(ts[sl].max())
+        hi = m if hi is None else max(hi, m)
+        out += op.process_watermark(hi - 1)
+    out += op.process_watermark(2**63 - 1)
+    return out

@@ -258,6 +258,16 @@ COOC_API int cooc_records_encode(int64_t n_records, const int32_t *items, const 
 COOC_API int cooc_records_decode(const uint8_t *bytes, int64_t n_bytes, int64_t *n_records, int64_t *n_others,
                                  int32_t *items, int16_t *increments, int64_t *rec_ptr, int32_t *others);
 
+/* ---- text ingest (FlinkCooccurrences.java:55-61,207-229: TextInputFormat + InteractionLineSplitter) --
+ * Host-only.  text: n_bytes of '\n'-delimited "user,item,timestamp" lines ("\r\n" accepted, fields after
+ * the third ignored, as String.split(",") + Integer.valueOf / Long.valueOf).  users == NULL (or
+ * items / ts NULL): *n_records = the number of lines only.  Else parses up to cap records; a line
+ * that the reference's splitter rejects (NumberFormatException / ArrayIndexOutOfBoundsException)
+ * fails with COOC_ERR_ARG and its 0-based index in *bad_line.  The watermark of the reference's
+ * AscendingTimestampExtractor after a prefix of records is (largest timestamp so far) - 1. */
+COOC_API int cooc_parse_interactions(const char *text, int64_t n_bytes, int64_t cap, int32_t *users, int32_t *items,
+                                     int64_t *ts, int64_t *n_records, int64_t *bad_line);
+
 /* ---- diagnostics (not part of the reference surface) ------------------------------------------
  * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the
  * stream it is launched on; read back after a call that ran it. */

@@ -659,3 +659,29 @@ def test_streaming_user_cut_vs_oracle(pkg, oracle, torch_cuda, U, M, cut):
     ex, v32 = op.core.global_rowsums()
     assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
     op.close()
+
+
+def test_text_source_operator_vs_oracle(pkg, oracle, torch_cuda):
+    """The job's input path end to end: "user,item,timestamp" text -> parse (InteractionLineSplitter,
+    FlinkCooccurrences.java:207-219) -> the operator with ascending-timestamp watermarks (:221-229)
+    == the oracle fed the same records and watermarks."""
+    from flink_cooccurrence_amd import datagen
+
+    d = datagen.config_c1(seed=6, U=800, M=200, mean=15.0)
+    users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
+    text = "".join(f"{u},{i},{t}\r\n" for u, i, t in zip(users, items, ts)).encode()
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=200, top_k=5)
+    got = pkg.run_text_source(op, text, records_per_watermark=3000)
+    ref = oracle.OracleStream(1000, topk=5)
+    want, hi = [], None
+    for lo in range(0, len(users), 3000):
+        sl = slice(lo, lo + 3000)
+        ref.process_elements(users[sl], items[sl], ts[sl])
+        hi = int(ts[sl].max()) if hi is None else max(hi, int(ts[sl].max()))
+        want += ref.process_watermark(hi - 1)
+    want += ref.process_watermark(INT64_MAX)
+    assert len(got) == len(want) > 3
+    for g, w in zip(got, want):
+        assert_windows_equal(g, w)
+    assert op.accumulators() == ref.counters()
+    op.close()
