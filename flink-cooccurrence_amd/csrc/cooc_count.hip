@@ -546,15 +546,21 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
   const int64_t n_chunks = tot->n_chunks;
   for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
   uint32_t xr = 0;
+  if (tid == 0) {
+    s_chunk = atomicAdd(queue, 1);
+    s_self = 0;
+  }
+  __syncthreads();
+  // Chunks at M = 1e6 are small (C3: ~185 pairs per (row, tile)), so the per-chunk chain of global
+  // round trips dominates: the next chunk is dequeued when this one starts and its descriptor is
+  // loaded during this chunk's compaction.
+  int32_t ch = s_chunk;
+  Chunk c = ch < n_chunks ? chunks[ch] : Chunk{0, -1, 0, 0, 0};
   for (;;) {
-    if (tid == 0) {
-      s_chunk = atomicAdd(queue, 1);
-      s_self = 0;
-    }
-    __syncthreads();
-    const int32_t ch = s_chunk;
     if (ch >= n_chunks) break;
-    const Chunk c = chunks[ch];
+    int32_t nxt = 0;
+    if (tid == 0) nxt = atomicAdd(queue, 1);  // lands while this chunk is walked
+    const int64_t chunk_work = epre[c.end] - epre[c.begin];
     for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
       const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
       const int64_t *vp = VEC ? vpre : epre;
@@ -670,14 +676,20 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     // the -1 at x_p for every new position applies to column x_p = row, in the tile that holds it
     const bool own = c.row >= col_off && c.row < col_off + M;
     const uint32_t self_total = own ? s_self : 0u;
-    const int64_t chunk_rowsum = (epre[c.end] - epre[c.begin]) - int64_t(self_total);
+    const int64_t chunk_rowsum = chunk_work - int64_t(self_total);
     if (tid == 0) {
       if (own) acc[c.row - col_off] -= self_total;
       atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
       if (c.split >= 0)
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
+      s_chunk = nxt;
     }
     __syncthreads();
+    // every thread has read s_self (above) and s_chunk is published: reset the self counter for the
+    // next chunk (its first use follows the __syncthreads at the end of this iteration)
+    if (tid == 0) s_self = 0;
+    const int32_t ch_next = s_chunk;
+    const Chunk c_next = ch_next < n_chunks ? chunks[ch_next] : Chunk{0, -1, 0, 0, 0};
     if (c.split < 0) {
       uint64_t sum;
       int64_t used;
@@ -706,6 +718,8 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       }
     }
     __syncthreads();
+    ch = ch_next;
+    c = c_next;
   }
 }
 
