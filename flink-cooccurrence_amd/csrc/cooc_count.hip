@@ -583,7 +583,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
         const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
         const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
         uint32_t v = lo + lane;
-        if (v < hi) {
+        if (!(X & 4) && v < hi) {
           // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
           int32_t l = 0, r = nb;
           while (r - l > 1) {
@@ -1661,7 +1661,8 @@ Status Counter::init(int32_t n_items) {
                         reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 32>),
                         reinterpret_cast<const void *>(k_accumulate2<4, true, 3, 8>),
                         reinterpret_cast<const void *>(k_accumulate2<8, true, 0, 8>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 7>)})
+                        reinterpret_cast<const void *>(k_accumulate2<4, true, 7>),
+                        reinterpret_cast<const void *>(k_accumulate2<16, false, 4>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
   if (n_items < kBatchMaxItems) {
     for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 4>),
@@ -1788,7 +1789,8 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
                       : xmode_ == 1 ? k_accumulate2<4, true, 1> : xmode_ == 2 ? k_accumulate2<4, true, 2>
                       : xmode_ == 3 ? k_accumulate2<4, true, 3> : vunroll_ == 8 ? k_accumulate2<8, true> : vunroll_ == 2 ? k_accumulate2<2, true>
                                                               : k_accumulate2<4, true>)
-                    : (unroll_ == 32 ? k_accumulate2<32, false>
+                    : (xmode_ == 4 ? k_accumulate2<16, false, 4>  // experiment: no walk (C3 phase split)
+                       : unroll_ == 32 ? k_accumulate2<32, false>
                        : unroll_ == 8 ? k_accumulate2<8, false>
                        : unroll_ == 4 ? k_accumulate2<4, false> : k_accumulate2<16, false>);
   kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(tw) * 4, s>>>(
