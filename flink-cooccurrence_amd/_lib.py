@@ -79,6 +79,8 @@ _SIGS = {
     "cooc_last_error": (ctypes.c_char_p, [vp]),
     "cooc_count_device": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
                                          ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_count_device_owned": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.c_int32, vp,
+                                               ctypes.c_int64, vp, ctypes.POINTER(CoocDeviceResult)]),
     "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
     "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),

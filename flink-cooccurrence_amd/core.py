@@ -41,6 +41,19 @@ def _p(a: np.ndarray, t):
     return a.ctypes.data_as(t) if a is not None else None
 
 
+def _stream_arg(stream, tensor):
+    """The HIP stream a device-tensor entry point runs on: the caller's, else torch's current stream
+    on the tensor's device, so that the library's kernels are ordered after the work that produced
+    the inputs and before the work that consumes the outputs (cooc.h, stream contract)."""
+    if stream is not None:
+        return ctypes.c_void_p(int(stream))
+    import torch
+
+    if getattr(tensor, "is_cuda", False):
+        return ctypes.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)
+    return None
+
+
 @dataclass
 class BatchResult:
     """C of one window over empty histories, as a packed CSR over all n_items rows."""
@@ -115,10 +128,22 @@ class CooccurrenceCore:
         """user_ptr: int64 device tensor [U+1] (user_ptr[0] == 0); items: int32 device tensor."""
         res = CoocDeviceResult()
         n_users = int(user_ptr.numel()) - 1
-        sp = None if stream is None else ctypes.c_void_p(int(stream))
         check(_lib.load().cooc_count_device(self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()),
-                                            ctypes.c_void_p(items.data_ptr()), int(items.numel()), sp,
-                                            ctypes.byref(res)), self._h)
+                                            ctypes.c_void_p(items.data_ptr()), int(items.numel()),
+                                            _stream_arg(stream, items), ctypes.byref(res)), self._h)
+        return res
+
+    def count_device_owned(self, user_ptr, items, owner, part: int, item_counts, n_total: int,
+                           stream=None) -> CoocDeviceResult:
+        """Rows a with owner[a] == part over every user given (multi-GPU, n_items >= 40,320).
+        owner: int32 device tensor [n_items]; item_counts: int64 device tensor [n_items] of the
+        global log (n_total interactions)."""
+        res = CoocDeviceResult()
+        n_users = int(user_ptr.numel()) - 1
+        check(_lib.load().cooc_count_device_owned(
+            self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()), ctypes.c_void_p(items.data_ptr()),
+            int(items.numel()), ctypes.c_void_p(owner.data_ptr()), int(part), ctypes.c_void_p(item_counts.data_ptr()),
+            int(n_total), _stream_arg(stream, items), ctypes.byref(res)), self._h)
         return res
 
     def count(self, user_ptr, items) -> BatchResult:
@@ -163,11 +188,11 @@ class CooccurrenceCore:
         """row_nnz: int32 device tensor [n_items]; entries: int64 device tensor [sum of the plan]."""
         check(_lib.load().cooc_partition_pack(self._h, n_parts, ctypes.c_void_p(row_nnz.data_ptr()),
                                               ctypes.c_void_p(entries.data_ptr()) if entries.numel() else None,
-                                              None if stream is None else ctypes.c_void_p(int(stream))), self._h)
+                                              _stream_arg(stream, row_nnz)), self._h)
 
     def copy_rowsum_device(self, rowsum, stream=None) -> None:
         check(_lib.load().cooc_copy_rowsum_device(self._h, ctypes.c_void_p(rowsum.data_ptr()),
-                                                  None if stream is None else ctypes.c_void_p(int(stream))),
+                                                  _stream_arg(stream, rowsum)),
               self._h)
 
     def merge_partitions(self, n_parts: int, part: int, recv_row_nnz, recv_entries, rowsum_global=None,
@@ -177,7 +202,7 @@ class CooccurrenceCore:
             self._h, n_parts, part, ctypes.c_void_p(recv_row_nnz.data_ptr()),
             ctypes.c_void_p(recv_entries.data_ptr()) if recv_entries.numel() else None,
             None if rowsum_global is None else ctypes.c_void_p(rowsum_global.data_ptr()),
-            None if stream is None else ctypes.c_void_p(int(stream)), ctypes.byref(res)), self._h)
+            _stream_arg(stream, recv_row_nnz), ctypes.byref(res)), self._h)
         return res
 
     # ---- sharded records (multi-GPU owner routing of pair records) -------------------------------
@@ -197,7 +222,7 @@ class CooccurrenceCore:
             self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()), ctypes.c_void_p(items.data_ptr()),
             int(items.numel()), n_parts, ctypes.c_void_p(desc.data_ptr()) if desc.numel() else None,
             ctypes.c_void_p(row_counts.data_ptr()), ctypes.c_void_p(arena.data_ptr()), int(arena.numel()),
-            None if stream is None else ctypes.c_void_p(int(stream)), _p(send, i64p), _p(info, i64p)), self._h)
+            _stream_arg(stream, items), _p(send, i64p), _p(info, i64p)), self._h)
         return send, int(info[0]), int(info[1])
 
     def shard_count(self, n_parts: int, part: int, recv_row_counts, recv_desc, arena_all, arena_stride: int,
@@ -208,7 +233,7 @@ class CooccurrenceCore:
             self._h, n_parts, part, ctypes.c_void_p(recv_row_counts.data_ptr()),
             ctypes.c_void_p(recv_desc.data_ptr()) if recv_desc.numel() else None, int(recv_desc.numel()),
             ctypes.c_void_p(arena_all.data_ptr()), int(arena_stride),
-            None if stream is None else ctypes.c_void_p(int(stream)), ctypes.byref(res)), self._h)
+            _stream_arg(stream, recv_row_counts), ctypes.byref(res)), self._h)
         return res
 
     def set_kernel_timing(self, enable: bool = True) -> None:

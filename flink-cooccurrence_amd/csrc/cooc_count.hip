@@ -30,8 +30,6 @@ namespace {
 constexpr int kAccThreads = 1024;
 constexpr int kAccWaves = kAccThreads / 64;
 constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
-constexpr int kMaxLdsCounters = 40704;            // dense row in LDS (uint32 counters)
-constexpr int kTileMax = 32768;                   // column tile width when n_items exceeds one LDS row
 constexpr int kLdsBudget = 160 * 1024 - 512;      // dynamic LDS left after the kernels' static LDS
 constexpr int kBatchLdsBudget = 160 * 1024 - 1536;  // k_acc_batch: its static LDS is under 1.5 KB
 
@@ -138,52 +136,8 @@ __global__ void k_cap_total(const int64_t *__restrict__ row_base, const int64_t 
   tot->nnz_total = 0;
 }
 
-__device__ inline void wave_sync() {  // LDS visibility among the lanes of one wave
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 
-// Tile partition of every user's history (column tiles of width tw): per user, its items grouped by
-// tile (order inside a tile segment is irrelevant to the counts), and tb[j][t] = offset of tile t's
-// segment inside the user's list (t = 0..T).  One wave per user, tile cursors in LDS.
-__global__ __launch_bounds__(256) void k_tile_partition(int64_t n_users, const int64_t *__restrict__ off,
-                                                        const int32_t *__restrict__ len,
-                                                        const int32_t *__restrict__ arena, int32_t tw, int32_t T,
-                                                        uint16_t *__restrict__ tarena, int32_t *__restrict__ tb) {
-  extern __shared__ int32_t cur[];  // [4 waves][T + 1]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t *c = cur + wave * (T + 1);
-  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t j = gw; j < n_users; j += n_waves) {
-    const int32_t *h = arena + off[j];
-    uint16_t *o = tarena + off[j];
-    const int32_t n = len[j];
-    for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
-    wave_sync();
-    for (int32_t p = lane; p < n; p += 64) atomicAdd(&c[h[p] / tw], 1);
-    wave_sync();
-    if (lane == 0) {  // exclusive prefix (T is small)
-      int32_t run = 0;
-      for (int32_t t = 0; t <= T; t++) {
-        const int32_t x = c[t];
-        c[t] = run;
-        run += x;
-      }
-    }
-    wave_sync();
-    for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
-    wave_sync();
-    for (int32_t p = lane; p < n; p += 64) {
-      const int32_t it = h[p];
-      const int32_t t = it / tw;
-      o[atomicAdd(&c[t], 1)] = uint16_t(it - t * tw);  // tile-relative id (< 32768)
-    }
-    wave_sync();
-  }
-}
-
-// The one-tile path reads partner ids as u16 (n_items <= 40,704): half the bytes per pair.
+// The general path reads partner ids as u16 (n_items <= 40,704): half the bytes per pair.
 __global__ void k_narrow(const int32_t *__restrict__ src, int64_t n, uint16_t *__restrict__ dst) {
   const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
   if (i + 3 < n) {
@@ -226,24 +180,6 @@ __global__ void k_seg_start_pad(const uint32_t *__restrict__ cvals, int64_t n, c
   if (c < n) seg[c] = poff[cvals[c] >> 1] | (int64_t(1) << 63);
 }
 
-struct TileWorkOp {  // pair work of a contribution inside column tile t
-  const int32_t *tb;
-  int32_t T, t;
-  __host__ __device__ int64_t operator()(uint32_t v) const {
-    const int64_t j = v >> 1;
-    return int64_t(tb[j * (T + 1) + t + 1] - tb[j * (T + 1) + t]);
-  }
-};
-
-__global__ void k_seg_start_tile(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ aoff,
-                                 const int32_t *__restrict__ tb, int32_t T, int32_t t, int64_t *__restrict__ seg) {
-  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const uint32_t v = cvals[c];
-  const int64_t j = v >> 1;
-  seg[c] = (aoff[j] + tb[j * (T + 1) + t]) | (int64_t(1) << 63);  // batch path: every position is new
-}
-
 // ---- 6. chunk table -------------------------------------------------------------------------------
 __global__ void k_make_chunks(const int32_t *__restrict__ order, const int32_t *__restrict__ ord_nch,
                               const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_ptr,
@@ -263,23 +199,6 @@ __global__ void k_make_chunks(const int32_t *__restrict__ order, const int32_t *
     chunks[ord_cbase[r] + j] = Chunk{a, slot, b, e, (int64_t(j) << 32) | int64_t(r)};
     b = e;
   }
-}
-
-// Chunk queue order: j-major (every row's j-th chunk together, heaviest rows first within a j), so
-// that the workgroups running at the same time sweep the same users (contributions are in user
-// order inside a row) and share those users' lists in L2.
-__global__ void k_chunk_keys(const Chunk *__restrict__ chunks, int64_t n, uint64_t *__restrict__ keys,
-                             int32_t *__restrict__ idx) {
-  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  keys[i] = uint64_t(chunks[i].pad);
-  idx[i] = int32_t(i);
-}
-
-__global__ void k_chunk_gather(const Chunk *__restrict__ src, const int32_t *__restrict__ idx, int64_t n,
-                               Chunk *__restrict__ dst) {
-  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = src[idx[i]];
 }
 
 // Block-wide sum of a uint64 (kAccThreads threads).
@@ -512,27 +431,22 @@ __global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const
   seg[c] = (v & 1u) ? off + aold[j] : (off | (int64_t(1) << 63));
 }
 
-// ★ v2: the chunk's contributions are flattened into one virtual pair range.  Up to `db`
-// segment descriptors (virtual start, arena start) are staged in LDS per batch; the 16 waves split
-// the batch's range into equal contiguous pieces and walk it 64 lanes wide, so every lane stays
-// busy whatever the user-list lengths, and no wave waits on a per-user descriptor chain.
+// ★ general path (streaming windows with resident histories, n_items <= 40,704): the chunk's
+// contributions are flattened into one virtual pair range.  Up to `db` segment descriptors
+// (virtual start, arena start) are staged in LDS per batch; the 16 waves split the batch's range
+// into equal contiguous pieces and walk it 64 lanes wide, so every lane stays busy whatever the
+// user-list lengths, and no wave waits on a per-user descriptor chain.
 // VEC: every segment starts 16-B aligned and spans a multiple of 8 ids (user lists padded with
 // 0xFFFF in the arena, virtual starts from the padded prefix `vpre`), so each lane loads 8 partner
 // ids with one 16-B load: 8x fewer load instructions in flight for the same bytes.
-// X (experiments only, never the default): bit 0 = no LDS atomics (ids folded into a register),
-// bit 1 = partner loads redirected into the first 256 KB of the arena (L2-resident).
-// S (VEC): lanes per walker; each walker owns a contiguous range of 8-id groups and steps S groups
-// at a time (S = 8: one 128-B line per walker-step, a segment boundary every few steps).
-template <int U, bool VEC, int X = 0, int S = 64>
+template <int U, bool VEC>
 __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
     const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
-    const int64_t *__restrict__ vpre,
-    int32_t M, int32_t col_off, int32_t db, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
-    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, uint32_t *__restrict__ staging,
-    int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum, int64_t *__restrict__ err,
-    unsigned long long *__restrict__ bump, int64_t bump_cap, int64_t *__restrict__ seg_off,
-    int32_t *__restrict__ seg_nnz, int32_t T, int32_t t) {
+    const int64_t *__restrict__ vpre, int32_t M, int32_t db, const int64_t *__restrict__ row_base,
+    int32_t *__restrict__ row_nnz, int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
+    uint32_t *__restrict__ staging, int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum,
+    int64_t *__restrict__ err) {
   extern __shared__ int64_t lds64[];
   int64_t *s_seg = lds64;                                            // [db] arena start - virtual start
   uint32_t *s_vst = reinterpret_cast<uint32_t *>(lds64 + db);        // [db + 1] virtual starts
@@ -545,21 +459,15 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_chunks = tot->n_chunks;
   for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
-  uint32_t xr = 0;
-  if (tid == 0) {
-    s_chunk = atomicAdd(queue, 1);
-    s_self = 0;
-  }
-  __syncthreads();
-  // Chunks at M = 1e6 are small (C3: ~185 pairs per (row, tile)), so the per-chunk chain of global
-  // round trips dominates: the next chunk is dequeued when this one starts and its descriptor is
-  // loaded during this chunk's compaction.
-  int32_t ch = s_chunk;
-  Chunk c = ch < n_chunks ? chunks[ch] : Chunk{0, -1, 0, 0, 0};
   for (;;) {
+    if (tid == 0) {
+      s_chunk = atomicAdd(queue, 1);
+      s_self = 0;
+    }
+    __syncthreads();
+    const int32_t ch = s_chunk;
     if (ch >= n_chunks) break;
-    int32_t nxt = 0;
-    if (tid == 0) nxt = atomicAdd(queue, 1);  // lands while this chunk is walked
+    const Chunk c = chunks[ch];
     const int64_t chunk_work = epre[c.end] - epre[c.begin];
     for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
       const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
@@ -583,7 +491,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
         const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
         const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
         uint32_t v = lo + lane;
-        if (!(X & 4) && v < hi) {
+        if (v < hi) {
           // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
           int32_t l = 0, r = nb;
           while (r - l > 1) {
@@ -619,12 +527,10 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       } else {
         // groups of 8 ids; every segment boundary is a multiple of 8
         const uint32_t groups = total >> 3;
-        constexpr uint32_t kWalkers = kAccThreads / S;
-        const uint32_t q = uint32_t(tid) / S;
-        const uint32_t lo = uint32_t((uint64_t(groups) * q) / kWalkers);
-        const uint32_t hi = uint32_t((uint64_t(groups) * (q + 1)) / kWalkers);
-        uint32_t g = lo + uint32_t(tid) % S;
-        if (!(X & 4) && g < hi) {
+        const uint32_t lo = uint32_t((uint64_t(groups) * uint32_t(wave)) / kAccWaves);
+        const uint32_t hi = uint32_t((uint64_t(groups) * uint32_t(wave + 1)) / kAccWaves);
+        uint32_t g = lo + lane;
+        if (g < hi) {
           int32_t l = 0, r = nb;
           while (r - l > 1) {
             const int32_t m = (l + r) >> 1;
@@ -633,11 +539,11 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
           int32_t cur = l;
           uint32_t next = s_vst[cur + 1];
           int64_t base = s_seg[cur];
-          for (; g < hi; g += uint32_t(S) * U) {
+          for (; g < hi; g += 64u * U) {
             int64_t a[U];
 #pragma unroll
             for (int k = 0; k < U; k++) {
-              const uint32_t gk = g + uint32_t(S) * k;
+              const uint32_t gk = g + 64u * k;
               a[k] = -1;
               if (gk < hi) {
                 while ((gk << 3) >= next) {
@@ -646,7 +552,6 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
                   base = s_seg[cur];
                 }
                 a[k] = base + (int64_t(gk) << 3);
-                if (X & 2) a[k] &= 0x1FFF8;
               }
             }
             uint4 q[U];
@@ -659,12 +564,8 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
 #pragma unroll
               for (int h = 0; h < 4; h++) {
                 const uint32_t lo16 = w4[h] & 0xFFFFu, hi16 = w4[h] >> 16;
-                if (X & 1) {
-                  xr += (lo16 != 0xFFFFu ? lo16 : 0u) ^ (hi16 != 0xFFFFu ? hi16 : 0u);
-                } else {
-                  if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
-                  if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
-                }
+                if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
+                if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
               }
             }
           }
@@ -672,40 +573,25 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       }
       __syncthreads();
     }
-    if ((X & 1) && xr == 0xDEADBEEFu) acc[0] = 1;  // keeps the folded loads alive
-    // the -1 at x_p for every new position applies to column x_p = row, in the tile that holds it
-    const bool own = c.row >= col_off && c.row < col_off + M;
-    const uint32_t self_total = own ? s_self : 0u;
+    // the -1 at x_p for every new position applies to column x_p = row
+    const uint32_t self_total = s_self;
     const int64_t chunk_rowsum = chunk_work - int64_t(self_total);
     if (tid == 0) {
-      if (own) acc[c.row - col_off] -= self_total;
+      acc[c.row] -= self_total;
       atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
       if (c.split >= 0)
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
-      s_chunk = nxt;
     }
     __syncthreads();
-    // every thread has read s_self (above) and s_chunk is published: reset the self counter for the
-    // next chunk (its first use follows the __syncthreads at the end of this iteration)
-    if (tid == 0) s_self = 0;
-    const int32_t ch_next = s_chunk;
-    const Chunk c_next = ch_next < n_chunks ? chunks[ch_next] : Chunk{0, -1, 0, 0, 0};
     if (c.split < 0) {
       uint64_t sum;
       int64_t used;
-      const int32_t filled = bump ? 0 : row_nnz[c.row];  // entries of earlier column tiles (padded rows)
-      const uint32_t nnz = compact_row_ranges(acc, M, col_off, col_out, cnt_out,
-                                              Place{bump ? 0 : row_base[c.row] + filled, bump, bump_cap}, &used, &sum,
-                                              s_wave, &s_base);
+      const uint32_t nnz = compact_row_ranges(acc, M, 0, col_out, cnt_out, Place{row_base[c.row], nullptr, 0}, &used,
+                                              &sum, s_wave, &s_base);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
-        if (bump) {
-          seg_off[int64_t(c.row) * T + t] = used;
-          seg_nnz[int64_t(c.row) * T + t] = int32_t(nnz);
-        } else {
-          row_nnz[c.row] = filled + int32_t(nnz);
-        }
-        if (X == 0 && total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+        row_nnz[c.row] = int32_t(nnz);
+        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       }
     } else {
       uint32_t *srow = staging + int64_t(c.split) * M;
@@ -718,71 +604,34 @@ __global__ __launch_bounds__(kAccThreads) void k_accumulate2(
       }
     }
     __syncthreads();
-    ch = ch_next;
-    c = c_next;
   }
 }
 
 // ---- 8. split rows: compact the staging rows ------------------------------------------------------
+// bump == nullptr: rows go to their padded place row_base[a]; else to an exact-size bump region
+// (row_base[a] is set).
 __global__ __launch_bounds__(kAccThreads) void k_finalize_split(
-    const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M, int32_t col_off,
-    uint32_t *__restrict__ staging, const int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+    const PlanTotals *__restrict__ tot, const int32_t *__restrict__ split_row, int32_t M,
+    uint32_t *__restrict__ staging, int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
     int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out, int64_t *__restrict__ split_sum,
-    int64_t *__restrict__ err, unsigned long long *__restrict__ bump, int64_t bump_cap, int64_t *__restrict__ seg_off,
-    int32_t *__restrict__ seg_nnz, int32_t T, int32_t t) {
+    int64_t *__restrict__ err, unsigned long long *__restrict__ bump, int64_t bump_cap) {
   __shared__ uint32_t s_wave[kAccWaves];
   __shared__ uint64_t s_red[kAccWaves];
   __shared__ int64_t s_base;
   const int64_t n_split = tot->n_split;
   for (int64_t s = blockIdx.x; s < n_split; s += gridDim.x) {
     const int32_t a = split_row[s];
-    const int32_t filled = bump ? 0 : row_nnz[a];
     uint64_t sum;
     int64_t used;
-    const uint32_t nnz = compact_row_ranges(staging + s * M, M, col_off, col_out, cnt_out,
-                                            Place{bump ? 0 : row_base[a] + filled, bump, bump_cap}, &used, &sum, s_wave,
+    const uint32_t nnz = compact_row_ranges(staging + s * M, M, 0, col_out, cnt_out,
+                                            Place{bump ? 0 : row_base[a], bump, bump_cap}, &used, &sum, s_wave,
                                             &s_base);
     const uint64_t total = block_sum_u64(sum, s_red);
     if (threadIdx.x == 0) {
-      if (bump) {
-        seg_off[int64_t(a) * T + t] = used;
-        seg_nnz[int64_t(a) * T + t] = int32_t(nnz);
-      } else {
-        row_nnz[a] = filled + int32_t(nnz);
-      }
+      if (bump) row_base[a] = used;
+      row_nnz[a] = int32_t(nnz);
       if (total != uint64_t(split_sum[s])) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
       split_sum[s] = 0;
-    }
-  }
-}
-
-// Column-tiled runs: row a = its tile segments in tile order (each ascending) -> one packed row.
-__global__ void k_row_nnz_from_segs(const int32_t *__restrict__ seg_nnz, int32_t M, int32_t T,
-                                    int32_t *__restrict__ row_nnz) {
-  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= M) return;
-  int32_t n = 0;
-  for (int32_t t = 0; t < T; t++) n += seg_nnz[int64_t(a) * T + t];
-  row_nnz[a] = n;
-}
-
-__global__ void k_gather_segs(const int64_t *__restrict__ seg_off, const int32_t *__restrict__ seg_nnz, int32_t M,
-                              int32_t T, const int64_t *__restrict__ row_base, const int32_t *__restrict__ col_in,
-                              const uint32_t *__restrict__ cnt_in, int32_t *__restrict__ col_out,
-                              uint32_t *__restrict__ cnt_out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t a = wave; a < M; a += n_waves) {
-    int64_t dst = row_base[a];
-    for (int32_t t = 0; t < T; t++) {
-      const int32_t n = seg_nnz[a * T + t];
-      const int64_t src = seg_off[a * T + t];
-      for (int32_t i = lane; i < n; i += 64) {
-        col_out[dst + i] = col_in[src + i];
-        cnt_out[dst + i] = cnt_in[src + i];
-      }
-      dst += n;
     }
   }
 }
@@ -1272,9 +1121,7 @@ constexpr int kSlabRows = 4;
 // Output: DENSE = the counts as a dense row-major uint32 [M x M] matrix in HBM (row a written whole
 // from LDS with coalesced stores; split rows add their chunks into the zeroed dense row with
 // global atomics); otherwise the column-order sparse compaction into a bump-allocated padded CSR.
-// X (experiments only, never the default): bit 2 = skip the walk, bit 3 = compaction without stores.
-// ST: sparse output store flavour (compact_row_ranges kStore).
-template <int U, int S, bool DENSE, int X = 0, int ST = 1>
+template <int U, int S, bool DENSE>
 __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
     const Chunk *__restrict__ chunks, PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
     const uint64_t *__restrict__ desc, const uint16_t *__restrict__ arena, int32_t M, int32_t db, int32_t W,
@@ -1305,15 +1152,6 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
   int32_t ch = s_chunk;
   Chunk c = ch < n_chunks ? chunks[ch] : Chunk{0, -1, 0, 0, 0};
   uint64_t d = (tid < db && c.begin + tid < c.end) ? desc[c.begin + tid] : 0;
-  uint64_t ph[5] = {0, 0, 0, 0, 0};  // X & 64: phase times (wall clock, thread 0)
-  uint64_t t_last = (X & 64) ? wall_clock64() : 0;
-  auto stamp = [&](int k) {
-    if (X & 64) {
-      const uint64_t t = wall_clock64();
-      ph[k] += t - t_last;
-      t_last = t;
-    }
-  };
   while (ch < n_chunks) {
     int32_t nxt = 0;
     if (tid == 0) nxt = atomicAdd(queue, 1);  // lands while this chunk is walked
@@ -1355,7 +1193,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       const uint32_t lo = uint32_t((uint64_t(total) * q) / kWalkers);
       const uint32_t hi = uint32_t((uint64_t(total) * (q + 1)) / kWalkers);
       uint32_t g = lo + ql;
-      if (!(X & 4) && g < hi) {
+      if (g < hi) {
         int32_t cur = s_qstart[q];
         uint32_t next = s_vst[cur + 1];
         int64_t base = s_seg[cur];
@@ -1410,7 +1248,6 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       }
       __syncthreads();
     }
-    stamp(0);
     if (tid == 0) s_chunk = nxt;
     // every contribution at a new position of the row's item has the -1 self term at its column.
     // Rows are local (output) indices; the row's item is part + row * W (W parts of the sharded path).
@@ -1429,7 +1266,6 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
     }
     __syncthreads();
-    stamp(1);
     if (DENSE && c.split < 0) {
       uint32_t *dst = dense + int64_t(c.row) * M;
       uint64_t sum = 0;
@@ -1439,7 +1275,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         uint4 *d4 = reinterpret_cast<uint4 *>(dst);
         for (int32_t q = tid; q < (M >> 2); q += kAccThreads) {
           const uint4 v = a4[q];
-          if (!(X & 8)) d4[q] = v;
+          d4[q] = v;
           a4[q] = make_uint4(0u, 0u, 0u, 0u);
           sum += uint64_t(v.x) + v.y + v.z + v.w;
           nnz += (v.x != 0u) + (v.y != 0u) + (v.z != 0u) + (v.w != 0u);
@@ -1447,7 +1283,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       } else {
         for (int32_t b = tid; b < M; b += kAccThreads) {
           const uint32_t v = acc[b];
-          if (!(X & 8)) dst[b] = v;
+          dst[b] = v;
           acc[b] = 0;
           sum += v;
           nnz += v != 0u;
@@ -1457,7 +1293,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
       const uint64_t both = block_sum_u64((sum << 24) | uint64_t(nnz), s_red);
       if (tid == 0) {
         row_nnz[c.row] = int32_t(both & 0xFFFFFFu);
-        if (X == 0 && (both >> 24) != uint64_t(chunk_rowsum))
+        if ((both >> 24) != uint64_t(chunk_rowsum))
           atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
       }
     } else if (DENSE) {
@@ -1469,18 +1305,17 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
           acc[b] = 0;
         }
       }
-    } else if (X & 16) {  // timing experiment: no compaction (counters left in LDS)
     } else if (c.split < 0) {
       uint64_t sum;
       int64_t used;
       const Place pl{0, bump, bump_cap, s_slab, int64_t(kSlabRows) * M, reinterpret_cast<unsigned long long *>(&tot->err)};
-      const uint32_t nnz = compact_row_ranges4<(X & 8) ? 0 : ST>(acc, M, col_out, cnt_out, pl, &used, &sum, s_wave,
+      const uint32_t nnz = compact_row_ranges4<1>(acc, M, col_out, cnt_out, pl, &used, &sum, s_wave,
                                                                   &s_base);
       const uint64_t total = block_sum_u64(sum, s_red);
       if (tid == 0) {
         row_base[c.row] = used;
         row_nnz[c.row] = int32_t(nnz);
-        if (X == 0 && total != uint64_t(chunk_rowsum))
+        if (total != uint64_t(chunk_rowsum))
           atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
       }
     } else {
@@ -1493,17 +1328,11 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_batch(
         }
       }
     }
-    stamp(2);
     __syncthreads();
-    stamp(3);
-    ph[4]++;
     ch = ch2;
     c = c2;
     d = d2;
   }
-  if ((X & 64) && tid == 0)
-    for (int k = 0; k < 5; k++)  // after the split rows' sums (the host reserves 8 more)
-      atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + tot->n_split + 1 + k), (unsigned long long)ph[k]);
 }
 
 // Dense output: rows of items without interactions (no chunk) are zero; one wave per row.
@@ -1632,97 +1461,43 @@ Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr
 Status Counter::init(int32_t n_items) {
   if (n_items <= 0) return Status{1, "n_items must be positive"};
   M_ = n_items;
-  // one LDS row over all items when it fits, else column tiles of <= kTileMax counters
-  if (n_items <= kMaxLdsCounters) {
-    T_ = 1;
-    tw_ = n_items;
-  } else {
-    T_ = (n_items + kTileMax - 1) / kTileMax;
-    tw_ = (n_items + T_ - 1) / T_;
-    if (T_ > 1024) return Status{1, "n_items too large (more than 1024 column tiles)"};
-  }
   COOC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_tot_), sizeof(PlanTotals), hipHostMallocDefault));
-  const size_t lds = size_t(tw_) * 4;
-  db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
-  if (db_ < 32) return Status{1, "column tile too wide for the LDS row plus descriptors"};
-  const size_t lds2 = size_t(db_) * 12 + 4 + lds;
-  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<4, false>),
-                        reinterpret_cast<const void *>(k_accumulate2<8, false>),
-                        reinterpret_cast<const void *>(k_accumulate2<16, false>),
-                        reinterpret_cast<const void *>(k_accumulate2<32, false>),
-                        reinterpret_cast<const void *>(k_accumulate2<2, true>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true>),
-                        reinterpret_cast<const void *>(k_accumulate2<8, true>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 1>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 2>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 3>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 8>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 16>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 0, 32>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 3, 8>),
-                        reinterpret_cast<const void *>(k_accumulate2<8, true, 0, 8>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true, 7>),
-                        reinterpret_cast<const void *>(k_accumulate2<16, false, 4>)})
-    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
-  if (n_items < kBatchMaxItems) {
-    for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 4>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, true, 8>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 16, true>),
-                          reinterpret_cast<const void *>(k_acc_batch<2, 8, true>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, true>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 4>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 8>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false, 0, 3>),
-                          reinterpret_cast<const void *>(k_acc_batch<4, 8, false>)})
-      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsBudget));
-    for (const void *k : {reinterpret_cast<const void *>(k_batch_hist), reinterpret_cast<const void *>(k_batch_scatter)})
-      COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(sizeof(uint32_t)) * n_items));
-  }
-  const char *sm = getenv("COOC_ACC_STORE");
-  store_mode_ = sm ? atoi(sm) : 1;
-  const char *aw = getenv("COOC_ACC_WGS");
-  acc_wgs_ = aw ? atoi(aw) : 1;
-  const char *cw = getenv("COOC_CHUNK_WORK");
-  chunk_work_ = cw ? std::max<int64_t>(4096, atoll(cw)) : kChunkWork;
-  const char *bs = getenv("COOC_BATCH_STRIDE");
-  bstride_ = bs ? atoi(bs) : 16;
-  const char *bu = getenv("COOC_BATCH_UNROLL");
-  bunroll_ = bu ? atoi(bu) : 4;
-  const char *co = getenv("COOC_CHUNK_ORDER");
-  chunk_order_ = co ? atoi(co) : 0;
-  const char *vv = getenv("COOC_ACC_VEC");
-  vec_allowed_ = !(vv && vv[0] == '0');
-  const char *vu = getenv("COOC_ACC_VUNROLL");
-  vunroll_ = vu ? atoi(vu) : 4;
-  const char *vx = getenv("COOC_ACC_X");
-  xmode_ = vx ? atoi(vx) : 0;
-  const char *vs = getenv("COOC_ACC_VSTRIDE");
-  vstride_ = vs ? atoi(vs) : 64;
-  if (vunroll_ != 2 && vunroll_ != 8) vunroll_ = 4;
-  const char *u = getenv("COOC_ACC_UNROLL");
-  unroll_ = u ? atoi(u) : 16;
-  if (unroll_ != 4 && unroll_ != 8 && unroll_ != 32) unroll_ = 16;
   int dev = 0;
   COOC_HIP_TRY(hipGetDevice(&dev));
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu_, hipDeviceAttributeMultiprocessorCount, dev));
+  if (n_items >= kBatchMaxItems) return Status::Ok();  // run_sparse (cooc_sparse.hip) sets its own attributes
+  // general planner (streaming windows): one LDS row over all items plus the descriptor batch
+  const size_t lds = size_t(n_items) * 4;
+  db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
+  if (db_ < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
+  const size_t lds2 = size_t(db_) * 12 + 4 + lds;
+  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<16, false>),
+                        reinterpret_cast<const void *>(k_accumulate2<4, true>)})
+    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 16, true>),
+                        reinterpret_cast<const void *>(k_acc_batch<4, 8, false>)})
+    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsBudget));
+  for (const void *k : {reinterpret_cast<const void *>(k_batch_hist), reinterpret_cast<const void *>(k_batch_scatter)})
+    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(sizeof(uint32_t)) * n_items));
   return Status::Ok();
 }
 
 void Counter::release() {
-  DevBuf *all[] = {&dense_, &bh_, &uidx_, &long_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_, &sort_tmp_, &epre_, &row_ptr_, &row_work_,
-                   &row_nch_, &row_cap_, &row_split_, &order_keys_, &order_, &ord_nch_, &ord_cbase_,
-                   &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_, &col_, &cnt_, &staging_,
-                   &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_, &split_sum_, &tarena_, &tb_, &chunks2_, &ckeys_, &cidx_, &bump_, &seg_off_,
-                   &seg_nnz_, &col2_, &cnt2_, &plen_, &poff_, &vpre_};
+  DevBuf *all[] = {&dense_, &bh_, &uidx_, &long_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_,
+                   &sort_tmp_, &epre_, &row_ptr_, &row_work_, &row_nch_, &row_cap_, &row_split_, &order_keys_,
+                   &order_, &ord_nch_, &ord_cbase_, &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_,
+                   &col_, &cnt_, &staging_, &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_,
+                   &split_sum_, &tarena_, &bump_, &seg_off_, &plen_, &poff_, &vpre_, &send_, &witems_, &sp_arena_, &sp_tb_,
+                   &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
 }
 
-// Plan, accumulate and compact one column tile [col_off, col_off + tw) given the per-contribution
-// work prefix (epre) and segment starts (seg) of that tile.
-Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer) {
-  const int32_t M = M_, tw = tw_;
+// Plan, accumulate and compact given the per-contribution work prefix (epre) and segment starts
+// (seg) of a window (general planner, one LDS row per chunk).
+Status Counter::run_tile(const uint16_t *arena, int64_t n, hipStream_t s, KernelTimer *timer) {
+  const int32_t M = M_;
   int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
   PlanTotals *tot = tot_.as<PlanTotals>();
   uint64_t *okeys = order_keys_.as<uint64_t>();
@@ -1755,63 +1530,30 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
   COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
   COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
   if (n_split > 0) {
-    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(tw);
+    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
     COOC_TRY(staging_.reserve(need));
     COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
   }
   k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
                                                    epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
   COOC_HIP_TRY(hipGetLastError());
-  if (chunk_order_ == 1 && n_split > 0) {
-    COOC_TRY(chunks2_.reserve(sizeof(Chunk) * (n_chunks + 1)));
-    COOC_TRY(ckeys_.reserve(sizeof(uint64_t) * 2 * (n_chunks + 1)));
-    COOC_TRY(cidx_.reserve(sizeof(int32_t) * 2 * (n_chunks + 1)));
-    uint64_t *k_in = ckeys_.as<uint64_t>(), *k_out = k_in + n_chunks + 1;
-    int32_t *i_in = cidx_.as<int32_t>(), *i_out = i_in + n_chunks + 1;
-    k_chunk_keys<<<blocks_for(n_chunks, 256), 256, 0, s>>>(chunks_.as<Chunk>(), n_chunks, k_in, i_in);
-    size_t q = 0;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, k_in, k_out, i_in, i_out, int(n_chunks), 0, 64, s));
-    COOC_TRY(sort_tmp_.reserve(q));
-    q = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, q, k_in, k_out, i_in, i_out, int(n_chunks), 0, 64, s));
-    k_chunk_gather<<<blocks_for(n_chunks, 256), 256, 0, s>>>(chunks_.as<Chunk>(), i_out, n_chunks,
-                                                             chunks2_.as<Chunk>());
-    COOC_HIP_TRY(hipGetLastError());
-    std::swap(chunks_, chunks2_);
-  }
   // ★ accumulate
   const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
-  if (timer && timer->enabled && col_off == 0) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  auto kern = vec_ ? (vstride_ == 8 ? (xmode_ == 3 ? k_accumulate2<4, true, 3, 8> : vunroll_ == 8 ? k_accumulate2<8, true, 0, 8>
-                                                                          : k_accumulate2<4, true, 0, 8>)
-                      : vstride_ == 16 ? k_accumulate2<4, true, 0, 16> : vstride_ == 32 ? k_accumulate2<4, true, 0, 32>
-                      : xmode_ == 7 ? k_accumulate2<4, true, 7>
-                      : xmode_ == 1 ? k_accumulate2<4, true, 1> : xmode_ == 2 ? k_accumulate2<4, true, 2>
-                      : xmode_ == 3 ? k_accumulate2<4, true, 3> : vunroll_ == 8 ? k_accumulate2<8, true> : vunroll_ == 2 ? k_accumulate2<2, true>
-                                                              : k_accumulate2<4, true>)
-                    : (xmode_ == 4 ? k_accumulate2<16, false, 4>  // experiment: no walk (C3 phase split)
-                       : unroll_ == 32 ? k_accumulate2<32, false>
-                       : unroll_ == 8 ? k_accumulate2<8, false>
-                       : unroll_ == 4 ? k_accumulate2<4, false> : k_accumulate2<16, false>);
-  kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(tw) * 4, s>>>(
-      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, vpre_.as<int64_t>(), tw,
-      col_off, db_,
+  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+  auto kern = vec_ ? k_accumulate2<4, true> : k_accumulate2<16, false>;
+  kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
+      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, vpre_.as<int64_t>(), M, db_,
       row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
-      staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(),
-      reinterpret_cast<int64_t *>(&tot->err), bump_mode_ ? bump_.as<unsigned long long>() : nullptr, bump_cap_,
-      seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), T_, col_off / tw);
+      staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
   COOC_HIP_TRY(hipGetLastError());
-  if (timer && timer->enabled && col_off + tw >= M) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
   if (n_split > 0) {
     const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
-    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), tw, col_off,
-                                                          staging_.as<uint32_t>(), row_base_.as<int64_t>(),
-                                                          row_nnz_.as<int32_t>(), col_.as<int32_t>(),
-                                                          cnt_.as<uint32_t>(), split_sum_.as<int64_t>(),
-                                                          reinterpret_cast<int64_t *>(&tot->err),
-                                                          bump_mode_ ? bump_.as<unsigned long long>() : nullptr,
-                                                          bump_cap_, seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), T_,
-                                                          col_off / tw);
+    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), M, staging_.as<uint32_t>(),
+                                                          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
+                                                          col_.as<int32_t>(), cnt_.as<uint32_t>(),
+                                                          split_sum_.as<int64_t>(),
+                                                          reinterpret_cast<int64_t *>(&tot->err), nullptr, 0);
     COOC_HIP_TRY(hipGetLastError());
   }
   return Status::Ok();
@@ -1820,11 +1562,12 @@ Status Counter::run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipS
 Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
   const int32_t M = M_;
   dense_mode_ = false;
+  last_rows_ = M;
   const int64_t n = au.n_contrib;
+  if (M > kMaxGeneralItems)
+    return Status{1, "n_items > " + std::to_string(kMaxGeneralItems) +
+                         " is supported for one-window batches (cooc_count_device), not for streaming windows"};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
-  if (T_ > 1 && au.n_new != au.n_contrib)
-    return Status{1, "n_items > " + std::to_string(kMaxLdsCounters) +
-                         " (column tiling) is supported for one-window batches, not for streaming windows"};
   // ---- workspace
   COOC_TRY(keys_in_.reserve(sizeof(uint32_t) * (n + 1)));
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n + 1)));
@@ -1892,7 +1635,7 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, work_it, epre + 1, int(n), s));
   }
-  // 3. row pointer; output capacity per row from the whole row's work (all column tiles)
+  // 3. row pointer; output capacity per row (padded CSR)
   k_row_ptr<<<blocks_for(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
   k_row_cap<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_cap_.as<int64_t>());
   COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t), s));
@@ -1907,27 +1650,10 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
   const int64_t cap = h_tot_->cap_total, work_total = h_tot_->work_total;
-  bump_mode_ = T_ > 1;
-  if (!bump_mode_) {
-    COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
-    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
-  } else {
-    // exact-size output: (row, tile) segments bump-allocated at compaction time, gathered at the end.
-    // The region is the padded bound capped by what the device can hold next to the final copy.
-    size_t free_b = 0, total_b = 0;
-    COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const int64_t budget = int64_t(free_b / 10 * 4) / 8;  // entries (col + cnt), 40% of free memory
-    bump_cap_ = std::max<int64_t>(1, std::min<int64_t>(cap, budget));
-    COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
-    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
-    COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
-    COOC_TRY(seg_off_.reserve(sizeof(int64_t) * size_t(M) * T_));
-    COOC_TRY(seg_nnz_.reserve(sizeof(int32_t) * size_t(M) * T_));
-    COOC_HIP_TRY(hipMemsetAsync(bump_.p, 0, sizeof(uint64_t) * 2, s));
-    COOC_HIP_TRY(hipMemsetAsync(seg_nnz_.p, 0, sizeof(int32_t) * size_t(M) * T_, s));
-  }
+  COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
+  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
 
-  vec_ = T_ == 1 && vec_allowed_ && au.n_new == au.n_contrib && n > 0;  // one-window batch: all kind 0
+  vec_ = au.n_new == au.n_contrib && n > 0;  // one-window batch: all kind 0
   if (vec_) {
     const int64_t U = au.n_active;
     COOC_TRY(plen_.reserve(sizeof(int64_t) * (U + 1)));
@@ -1953,8 +1679,8 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
         U, au.off, au.len, poff_.as<int64_t>(), au.arena, tarena_.as<uint16_t>());
     k_seg_start_pad<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, poff_.as<int64_t>(), seg_.as<int64_t>());
     COOC_HIP_TRY(hipGetLastError());
-    COOC_TRY(run_tile(tarena_.as<uint16_t>(), 0, n, s, timer));
-  } else if (T_ == 1) {
+    COOC_TRY(run_tile(tarena_.as<uint16_t>(), n, s, timer));
+  } else {
     if (n > 0) {
       k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
       COOC_HIP_TRY(hipGetLastError());
@@ -1969,65 +1695,15 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
       }
       a16 = tarena_.as<uint16_t>();
     }
-    COOC_TRY(run_tile(a16, 0, n, s, timer));
-  } else {
-    // column tiles: each user's history regrouped by tile once, then one pass per tile
-    COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (n + 8)));
-    COOC_TRY(tb_.reserve(sizeof(int32_t) * size_t(au.n_active + 1) * size_t(T_ + 1)));
-    if (au.n_active > 0) {
-      const int64_t waves = std::min<int64_t>(au.n_active, 65536);
-      k_tile_partition<<<blocks_for(waves * 64, 256), 256, sizeof(int32_t) * 4 * (T_ + 1), s>>>(
-          au.n_active, au.off, au.len, au.arena, tw_, T_, tarena_.as<uint16_t>(), tb_.as<int32_t>());
-      COOC_HIP_TRY(hipGetLastError());
-    }
-    for (int32_t t = 0; t < T_; t++) {
-      if (n > 0) {
-        hipcub::TransformInputIterator<int64_t, TileWorkOp, const uint32_t *> tw_it(
-            vals, TileWorkOp{tb_.as<int32_t>(), T_, t});
-        size_t b = 0;
-        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, tw_it, epre + 1, int(n), s));
-        COOC_TRY(sort_tmp_.reserve(b));
-        b = sort_tmp_.cap;
-        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, tw_it, epre + 1, int(n), s));
-        k_seg_start_tile<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, tb_.as<int32_t>(), T_, t,
-                                                            seg_.as<int64_t>());
-        COOC_HIP_TRY(hipGetLastError());
-      }
-      COOC_TRY(run_tile(tarena_.as<uint16_t>(), t * tw_, n, s, timer));
-    }
-  }
-  int32_t *out_col = col_.as<int32_t>();
-  uint32_t *out_cnt = cnt_.as<uint32_t>();
-  if (bump_mode_) {
-    uint64_t used = 0;
-    COOC_HIP_TRY(hipMemcpyAsync(&used, bump_.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    COOC_HIP_TRY(hipStreamSynchronize(s));
-    if (int64_t(used) > bump_cap_)
-      return Status{4, "column-tiled output needs " + std::to_string(used) + " entries, the region holds " +
-                           std::to_string(bump_cap_)};
-    k_row_nnz_from_segs<<<blocks_for(M, 256), 256, 0, s>>>(seg_nnz_.as<int32_t>(), M, T_, row_nnz_.as<int32_t>());
-    hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> nnz64(row_nnz_.as<int32_t>(), WidenI64{});
-    size_t b = 0;
-    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b, nnz64, row_base_.as<int64_t>(), M, s));
-    COOC_TRY(sort_tmp_.reserve(b));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, nnz64, row_base_.as<int64_t>(), M, s));
-    COOC_TRY(col2_.reserve(sizeof(int32_t) * (used + 1)));
-    COOC_TRY(cnt2_.reserve(sizeof(uint32_t) * (used + 1)));
-    k_gather_segs<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 16384), 256, 0, s>>>(
-        seg_off_.as<int64_t>(), seg_nnz_.as<int32_t>(), M, T_, row_base_.as<int64_t>(), col_.as<int32_t>(),
-        cnt_.as<uint32_t>(), col2_.as<int32_t>(), cnt2_.as<uint32_t>());
-    COOC_HIP_TRY(hipGetLastError());
-    out_col = col2_.as<int32_t>();
-    out_cnt = cnt2_.as<uint32_t>();
+    COOC_TRY(run_tile(a16, n, s, timer));
   }
   k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
   COOC_HIP_TRY(hipGetLastError());
 
   out->row_base = row_base_.as<int64_t>();
   out->row_nnz = row_nnz_.as<int32_t>();
-  out->col = out_col;
-  out->cnt = out_cnt;
+  out->col = col_.as<int32_t>();
+  out->cnt = cnt_.as<uint32_t>();
   out->rowsum = rowsum_.as<int64_t>();
   out->work = work_total;
   out->observed = work_total - au.n_new;
@@ -2228,14 +1904,13 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
   }
   dense_mode_ = dense;
   last_rows_ = R;
-  bump_mode_ = false;  // the bump region IS the sparse output (one column tile): no gather
   if (dense) {
     COOC_TRY(dense_.reserve(sizeof(uint32_t) * size_t(std::max<int64_t>(RM, 1))));
   } else {
     // rows are placed in per-workgroup slabs of kSlabRows * M entries; a slab switch abandons less
     // than one row (< M entries, a quarter of a slab) and every workgroup ends inside one slab
     const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(RM, pairs));
-    bump_cap_ = bound + bound / 3 + int64_t(n_cu_) * std::max<int64_t>(1, acc_wgs_) * (kSlabRows + 1) * int64_t(M);
+    bump_cap_ = bound + bound / 3 + int64_t(n_cu_) * (kSlabRows + 1) * int64_t(M);
     COOC_TRY(col_.reserve(sizeof(int32_t) * (bump_cap_ + 1)));
     COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (bump_cap_ + 1)));
   }
@@ -2262,16 +1937,10 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
     const size_t acc_bytes = sizeof(uint32_t) * size_t((M + 2) & ~1);
     const int db = int(std::min<int64_t>(1024, (int64_t(kBatchLdsBudget) - int64_t(acc_bytes) - 4) / 12));
     if (db < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
-    size_t lds = acc_bytes + size_t(db) * 12 + 4;
-    static const char *lp = getenv("COOC_ACC_LDS_MIN");  // experiments: inflate LDS to limit occupancy
-    if (lp) lds = std::max<size_t>(lds, size_t(atol(lp)));
-    const int64_t grid = std::min<int64_t>(n_chunks, int64_t(n_cu_) * std::max<int64_t>(1, acc_wgs_));
-    auto kern = dense_mode_ ? (xmode_ == 4 ? k_acc_batch<4, 8, true, 4> : xmode_ == 8 ? k_acc_batch<4, 8, true, 8>
-                               : bstride_ == 16 ? k_acc_batch<4, 16, true> : bunroll_ == 2 ? k_acc_batch<2, 8, true>
-                                                                                         : k_acc_batch<4, 8, true>)
-              : xmode_ == 4 ? k_acc_batch<4, 8, false, 4> : xmode_ == 8 ? k_acc_batch<4, 8, false, 8>
-              : xmode_ == 20 ? k_acc_batch<4, 8, false, 20> : xmode_ == 64 ? k_acc_batch<4, 8, false, 64>
-              : store_mode_ == 3 ? k_acc_batch<4, 8, false, 0, 3> : k_acc_batch<4, 8, false>;
+    const size_t lds = acc_bytes + size_t(db) * 12 + 4;
+    const int64_t grid = std::min<int64_t>(n_chunks, int64_t(n_cu_));
+    // dense rows: 16-lane walkers; sparse rows: 8-lane walkers (profiles/r01: dense/, batch/)
+    auto kern = dense_mode_ ? k_acc_batch<4, 16, true> : k_acc_batch<4, 8, false>;
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     kern<<<unsigned(grid), kAccThreads, lds, s>>>(chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), desc, arena, M, db,
                                                   W, part, col_.as<int32_t>(), cnt_.as<uint32_t>(),
@@ -2281,14 +1950,6 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
                                                   dense_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
-    if (xmode_ == 64) {  // phase times of k_acc_batch (experiments)
-      int64_t ph[5];
-      COOC_HIP_TRY(hipMemcpyAsync(ph, split_sum_.as<int64_t>() + n_split + 1, sizeof(ph), hipMemcpyDeviceToHost, s));
-      COOC_HIP_TRY(hipStreamSynchronize(s));
-      fprintf(stderr, "[k_acc_batch phases] chunks %lld grid %lld  walk %.1f  sum+fetch %.1f  out %.1f  barrier %.1f us per WG\n",
-              (long long)ph[4], (long long)grid, ph[0] / 100.0 / grid, ph[1] / 100.0 / grid, ph[2] / 100.0 / grid,
-              ph[3] / 100.0 / grid);
-    }
     if (dense && n_split > 0) {
       k_dense_split_check<<<unsigned(std::min<int64_t>(n_split, 4 * int64_t(n_cu_))), kAccThreads, 0, s>>>(
           split_row_.as<int32_t>(), tot, M, dense_.as<uint32_t>(), split_sum_.as<int64_t>(), row_nnz_.as<int32_t>());
@@ -2296,10 +1957,9 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
     } else if (n_split > 0) {
       const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
       k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(
-          tot, split_row_.as<int32_t>(), M, 0, staging_.as<uint32_t>(), row_base_.as<int64_t>(),
+          tot, split_row_.as<int32_t>(), M, staging_.as<uint32_t>(), row_base_.as<int64_t>(),
           row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(), split_sum_.as<int64_t>(),
-          reinterpret_cast<int64_t *>(&tot->err), bump_.as<unsigned long long>(), bump_cap_,
-          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), 1, 0);
+          reinterpret_cast<int64_t *>(&tot->err), bump_.as<unsigned long long>(), bump_cap_);
       COOC_HIP_TRY(hipGetLastError());
     }
   } else if (timer && timer->enabled) {

@@ -36,8 +36,7 @@ Status cooc_ctx::init(const cooc_config &c) {
   COOC_HIP_TRY(hipEventCreate(&timer.acc_end));
   COOC_TRY(counter.init(c.n_items));
   counter.set_output_layout((c.flags & COOC_FLAG_OUTPUT_DENSE) ? 2 : (c.flags & COOC_FLAG_OUTPUT_CSR) ? 1 : 0);
-  const char *env = getenv("COOC_BATCH");  // COOC_BATCH=0: the general planner for every context (A/B)
-  counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0 || (env && env[0] == '0'));
+  counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0);
   return Status::Ok();
 }
 
@@ -64,9 +63,28 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   cooc::CountResult r;
   if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
+  } else if (counter.sparse()) {
+    COOC_TRY(counter.run_sparse(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
   } else {
     COOC_TRY(count_general(n_users, d_user_ptr, d_items, n_interactions, s, &r));
   }
+  return finish_batch(r, s, out);
+}
+
+Status cooc_ctx::count_device_owned(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                                    int64_t n_interactions, const int32_t *d_owner, int32_t part,
+                                    const int64_t *d_item_counts, int64_t n_total, hipStream_t s,
+                                    cooc_device_result *out) {
+  if (!counter.sparse())
+    return Status{COOC_ERR_ARG, "cooc_count_device_owned needs n_items >= " + std::to_string(cooc::Counter::kBatchMaxItems) +
+                                    " (smaller universes shard with cooc_shard_plan / cooc_shard_count)"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  have_batch = false;
+  batch_topk = 0;
+  COOC_TRY(apply_user_cut(n_users, &d_user_ptr, &d_items, &n_interactions, s));
+  cooc::CountResult r;
+  COOC_TRY(counter.run_sparse(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr,
+                              d_owner, part, d_item_counts, n_total));
   return finish_batch(r, s, out);
 }
 
@@ -117,8 +135,7 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
     nnz = h.nnz_total;
     err = h.err;
   }
-  static const bool x_mode = getenv("COOC_ACC_X") && atoi(getenv("COOC_ACC_X")) != 0;  // experiments: counts invalid
-  if ((err & 2) && !x_mode) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  if (err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
   if (err & 4) return Status{COOC_ERR_OOM, "the sparse output region is exhausted"};
   out->n_items = cfg.n_items;
   out->nnz = nnz;

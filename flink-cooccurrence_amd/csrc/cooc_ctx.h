@@ -98,6 +98,10 @@ struct cooc_ctx {
 
   cooc::Status count_device(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
                             hipStream_t s, cooc_device_result *out);
+  cooc::Status count_device_owned(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                                  int64_t n_interactions, const int32_t *d_owner, int32_t part,
+                                  const int64_t *d_item_counts, int64_t n_total, hipStream_t s,
+                                  cooc_device_result *out);
   // user_cut > 0: replaces the CSR by its capped copy (b_cut_*); no-op otherwise
   cooc::Status apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, const int32_t **d_items,
                               int64_t *n_interactions, hipStream_t s);

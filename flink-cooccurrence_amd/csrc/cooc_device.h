@@ -91,6 +91,10 @@ struct PlanTotals {
   int64_t sum_lpl;    // sum_u n_u * pad8(n_u): padded partner ids read
   int64_t max_len;    // longest history
   int64_t n_long;     // histories longer than kFillThread (filled by a workgroup each)
+  // large-universe path (run_sparse)
+  int64_t est_nnz;       // expected distinct keys (planner estimate, sizes the output region)
+  int64_t n_split_work;  // work items of the split rows
+  int64_t n_active;      // rows with at least one contribution
 };
 
 // Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
@@ -128,7 +132,19 @@ class Counter {
   // CSR as run().  Synchronises `stream` once (to size chunks and the output region).
   Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                    CountResult *out, KernelTimer *timer = nullptr);
-  bool batch_ok() const { return T_ == 1 && M_ < kBatchMaxItems && !general_only_; }
+  bool batch_ok() const { return M_ < kBatchMaxItems && !general_only_; }
+  // n_items >= kBatchMaxItems: one window over empty histories through the large-universe path
+  // (cooc_sparse.hip: per-row workgroups, LDS hash / dense-tile chunks, split staging rows).  Same
+  // padded CSR result as run().  Synchronises `stream` twice (plan totals, output-region check).
+  // owner != NULL (multi-GPU): only the rows a with owner[a] == part are counted (over every user
+  // given), and the planner's column frequencies come from freq (int64[n_items], n_freq in total:
+  // the global log's item counts); other rows come out empty.
+  Status run_sparse(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
+                    CountResult *out, KernelTimer *timer = nullptr, const int32_t *owner = nullptr,
+                    int32_t part = 0, const int64_t *freq = nullptr, int64_t n_freq = 0);
+  bool sparse() const { return M_ >= kBatchMaxItems; }
+  // run() (the streaming general planner) keeps one LDS row per chunk: n_items <= kMaxGeneralItems
+  static constexpr int32_t kMaxGeneralItems = 40704;
   // A streaming window (resident histories) through the batch planner and k_acc_batch; needs
   // batch_ok().  Same padded CSR result as run().  Synchronises `stream` once.
   Status run_window(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
@@ -163,12 +179,12 @@ class Counter {
   const int64_t *last_rowsum() const { return rowsum_.as<int64_t>(); }
   const int32_t *last_row_nnz() const { return row_nnz_.as<int32_t>(); }
   const int64_t *last_row_base() const { return row_base_.as<int64_t>(); }
-  const int32_t *last_col() const { return bump_mode_ ? col2_.as<int32_t>() : col_.as<int32_t>(); }
-  const uint32_t *last_cnt() const { return bump_mode_ ? cnt2_.as<uint32_t>() : cnt_.as<uint32_t>(); }
+  const int32_t *last_col() const { return col_.as<int32_t>(); }
+  const uint32_t *last_cnt() const { return cnt_.as<uint32_t>(); }
   int32_t n_items() const { return M_; }
 
  private:
-  Status run_tile(const uint16_t *arena, int32_t col_off, int64_t n, hipStream_t s, KernelTimer *timer);
+  Status run_tile(const uint16_t *arena, int64_t n, hipStream_t s, KernelTimer *timer);
   Status plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
                     uint64_t *desc, uint16_t *arena, int64_t arena_cap, const int32_t *old = nullptr,
                     const int64_t *hoff = nullptr);
@@ -177,37 +193,28 @@ class Counter {
                          hipStream_t s, CountResult *out, KernelTimer *timer);
 
   int32_t M_ = 0;
-  int32_t T_ = 1;    // column tiles (1 when the whole row fits one LDS row)
-  int32_t tw_ = 0;   // column tile width
-  int db_ = 0;       // segment descriptors staged per batch
-  int unroll_ = 16;  // COOC_ACC_UNROLL: partner loads in flight per lane (4, 8, 16, 32)
+  int db_ = 0;       // segment descriptors staged per batch (general planner)
   int n_cu_ = 256;
   // workspace
   DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
   DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
-  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_, tb_, chunks2_, ckeys_, cidx_;
-  int chunk_order_ = 0;  // COOC_CHUNK_ORDER=1: j-major chunk queue (A/B)
-  bool bump_mode_ = false;  // column-tiled runs: exact-size (row, tile) segments + final gather
-  int64_t bump_cap_ = 0;
-  DevBuf bump_, seg_off_, seg_nnz_, col2_, cnt2_;
-  bool vec_ = false, vec_allowed_ = true;  // 16-B partner-id loads over a padded arena (batch, one tile)
-  int vstride_ = 64;                       // COOC_ACC_VSTRIDE: lanes per walker of the VEC path (8, 16, 32, 64)
-  int xmode_ = 0;                          // COOC_ACC_X: experiment modes of k_accumulate2 (bench only)
-  int vunroll_ = 4;                        // COOC_ACC_VUNROLL: 16-B loads in flight per lane (2, 4, 8)
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_;
+  int64_t bump_cap_ = 0;    // k_acc_batch sparse output: entries in the bump region
+  DevBuf bump_, seg_off_;  // seg_off_: sharded records, per (source, owned row) segment offsets
+  bool vec_ = false;        // general planner: 16-B partner-id loads over a padded arena (one-window batch)
   DevBuf plen_, poff_, vpre_;
   DevBuf bh_, uidx_, long_, rcnt_, desc_;  // batch planner: block histograms, user of each interaction,
                                            // long lists, row counts, descriptors
-  int bstride_ = 8, bunroll_ = 4;
-  int store_mode_ = 1;                // COOC_ACC_STORE: output stores 1 plain, 2 sc1, 3 nt (A/B)
   int output_pref_ = 0;               // set_output_layout
   bool dense_mode_ = false;           // the last run's output is dense_
   DevBuf dense_, send_, witems_;
+  // large-universe path: tile-grouped arena, tile starts, per-row work and plan, estimates, queue
+  DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_;
   bool general_only_ = false;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
-  int64_t chunk_work_ = 0;            // COOC_CHUNK_WORK: pairs per chunk of the batch planner (A/B)
-  int acc_wgs_ = 1;                  // COOC_ACC_WGS: k_acc_batch workgroups launched per CU
+  static constexpr int64_t chunk_work_ = int64_t(1) << 22;  // pairs per chunk of the batch planner
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
 

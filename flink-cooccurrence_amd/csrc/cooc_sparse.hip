@@ -1,0 +1,1290 @@
+// cooc_sparse.hip — one window over empty histories for LARGE item universes (n_items >= 40,320,
+// the C3 / C5 configs: 1e6 items), on gfx950.
+//
+// Same semantics as the batch path (cooc_count.hip): NonSampledUserInteractionCounter...java:113-165
+// expanded from empty histories, reduced per row like ItemRowAggregator.java:26-31
+// (Int2ShortOpenHashMap.addTo, exact uint32 here) and RowSumAggregator.java:25-27:
+//   C[a, b] = sum_u #{ordered position pairs (p != q) : x_p = a, x_q = b},  rowsum[a] = sum_b C[a, b].
+// A row a is the sum of the lists of the users that hold a (one "contribution" per interaction
+// (u, a)), minus 1 at column a per contribution (the pair of a position with itself).
+//
+// At n_items = 1e6 a row cannot live in one LDS row (160 KB = 40K counters), and most rows are
+// sparse: under Zipf(1) the row of an item of rank r holds ~W_1 / r pairs over up to 1e6 columns.
+// The work unit is therefore a whole ROW, taken by one persistent workgroup per CU (heaviest rows
+// first), which walks the row's column range as a sequence of CHUNKS and appends each chunk's
+// entries, in column order, to the row's contiguous output (no gather pass):
+//   * hash chunk  — a range of column tiles whose expected distinct keys fit an LDS open-addressing
+//                   table (keys + counts, 1K..16K slots, the Int2ShortOpenHashMap of
+//                   ItemRowAggregator.java:21-31 in LDS).  Sorted output without a sort: the keys'
+//                   32-column blocks are ranked through a bitmap (L1) and per-block 32-bit masks, and
+//                   an entry's slot is its block's base + the popcount of its mask below it.  A table
+//                   that overflows (more distinct keys than expected) is redone with a 4x table, and
+//                   at 16K slots as dense tiles.
+//   * dense chunk — one column tile of 32,768 columns as uint32 LDS counters (one ds_add per pair),
+//                   compacted in column order.
+// The chunk plan of a row comes from its pair work W_a (exact) and the expected distinct keys per
+// tile, E[d_t | W] = sum_{b in t} 1 - exp(-W f_b / N) (f_b = global frequency of b), tabulated per
+// tile for W = 2^(k/2).  Per-user lists are regrouped by tile once (tb[u][t] = first position of
+// tile t in u's list), so a tile range of a user's list is one contiguous segment.
+// The few rows above kSplitWork pairs (the hottest items) are split into (row, tile, contribution
+// range) work items that add into a dense uint32 staging row in HBM; a finalize kernel compacts
+// each staging row (with the uint32 overflow check: sum of the counts == the closed-form row sum).
+//
+// HBM layout: tarena uint32[N] (tile-grouped user lists), tb int32[U x (T+1)], contributions
+// (item-sorted user indices) uint32[N], epre int64[N+1] (prefix of the contributions' list
+// lengths), per-row plan (W, two 64-bit tile masks), output = padded CSR (row_base, row_nnz, col,
+// cnt) over per-workgroup slabs of a bump-allocated region.
+#include <hipcub/hipcub.hpp>
+
+#include "cooc_device.h"
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include <unistd.h>
+#ifdef COOC_SP_TRACE
+#define SPT(msg) do { hipStreamSynchronize(s); fprintf(stderr, "[sp] %s\n", msg); } while (0)
+#else
+#define SPT(msg) do {} while (0)
+#endif
+
+namespace cooc {
+
+namespace {
+
+constexpr int kSpThreads = 1024;
+constexpr int kSpWaves = kSpThreads / 64;
+constexpr int kTW = 32768;  // dense tile width (uint32 LDS counters: 128 KB)
+constexpr int kTShift = 15;
+constexpr int kSpMaxTiles = 64;                        // per-row plans are 64-bit tile masks
+constexpr int kHashMax = 8192;                        // slots: keys + counts = the dense tile's 128 KB
+constexpr int kHashMin = 1024;                         // one slot per thread at least
+constexpr int kHashMaxTiles = 32;                      // a hash chunk spans <= 2^20 columns ...
+constexpr int kL1Words = kHashMaxTiles * kTW / 1024;   // ... so its block bitmap is <= 1024 words
+constexpr int kSpDb = 512;                             // contribution descriptors per batch
+constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
+constexpr int kSpU = 4;                                // partner loads in flight per lane
+constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
+constexpr int64_t kSplitWork = int64_t(1) << 25;       // rows above this pair work are split
+constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
+constexpr float kHashFill = 0.5f * kHashMax;           // expected distinct keys per hash chunk
+constexpr float kDensePairs = 65536.f;                 // a tile with more expected pairs is dense
+constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + 256 * 4;
+
+struct SpWork {
+  int32_t row;
+  int32_t tile;  // < 0: the whole row (chunk plan from pstart / pdense); else a split work item
+  int32_t sub;   // contribution share sub of nsub
+  int32_t nsub;
+};
+
+struct SpArgs {
+  const SpWork *queue;
+  PlanTotals *tot;
+  int32_t *qctr;
+  const uint32_t *vals;     // contributions: user index, item-sorted
+  const int64_t *row_ptr;   // [M + 1] into vals
+  const int64_t *up;        // [U + 1] user_ptr
+  const int32_t *tb;        // [U x (T + 1)] tile starts inside each user's list
+  const uint32_t *tarena;   // tile-grouped lists, user u at up[u]
+  const int64_t *row_w;     // [M] pair work W_a = sum of the contributions' list lengths
+  const uint64_t *pstart;   // [M] bit t: a chunk starts at tile t
+  const uint64_t *pdense;   // [M] bit t: tile t is a dense chunk
+  const float *est;         // [T x kEstK] expected distinct keys per tile
+  uint32_t *staging;        // [n_split x M]
+  const int32_t *split_slot;
+  int32_t *col_out;
+  uint32_t *cnt_out;
+  unsigned long long *bump;
+  int64_t cap;
+  int64_t slab;
+  int64_t *row_base;
+  int32_t *row_nnz;
+  int32_t M, T;
+  unsigned long long *prog;  // COOC_SP_TRACE: per-workgroup progress in pinned host memory
+  int64_t n_contrib, n_users, n_arena;
+};
+
+#ifdef COOC_SP_TRACE
+#define PROG(A, k, v) do { if (threadIdx.x == 0) __hip_atomic_store((A).prog + blockIdx.x * 64 + (k), (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#define WPROG(A, v) do { if ((threadIdx.x & 63) == 0) __hip_atomic_store((A).prog + blockIdx.x * 64 + 16 + (threadIdx.x >> 6), (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#define BCHK(A, cond, bit) ((cond) ? true : (atomicOr((A).prog + 2047, (unsigned long long)(bit)), false))
+#define TR(A, v) do { if (threadIdx.x == 0 || threadIdx.x == 64) { unsigned long long *q_ = (A).prog + 1024 + (threadIdx.x ? 512 : 0); unsigned long long n_ = __hip_atomic_load(q_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); __hip_atomic_store(q_ + 1 + (n_ & 255), (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); __hip_atomic_store(q_, n_ + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } } while (0)
+#else
+#define TR(A, v) do {} while (0)
+#define BCHK(A, cond, bit) true
+#define PROG(A, k, v) do {} while (0)
+#define WPROG(A, v) do {} while (0)
+#endif
+
+// Values every thread of the workgroup holds identically (read from LDS after a barrier): made
+// explicitly uniform so that the branches on them are scalar and no barrier sits in exec-masked code.
+__device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline int32_t uni(int32_t v) { return int32_t(__builtin_amdgcn_readfirstlane(uint32_t(v))); }
+__device__ inline int64_t uni(int64_t v) {
+  const uint64_t u = uint64_t(v);
+  return int64_t((uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(u >> 32))) << 32) |
+                 uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(u))));
+}
+
+__device__ inline uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan (kSpThreads threads); *total = the block sum.  Two barriers.
+__device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t *total, uint32_t *s_wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(x);
+  if (lane == 63) s_wtot[wave] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kSpWaves; w++) {
+    const uint32_t v = s_wtot[w];
+    pre += w < wave ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  *total = uni(tot);
+  return pre + inc - x;
+}
+
+__device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t *s_red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int w = 0; w < kSpWaves; w++) t += s_red[w];
+  __syncthreads();
+  return t;
+}
+
+// E[distinct keys of tile t | pair work W], interpolated in log2(W) between table points.
+__device__ inline float est_distinct(const float *est, int t, int64_t W) {
+  if (W <= 0) return 0.f;
+  const float x = 2.f * log2f(float(W));
+  int k = int(x);
+  if (k >= kEstK - 1) return est[t * kEstK + kEstK - 1];
+  const float f = x - float(k);
+  const float lo = est[t * kEstK + k], hi = est[t * kEstK + k + 1];
+  return lo + f * (hi - lo);
+}
+
+// ---- planner kernels ------------------------------------------------------------------------------
+// One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
+// item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and regroups the list by
+// column tile: tarena[up[u] + ...] = the list tile by tile, tb[u][t] = offset of tile t (tb[u][T] = n_u).
+__global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
+                                                      const int32_t *__restrict__ items, int32_t M, int32_t T,
+                                                      uint32_t *__restrict__ tarena, int32_t *__restrict__ tb,
+                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                      const int32_t *__restrict__ owner, int32_t part,
+                                                      int32_t *__restrict__ ownc, PlanTotals *__restrict__ tot) {
+  __shared__ int32_t cur[4][kSpMaxTiles + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t *c = cur[wave];
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  bool bad = false;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up[j];
+    const int32_t n = int32_t(up[j + 1] - s);
+    for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int32_t mine = 0;
+    for (int32_t p = lane; p < n; p += 64) {
+      int32_t it = items[s + p];
+      if (uint32_t(it) >= uint32_t(M)) {
+        bad = true;
+        it = 0;
+      }
+      atomicAdd(&c[it >> kTShift], 1);
+      if (!owner) {
+        keys[s + p] = uint32_t(it);
+        vals[s + p] = uint32_t(j);
+      } else {
+        mine += owner[it] == part;
+      }
+    }
+    if (owner) {
+      for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+      if (lane == 0) ownc[j] = mine;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      int32_t run = 0;
+      for (int32_t t = 0; t <= T; t++) {
+        const int32_t x = c[t];
+        c[t] = run;
+        run += x;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int32_t p = lane; p < n; p += 64) {
+      int32_t it = items[s + p];
+      if (uint32_t(it) >= uint32_t(M)) it = 0;
+      tarena[s + atomicAdd(&c[it >> kTShift], 1)] = uint32_t(it);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
+}
+
+// Owner-filtered contributions (multi-GPU: this part's rows only): user j's owned interactions at
+// ownoff[j] (exclusive prefix of the per-user counts), in list order.  One wave per user.
+__global__ __launch_bounds__(256) void k_sp_owned_contribs(int64_t U, const int64_t *__restrict__ up,
+                                                           const int32_t *__restrict__ items, int32_t M,
+                                                           const int32_t *__restrict__ owner, int32_t part,
+                                                           const int64_t *__restrict__ ownoff,
+                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up[j];
+    const int32_t n = int32_t(up[j + 1] - s);
+    int64_t o = ownoff[j];
+    for (int32_t p0 = 0; p0 < n; p0 += 64) {
+      const int32_t p = p0 + lane;
+      int32_t it = p < n ? items[s + p] : -1;
+      const bool m = p < n && uint32_t(it) < uint32_t(M) && owner[it] == part;
+      const uint64_t bal = __ballot(m);
+      if (m) {
+        keys[o + __popcll(bal & lt)] = uint32_t(it);
+        vals[o + __popcll(bal & lt)] = uint32_t(j);
+      }
+      o += __popcll(bal);
+    }
+  }
+}
+
+struct WidenCount {
+  __host__ __device__ int64_t operator()(int32_t v) const { return int64_t(v); }
+};
+
+__global__ void k_sp_row_ptr(const uint32_t *__restrict__ keys, int64_t n, int32_t M, int64_t *__restrict__ row_ptr) {
+  const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (a > M) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < uint32_t(a)) lo = mid + 1; else hi = mid;
+  }
+  row_ptr[a] = lo;
+}
+
+struct UserLen {  // list length of a contribution's user
+  const int64_t *up;
+  __host__ __device__ int64_t operator()(uint32_t u) const { return up[u + 1] - up[u]; }
+};
+
+// est[t][k] = sum over the columns b of tile t of 1 - exp(-2^(k/2) f_b / N); gmass[t] = tile t's
+// share of the interactions.  One block per (tile, k).
+__global__ __launch_bounds__(256) void k_sp_est(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ freq,
+                                                int32_t M, int64_t n, float *__restrict__ est, float *__restrict__ gmass) {
+  __shared__ double s_mass[4];
+  __shared__ float s[4];
+  const int t = blockIdx.x, k = blockIdx.y;
+  const int32_t b0 = t * kTW, b1 = min(M, b0 + kTW);
+  const float scale = exp2f(0.5f * float(k)) / float(n);
+  float acc = 0.f;
+  double mass = 0.0;
+  for (int32_t b = b0 + threadIdx.x; b < b1; b += 256) {
+    const int64_t fi = freq ? freq[b] : row_ptr[b + 1] - row_ptr[b];
+    const float f = float(fi);
+    mass += double(fi);
+    if (f > 0.f) acc += -expm1f(-f * scale);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_xor(acc, o, 64);
+    mass += __shfl_xor(mass, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s[threadIdx.x >> 6] = acc;
+    s_mass[threadIdx.x >> 6] = mass;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    est[t * kEstK + k] = s[0] + s[1] + s[2] + s[3];
+    if (k == 0) gmass[t] = float((s_mass[0] + s_mass[1] + s_mass[2] + s_mass[3]) / double(n));
+  }
+}
+
+// Per row: pair work W_a (exact), row sum W_a - c_a (closed form), and the chunk plan.
+__global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int64_t *__restrict__ row_ptr,
+                                                 const int64_t *__restrict__ epre, const float *__restrict__ est,
+                                                 const float *__restrict__ gmass, int64_t *__restrict__ rowsum,
+                                                 int64_t *__restrict__ row_w, uint64_t *__restrict__ pstart,
+                                                 uint64_t *__restrict__ pdense, uint64_t *__restrict__ skey,
+                                                 int32_t *__restrict__ order, int32_t *__restrict__ nwork,
+                                                 int32_t *__restrict__ row_nnz, int64_t *__restrict__ row_base,
+                                                 PlanTotals *__restrict__ tot) {
+  __shared__ uint64_t s_red[4][4];
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0;
+  if (a < M) {
+    const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
+    const int64_t W = epre[k0 + c] - epre[k0];
+    rowsum[a] = W - c;
+    row_w[a] = W;
+    row_nnz[a] = 0;
+    row_base[a] = 0;
+    order[a] = a;
+    skey[a] = uint64_t(W);
+    uint64_t st = 0, dn = 0;
+    int32_t nw = 0;
+    if (c > 0) {
+      n_active = 1;
+      bound = uint64_t(min<int64_t>(W - c, M));
+      float e_tot = 0.f;
+      if (W > kSplitWork) {
+        n_split = 1;
+        for (int t = 0; t < T; t++) {
+          e_tot += est_distinct(est, t, W);
+          const float g = gmass[t];
+          if (g > 0.f) nw += max(1, int32_t(ceilf(float(W) * g / float(kSubWork))));
+        }
+        split_work = uint64_t(nw);
+      } else {
+        float cur = 0.f;
+        int n_in = 0;
+        bool open = false;
+        for (int t = 0; t < T; t++) {
+          const float d = est_distinct(est, t, W);
+          const float e = float(W) * gmass[t];
+          e_tot += d;
+          if (d > kHashFill || e > kDensePairs) {
+            st |= uint64_t(1) << t;
+            dn |= uint64_t(1) << t;
+            open = false;
+          } else {
+            if (!open || cur + d > kHashFill || n_in == kHashMaxTiles) {
+              st |= uint64_t(1) << t;
+              open = true;
+              cur = 0.f;
+              n_in = 0;
+            }
+            cur += d;
+            n_in++;
+          }
+        }
+      }
+      est_sum = uint64_t(e_tot) + 1;
+    }
+    pstart[a] = st;
+    pdense[a] = dn;
+    nwork[a] = nw;
+  }
+  uint64_t v[4] = {est_sum, bound, n_split, split_work};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = 0; i < 4; i++) {
+    for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);
+    if (lane == 0) s_red[i][w] = v[i];
+  }
+  uint64_t act = n_active;
+  for (int o = 32; o > 0; o >>= 1) act += __shfl_xor(act, o, 64);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t r[4];
+    for (int i = 0; i < 4; i++) r[i] = s_red[i][0] + s_red[i][1] + s_red[i][2] + s_red[i][3];
+    if (r[0]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->est_nnz), (unsigned long long)r[0]);
+    if (r[1]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->cap_total), (unsigned long long)r[1]);
+    if (r[2]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_split), (unsigned long long)r[2]);
+    if (r[3]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_split_work), (unsigned long long)r[3]);
+  }
+  if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
+}
+
+__global__ void k_sp_gather_nwork(const int32_t *__restrict__ order, const int32_t *__restrict__ nwork, int32_t M,
+                                  int32_t *__restrict__ out) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < M) out[r] = nwork[order[r]];
+}
+
+// Work queue: the split rows' work items (they are the heaviest rows, so the first n_split rows of
+// the W-descending order), then every other row with contributions, heaviest first.
+__global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__restrict__ skey,
+                           const int32_t *__restrict__ wbase, const float *__restrict__ gmass, int32_t M, int32_t T,
+                           PlanTotals *__restrict__ tot, SpWork *__restrict__ queue, int32_t *__restrict__ split_slot,
+                           int32_t *__restrict__ split_row) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= M) return;
+  const int64_t n_split = tot->n_split, n_split_work = tot->n_split_work;
+  const int32_t a = order[r];
+  const int64_t W = int64_t(skey[r]);
+  if (W <= 0) return;
+  if (r < n_split) {
+    split_slot[a] = r;
+    split_row[r] = a;
+    int64_t q = wbase[r];
+    for (int t = 0; t < T; t++) {
+      const float g = gmass[t];
+      if (g <= 0.f) continue;
+      const int32_t ns = max(1, int32_t(ceilf(float(W) * g / float(kSubWork))));
+      for (int32_t s = 0; s < ns; s++) queue[q++] = SpWork{a, t, s, ns};
+    }
+  } else {
+    queue[n_split_work + (r - n_split)] = SpWork{a, -1, 0, 0};
+  }
+}
+
+__global__ void k_sp_totals(PlanTotals *__restrict__ tot, const int64_t *__restrict__ epre, int64_t n,
+                            int32_t *__restrict__ qctr) {
+  tot->n_chunks = tot->n_split_work + (tot->n_active - tot->n_split);
+  tot->work_total = epre[n];
+  qctr[0] = 0;
+}
+
+// ---- the accumulate kernel --------------------------------------------------------------------------
+struct SpShared {
+  uint32_t *R;       // [kTW] dense counters | hash keys [0, H) + counts [kHashMax, kHashMax + H)
+  uint32_t *L1;      // [kL1Words] hash compaction: one bit per 32-column block
+  uint32_t *L1pre;   // [kL1Words] its exclusive popcount prefix
+  int64_t *seg;      // [kSpDb] segment start - virtual start
+  uint32_t *vst;     // [kSpDb + 1] virtual starts
+  int32_t *qstart;   // [256] first segment of every walker
+};
+
+struct SpStatic {
+  uint32_t wtot[kSpWaves];
+  uint64_t red[kSpWaves];
+  int32_t work;
+  uint32_t flag, claims;
+  int64_t slab_cur, slab_end, row_begin, row_n, pos, copy_from, copy_n;
+  float dt[kSpMaxTiles];
+};
+
+// Insert one partner id into the LDS table (keys store id + 1; 0 = empty).  Linear probing from a
+// multiplicative hash; raises *flag when the probe budget or the fill limit is exceeded.
+__device__ inline void sp_hash_insert(uint32_t *keys, uint32_t *cnts, uint32_t id, uint32_t hshift, uint32_t hmask,
+                                      uint32_t fill_limit, SpStatic &S_) {
+  const uint32_t k = id + 1u;
+  uint32_t h = (id * 0x9E3779B1u) >> hshift;
+  for (int p = 0; p < kMaxProbe; p++) {
+    uint32_t cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0u) {
+      cur = atomicCAS(keys + h, 0u, k);
+      if (cur == 0u) {
+        atomicAdd(cnts + h, 1u);
+        if (atomicAdd(&S_.claims, 1u) >= fill_limit) S_.flag = 1u;
+        return;
+      }
+    }
+    if (cur == k) {
+      atomicAdd(cnts + h, 1u);
+      return;
+    }
+    h = (h + 1u) & hmask;
+  }
+  S_.flag = 1u;
+}
+
+struct WalkOp {
+  int mode;  // 0: dense counters R[id - c0]; 1: hash insert
+  uint32_t c0, hshift, hmask, limit;
+};
+
+__device__ inline void sp_apply(const SpShared &L, SpStatic &S_, const WalkOp &op, uint32_t id) {
+  if (op.mode == 0)
+    atomicAdd(&L.R[id - op.c0], 1u);
+  else
+    sp_hash_insert(L.R, L.R + kHashMax, id, op.hshift, op.hmask, op.limit, S_);
+}
+
+// Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
+// applying op to every id (dense: one LDS counter add; hash: one table insert).  Batches of kSpDb descriptors are block-scanned into virtual starts;
+// walkers of S lanes (S from the mean segment length) own equal contiguous shares of the batch's
+// virtual range and step S ids at a time, kSpU loads in flight per lane.  Returns early (uniformly)
+// when *flag is raised.
+__device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0, int t1,
+                               bool full, const WalkOp &op) {
+  const int tid = threadIdx.x;
+  const uint32_t *__restrict__ ar = A.tarena;
+  for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
+    const int nb = int(min<int64_t>(kSpDb, k1 - b0));
+    uint32_t len = 0;
+    int64_t start = 0;
+    if (tid < nb) {
+      const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] : 0u;
+      const int64_t base = BCHK(A, u < A.n_users, 2) ? A.up[u] : 0;
+      if (full) {
+        len = uint32_t(A.up[u + 1] - base);
+        start = base;
+      } else {
+        const int32_t *tbu = A.tb + int64_t(u) * (A.T + 1);
+        const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
+        const int32_t s0 = okt ? tbu[t0] : 0;
+        len = okt ? uint32_t(tbu[t1] - s0) : 0u;
+        start = base + s0;
+      }
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
+    if (total == 0) continue;  // uniform (scalar branch): no barrier is skipped by part of the block
+    const uint32_t mean = total / uint32_t(nb);
+    const uint32_t S = mean >= 48 ? 64u : mean >= 12 ? 16u : 4u;
+    const uint32_t nW = kSpThreads / S;
+    if (tid < nb) {
+      L.vst[tid] = ex;
+      L.seg[tid] = start - int64_t(ex);
+      if (len) {
+        const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
+        const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
+        for (uint32_t q = q0; q < q1 && q < nW; q++) L.qstart[q] = tid;
+      }
+    }
+    if (tid == 0) L.vst[nb] = total;
+    __syncthreads();
+    const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
+    const uint32_t lo = uint32_t(uint64_t(total) * q / nW), hi = uint32_t(uint64_t(total) * (q + 1) / nW);
+    uint32_t g = lo + ql;
+    if (g < hi) {
+      int32_t cur = L.qstart[q];
+      uint32_t next = L.vst[cur + 1];
+      int64_t base = L.seg[cur];
+      uint32_t v[kSpU] = {};
+      bool ok[kSpU];
+#pragma unroll
+      for (int k = 0; k < kSpU; k++) {
+        const uint32_t gk = g + S * k;
+        ok[k] = gk < hi;
+        if (ok[k]) {
+          while (gk >= next) {
+            cur++;
+            next = L.vst[cur + 1];
+            base = L.seg[cur];
+          }
+          v[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_arena, 8) ? ar[base + gk] : 0u;
+        }
+      }
+      for (; g < hi; g += S * kSpU) {
+        uint32_t vn[kSpU] = {};
+        bool okn[kSpU];
+#pragma unroll
+        for (int k = 0; k < kSpU; k++) {
+          const uint32_t gk = g + S * (kSpU + k);
+          okn[k] = gk < hi;
+          if (okn[k]) {
+            while (gk >= next) {
+              cur++;
+              next = L.vst[cur + 1];
+              base = L.seg[cur];
+            }
+            vn[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_arena, 16) ? ar[base + gk] : 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kSpU; k++)
+          if (ok[k]) sp_apply(L, S_, op, v[k]);
+#pragma unroll
+        for (int k = 0; k < kSpU; k++) {
+          v[k] = vn[k];
+          ok[k] = okn[k];
+        }
+      }
+    }
+    __syncthreads();
+    if (uni(S_.flag)) break;
+  }
+}
+
+// Output space for n more entries of the current row (thread-uniform call).  Moves the row's
+// entries so far to a new slab when the workgroup's slab is exhausted.  Returns the write position
+// (-1 when the output region is exhausted: the host reruns with a larger region).
+__device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    S_.copy_n = 0;
+    if (S_.slab_cur + n > S_.slab_end) {
+      const int64_t need = S_.row_n + n;
+      const int64_t take = max(A.slab, need);
+      int64_t b = int64_t(atomicAdd(A.bump, (unsigned long long)take));
+      if (b + take > A.cap) {
+        atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 4ull);
+        S_.pos = -1;
+      } else {
+        S_.copy_from = S_.row_begin;
+        S_.copy_n = S_.row_n;
+        S_.row_begin = b;
+        S_.slab_cur = b + S_.row_n;
+        S_.slab_end = b + take;
+        S_.pos = S_.slab_cur;
+        S_.slab_cur += n;
+      }
+    } else {
+      S_.pos = S_.slab_cur;
+      S_.slab_cur += n;
+    }
+    if (S_.pos >= 0) S_.row_n += n;
+  }
+  __syncthreads();
+  const int64_t cn = uni(S_.copy_n);
+  if (cn > 0) {  // the row's earlier entries follow it to the new slab (rare)
+    const int64_t from = S_.copy_from, to = S_.row_begin;
+    for (int64_t i = tid; i < cn; i += kSpThreads) {
+      if (BCHK(A, to + i < A.cap && from + i < A.cap && from >= 0, 32)) {
+        A.col_out[to + i] = A.col_out[from + i];
+        A.cnt_out[to + i] = A.cnt_out[from + i];
+      }
+    }
+  }
+  return uni(S_.pos);
+}
+
+// Column-order compaction of w dense counters (16-B aligned), appended to the row's output; the
+// counters are left zero.  Waves own 256-column-aligned ranges, 4 counters per lane.
+__device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t w, int32_t c0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t *row = L.R;
+  const int32_t per = ((w + kSpWaves - 1) / kSpWaves + 255) & ~255;
+  const int32_t lo = min(w, wave * per), hi = min(w, lo + per);
+  const uint4 *row4 = reinterpret_cast<const uint4 *>(row);
+  auto load = [&](int32_t b, uint32_t v[4]) {
+    if (b < hi) {
+      const uint4 q = row4[b >> 2];
+      v[0] = q.x;
+      v[1] = b + 1 < hi ? q.y : 0u;
+      v[2] = b + 2 < hi ? q.z : 0u;
+      v[3] = b + 3 < hi ? q.w : 0u;
+    } else {
+      v[0] = v[1] = v[2] = v[3] = 0u;
+    }
+  };
+  uint32_t cnt = 0;
+  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
+    uint32_t v[4];
+    load(b0 + 4 * lane, v);
+    cnt += (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) S_.wtot[wave] = cnt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int wv = 0; wv < kSpWaves; wv++) {
+    const uint32_t x = S_.wtot[wv];
+    off += wv < wave ? x : 0u;
+    tot += x;
+  }
+  const int64_t base = sp_reserve(A, S_, tot);  // (barrier: every wave has read wtot)
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
+    const int32_t b = b0 + 4 * lane;
+    uint32_t v[4];
+    load(b, v);
+    const uint32_t c = (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+    const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
+    const uint32_t pre = uint32_t(__popcll(m0 & lt_mask)) + 2u * uint32_t(__popcll(m1 & lt_mask)) +
+                         4u * uint32_t(__popcll(m2 & lt_mask));
+    if (c) {
+      int64_t pos = base + off + pre;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (!v[k]) continue;
+        if (base >= 0) {
+          if (BCHK(A, pos >= 0 && pos < A.cap, 64)) {
+            A.col_out[pos] = c0 + b + k;
+            A.cnt_out[pos] = v[k];
+          }
+        }
+        pos++;
+      }
+      if (b + 3 < hi) {
+        reinterpret_cast<uint4 *>(row)[b >> 2] = make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        for (int k = 0; k < 4 && b + k < hi; k++) row[b + k] = 0u;
+      }
+    }
+    off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2));
+  }
+  __syncthreads();
+}
+
+// Column-order compaction of the hash table (H slots) of the column range [c0, c1), appended to the
+// row's output; leaves the table, L1 and the scratch it uses zero.  Entries are kept in registers
+// (H / kSpThreads <= 16 per thread); their 32-column blocks are ranked through the L1 bitmap, every
+// block gets a 32-bit column mask (in the keys area) and a base (prefix of mask popcounts, in the
+// counts area); an entry goes to base + popcount(mask below its column).
+__device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t H, int32_t c0,
+                                       int32_t c1) {
+  const int tid = threadIdx.x;
+  uint32_t *keys = L.R, *cnts = L.R + kHashMax;
+  const int per = H / kSpThreads;
+  const int32_t nL1 = (c1 - c0 + 1023) >> 10;
+  uint32_t ek[kHashMax / kSpThreads], ec[kHashMax / kSpThreads], er[kHashMax / kSpThreads];
+#pragma unroll
+  for (int i = 0; i < kHashMax / kSpThreads; i++) {
+    ek[i] = ~0u;
+    ec[i] = 0u;
+    er[i] = 0u;
+    if (i < per) {
+      const int j = tid + i * kSpThreads;
+      const uint32_t k = keys[j], v = cnts[j];
+      keys[j] = 0u;
+      cnts[j] = 0u;
+      if (k && v) {
+        const uint32_t col = k - 1u - uint32_t(c0);
+        ek[i] = col;
+        ec[i] = v;
+        atomicOr(&L.L1[col >> 10], 1u << ((col >> 5) & 31u));
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t nblk;
+  {
+    const uint32_t x = tid < nL1 ? uint32_t(__popc(L.L1[tid])) : 0u;
+    const uint32_t p = block_excl_scan(x, &nblk, S_.wtot);
+    if (tid < nL1) L.L1pre[tid] = p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kHashMax / kSpThreads; i++) {
+    if (ek[i] == ~0u) continue;
+    const uint32_t col = ek[i], wd = col >> 10, bit = (col >> 5) & 31u;
+    const uint32_t r = L.L1pre[wd] + uint32_t(__popc(L.L1[wd] & ((1u << bit) - 1u)));
+    er[i] = r;
+    atomicOr(&keys[r], 1u << (col & 31u));
+  }
+  __syncthreads();
+  const uint32_t pb = (nblk + kSpThreads - 1) / kSpThreads;
+  const uint32_t r0 = min(nblk, uint32_t(tid) * pb), r1 = min(nblk, r0 + pb);
+  uint32_t local = 0;
+  for (uint32_t r = r0; r < r1; r++) local += uint32_t(__popc(keys[r]));
+  uint32_t ne;
+  uint32_t run = block_excl_scan(local, &ne, S_.wtot);
+  for (uint32_t r = r0; r < r1; r++) {
+    cnts[r] = run;
+    run += uint32_t(__popc(keys[r]));
+  }
+  const int64_t base = sp_reserve(A, S_, ne);  // (barrier: bases visible)
+  if (base >= 0) {
+#pragma unroll
+    for (int i = 0; i < kHashMax / kSpThreads; i++) {
+      if (ek[i] == ~0u) continue;
+      const uint32_t col = ek[i], r = er[i];
+      const int64_t pos = base + cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
+      if (BCHK(A, pos >= 0 && pos < A.cap, 128)) {
+        A.col_out[pos] = c0 + int32_t(col);
+        A.cnt_out[pos] = ec[i];
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < nblk; r += kSpThreads) {
+    keys[r] = 0u;
+    cnts[r] = 0u;
+  }
+  if (tid < nL1) L.L1[tid] = 0u;
+  __syncthreads();
+}
+
+// The workgroup loop.  A work item is a whole row (its chunks in column order, appended to the row's
+// contiguous output) or a split row's (tile, contribution share), added into the staging row.  One
+// code path for every chunk kind, so that the walk and the two compactions exist once.
+__global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ SpStatic S_;
+  SpShared L;
+  L.R = lds;
+  L.L1 = L.R + kTW;
+  L.L1pre = L.L1 + kL1Words;
+  L.seg = reinterpret_cast<int64_t *>(L.L1pre + kL1Words);
+  L.vst = reinterpret_cast<uint32_t *>(L.seg + kSpDb);
+  L.qstart = reinterpret_cast<int32_t *>(L.vst + kSpDb + 4);
+  const int tid = threadIdx.x;
+  for (int32_t i = tid; i < kTW + kL1Words; i += kSpThreads) L.R[i] = 0u;
+  if (tid == 0) {
+    S_.slab_cur = S_.slab_end = 0;
+    S_.flag = 0u;
+  }
+  const int64_t n_work = A.tot->n_chunks;
+  __syncthreads();
+  for (;;) {
+    if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
+    __syncthreads();
+    const int32_t w = uni(S_.work);
+    if (w >= n_work) break;
+    const SpWork it = A.queue[w];
+    const int32_t a = it.row;
+    const int64_t r0 = A.row_ptr[a], r1 = A.row_ptr[a + 1];
+    const bool split = it.tile >= 0;
+    int64_t k0 = r0, k1 = r1;
+    int t = 0, t_end = A.T;
+    uint64_t st = 0, dn = 0;
+    if (split) {  // tile `tile` of a share of the row's contributions
+      k0 = r0 + (r1 - r0) * it.sub / it.nsub;
+      k1 = r0 + (r1 - r0) * (it.sub + 1) / it.nsub;
+      t = it.tile;
+      t_end = t + 1;
+    } else {
+      const int64_t W = A.row_w[a];
+      st = A.pstart[a];
+      dn = A.pdense[a];
+      if (tid < A.T) S_.dt[tid] = est_distinct(A.est, tid, W);
+      if (tid == 0) {
+        S_.row_begin = S_.slab_cur;
+        S_.row_n = 0;
+      }
+      __syncthreads();  // dt[] is read by every thread below
+    }
+    int dense_until = split ? t_end : -1;  // tiles below it go dense (split items; hash overflow fallback)
+    int32_t H = 0;                         // 0: table size from the estimate
+    while (t < t_end) {
+      // ---- this chunk: tiles [t, t1), dense or hash
+      const bool dense = t < dense_until || ((dn >> t) & 1ull);
+      int t1 = t + 1;
+      if (!dense) {
+        const uint64_t rest = t + 1 < 64 ? st >> (t + 1) : 0ull;
+        t1 = rest ? min(t_end, t + __ffsll((long long)rest)) : t_end;
+        if (H == 0) {
+          float e = 0.f;
+          for (int x = t; x < t1; x++) e += S_.dt[x];
+          H = kHashMin;
+          while (H < kHashMax && float(H) < 2.f * e + 64.f) H <<= 1;
+          H = uni(H);
+        }
+      }
+      const int32_t c0 = t * kTW, c1 = min(A.M, t1 * kTW);
+      WalkOp op;
+      op.mode = dense ? 0 : 1;
+      op.c0 = uint32_t(c0);
+      const uint32_t lg = dense ? 0u : 31u - uint32_t(__clz(uint32_t(H)));
+      op.hshift = 32u - lg;
+      op.hmask = uint32_t(H) - 1u;
+      op.limit = uint32_t(H) - uint32_t(H) / 8u;
+      if (tid == 0) {
+        S_.flag = 0u;
+        S_.claims = 0u;
+      }
+      __syncthreads();
+      sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+      if (!dense && uni(S_.flag)) {
+        // overflow: clear the table; retry with a 4x table, at the largest size as dense tiles
+        for (int32_t j = tid; j < H; j += kSpThreads) {
+          L.R[j] = 0u;
+          L.R[kHashMax + j] = 0u;
+        }
+        if (H < kHashMax) {
+          H = min(kHashMax, H * 4);
+        } else {
+          dense_until = t1;
+          H = 0;
+        }
+        __syncthreads();  // every wave has read the flag before the retry resets it
+        continue;
+      }
+      const uint32_t self = uint32_t(k1 - k0);  // the -1 at column a per contribution (whole rows)
+      if (split) {
+        uint32_t *dst = A.staging + int64_t(A.split_slot[a]) * A.M + c0;
+        for (int32_t i = tid; i < c1 - c0; i += kSpThreads) {
+          const uint32_t v = L.R[i];
+          if (v) {
+            atomicAdd(dst + i, v);
+            L.R[i] = 0u;
+          }
+        }
+        __syncthreads();
+      } else if (dense) {
+        if (tid == 0 && a >= c0 && a < c1) L.R[a - c0] -= self;
+        __syncthreads();
+        sp_dense_compact(A, L, S_, c1 - c0, c0);
+      } else {
+        if (tid == 0 && a >= c0 && a < c1) {
+          uint32_t h = (uint32_t(a) * 0x9E3779B1u) >> op.hshift;
+          for (int p = 0; p < H; p++) {
+            if (L.R[h] == uint32_t(a) + 1u) {
+              L.R[kHashMax + h] -= self;
+              break;
+            }
+            h = (h + 1u) & op.hmask;
+          }
+        }
+        __syncthreads();
+        sp_hash_compact(A, L, S_, H, c0, c1);
+      }
+      t = t1;
+      H = 0;
+    }
+    if (!split && tid == 0) {
+      A.row_base[a] = S_.row_n ? S_.row_begin : 0;
+      A.row_nnz[a] = int32_t(S_.row_n);
+    }
+  }
+}
+
+// Split rows: the staging row (self term applied on the fly) compacted in column order into an
+// exact-size region; the uint32 overflow check compares the count sum with the closed-form row sum.
+__global__ __launch_bounds__(kSpThreads) void k_sp_split_finalize(const int32_t *__restrict__ split_row,
+                                                                   const uint32_t *__restrict__ staging, int32_t M,
+                                                                   const int64_t *__restrict__ row_ptr,
+                                                                   const int64_t *__restrict__ rowsum,
+                                                                   int32_t *__restrict__ col_out,
+                                                                   uint32_t *__restrict__ cnt_out,
+                                                                   unsigned long long *__restrict__ bump, int64_t cap,
+                                                                   int64_t *__restrict__ row_base,
+                                                                   int32_t *__restrict__ row_nnz,
+                                                                   PlanTotals *__restrict__ tot) {
+  __shared__ uint32_t s_w[kSpWaves];
+  __shared__ uint64_t s_red[kSpWaves];
+  __shared__ int64_t s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t s = blockIdx.x;
+  const int32_t a = split_row[s];
+  const uint32_t self = uint32_t(row_ptr[a + 1] - row_ptr[a]);
+  const uint32_t *row = staging + int64_t(s) * M;
+  const int32_t per = ((M + kSpWaves - 1) / kSpWaves + 63) & ~63;
+  const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
+  auto val = [&](int32_t b) -> uint32_t {
+    if (b >= hi) return 0u;
+    const uint32_t v = row[b];
+    return b == a ? v - self : v;
+  };
+  uint32_t cnt = 0;
+  uint64_t sum = 0;
+  for (int32_t b = lo + lane; b < hi; b += 64) {
+    const uint32_t v = val(b);
+    cnt += v != 0u;
+    sum += v;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) s_w[wave] = cnt;
+  const uint64_t total_sum = block_sum_u64(sum, s_red);
+  uint32_t off = 0, tot_n = 0;
+  for (int w = 0; w < kSpWaves; w++) {
+    off += w < wave ? s_w[w] : 0u;
+    tot_n += s_w[w];
+  }
+  if (tid == 0) {
+    int64_t b = int64_t(atomicAdd(bump, (unsigned long long)tot_n));
+    if (b + int64_t(tot_n) > cap) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 4ull);
+      b = -1;
+    }
+    s_base = b;
+    row_base[a] = b < 0 ? 0 : b;
+    row_nnz[a] = int32_t(tot_n);
+    if (total_sum != uint64_t(rowsum[a])) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+  }
+  __syncthreads();
+  const int64_t base = s_base;
+  if (base < 0) return;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t b0 = lo; b0 < hi; b0 += 64) {
+    const int32_t b = b0 + lane;
+    const uint32_t v = val(b);
+    const uint64_t m = __ballot(v != 0u);
+    if (v) {
+      const int64_t pos = base + off + uint32_t(__popcll(m & lt_mask));
+      col_out[pos] = b;
+      cnt_out[pos] = v;
+    }
+    off += uint32_t(__popcll(m));
+  }
+}
+
+__global__ void k_sp_nnz_total(const int32_t *__restrict__ row_nnz, int32_t M, PlanTotals *__restrict__ tot) {
+  __shared__ uint64_t s[4];
+  uint64_t v = 0;
+  for (int32_t a = blockIdx.x * 256 + threadIdx.x; a < M; a += gridDim.x * 256) v += uint64_t(row_nnz[a]);
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t = s[0] + s[1] + s[2] + s[3];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->nnz_total), (unsigned long long)t);
+  }
+}
+
+__global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict__ qctr,
+                               unsigned long long *__restrict__ bump) {
+  tot->err &= ~int64_t(4);
+  tot->nnz_total = 0;
+  qctr[0] = 0;
+  bump[0] = 0;
+}
+
+inline unsigned nblocks(int64_t n, int t) { return unsigned((n + t - 1) / t); }
+
+int bits_for(int64_t v) {
+  int b = 1;
+  while ((int64_t(1) << b) < v) b++;
+  return b;
+}
+
+}  // namespace
+
+Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
+                           CountResult *out, KernelTimer *timer, const int32_t *owner, int32_t part,
+                           const int64_t *freq, int64_t n_freq) {
+  const int32_t M = M_;
+  const int32_t T = int32_t((int64_t(M) + kTW - 1) / kTW);
+  if (T > kSpMaxTiles)
+    return Status{1, "n_items > " + std::to_string(int64_t(kSpMaxTiles) * kTW) + " is not supported"};
+  if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
+  if (U >= int64_t(UINT32_MAX)) return Status{1, "more than 2^32 - 1 users in one window"};
+  const int64_t U1 = std::max<int64_t>(U, 1), n1 = std::max<int64_t>(n, 1);
+  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
+  COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
+  COOC_TRY(keys_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
+  COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
+  COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
+  COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
+  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * (n1 + 4)));
+  COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 1)));
+  COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
+  COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
+  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(sp_roww_.reserve(sizeof(int64_t) * M));
+  COOC_TRY(sp_pstart_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(sp_pdense_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * 2 * M));
+  COOC_TRY(order_.reserve(sizeof(int32_t) * 2 * M));
+  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));           // work items per row (split rows)
+  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * M));           // ... in sorted order
+  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (M + 1)));   // ... exclusive prefix
+  COOC_TRY(sp_est_.reserve(sizeof(float) * (T * kEstK + T)));
+  PlanTotals *tot = tot_.as<PlanTotals>();
+  uint32_t *keys_in = keys_in_.as<uint32_t>(), *vals_in = vals_in_.as<uint32_t>();
+  uint32_t *keys = keys_out_.as<uint32_t>(), *vals = vals_out_.as<uint32_t>();
+  int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
+  float *est = sp_est_.as<float>(), *gmass = est + T * kEstK;
+  int32_t *qctr = queue_.as<int32_t>();
+  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
+  COOC_HIP_TRY(hipMemsetAsync(epre, 0, sizeof(int64_t), s));
+
+  // temp storage of the hipCUB calls
+  const int kb = bits_for(M);
+  size_t tmp = 0, q = 0;
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n1), 0, kb, s));
+  tmp = std::max(tmp, q);
+  hipcub::TransformInputIterator<int64_t, UserLen, const uint32_t *> len_it(vals, UserLen{up});
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, len_it, epre + 1, int(n1), s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, order_keys_.as<uint64_t>(),
+                                                            order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
+                                                            order_.as<int32_t>() + M, M, 0, 64, s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, q, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), M, s));
+  tmp = std::max(tmp, q);
+  COOC_TRY(sort_tmp_.reserve(tmp));
+
+  // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
+  const int64_t waves = std::min<int64_t>(std::max<int64_t>(U, 1), 65536);
+  if (owner) {
+    COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
+    COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
+  }
+  if (U > 0) {
+    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_arena_.as<uint32_t>(),
+                                                           sp_tb_.as<int32_t>(), keys_in, vals_in, owner, part,
+                                                           sp_ownc_.as<int32_t>(), tot);
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  int64_t n_c = n;  // contributions: every interaction, or those of the owned rows
+  if (owner) {
+    int64_t *ownoff = sp_ownoff_.as<int64_t>();
+    COOC_HIP_TRY(hipMemsetAsync(ownoff, 0, sizeof(int64_t), s));
+    if (U > 0) {
+      hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> oc(sp_ownc_.as<int32_t>(), WidenCount{});
+      size_t b = 0;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, oc, ownoff + 1, int(U), s));
+      COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
+      b = sort_tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, oc, ownoff + 1, int(U), s));
+      k_sp_owned_contribs<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, owner, part, ownoff, keys_in,
+                                                                  vals_in);
+      COOC_HIP_TRY(hipGetLastError());
+    }
+    COOC_HIP_TRY(hipMemcpyAsync(&n_c, ownoff + U, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+  }
+  SPT("partition");
+  // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152); 3. row pointer; 4. pair work
+  if (n_c > 0) {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n_c), 0, kb, s));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, len_it, epre + 1, int(n_c), s));
+  }
+  SPT("sort+scan");
+  k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n_c, M, row_ptr);
+  // 5. expected distinct keys per tile; 6. per-row plan
+  // column frequencies: of this log's interactions (owner == NULL), else the caller's global counts
+  const int64_t n_est = freq ? n_freq : n;
+  if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, freq, M, n_est, est, gmass);
+  else COOC_HIP_TRY(hipMemsetAsync(est, 0, sizeof(float) * (T * kEstK + T), s));
+  SPT("est");
+  k_sp_plan<<<nblocks(M, 256), 256, 0, s>>>(M, T, row_ptr, epre, est, gmass, rowsum_.as<int64_t>(),
+                                            sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(),
+                                            sp_pdense_.as<uint64_t>(), order_keys_.as<uint64_t>(),
+                                            order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
+                                            row_base_.as<int64_t>(), tot);
+  k_sp_totals<<<1, 1, 0, s>>>(tot, epre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+  const int64_t n_split = h_tot_->n_split;
+  const int64_t n_work = h_tot_->n_chunks;
+  const int64_t work_total = h_tot_->work_total;
+  const int64_t bound = h_tot_->cap_total, est_nnz = h_tot_->est_nnz;
+
+  SPT("plan+sync");
+#ifdef COOC_SP_TRACE
+  {
+    std::vector<uint64_t> ps(M), pd(M);
+    std::vector<int64_t> rw(M);
+    std::vector<float> es(T * kEstK + T);
+    hipMemcpy(ps.data(), sp_pstart_.p, 8 * M, hipMemcpyDeviceToHost);
+    hipMemcpy(pd.data(), sp_pdense_.p, 8 * M, hipMemcpyDeviceToHost);
+    hipMemcpy(rw.data(), sp_roww_.p, 8 * M, hipMemcpyDeviceToHost);
+    hipMemcpy(es.data(), est, 4 * (T * kEstK + T), hipMemcpyDeviceToHost);
+    for (int t = 0; t < T; t++) fprintf(stderr, "[sp] tile %d gmass %g est[0] %g est[20] %g est[40] %g\n", t, es[T * kEstK + t], es[t * kEstK], es[t * kEstK + 20], es[t * kEstK + 40]);
+    int shown = 0;
+    for (int a = 0; a < M && shown < 12; a++)
+      if (rw[a] > 0) { fprintf(stderr, "[sp] row %d W %lld start %llx dense %llx\n", a, (long long)rw[a], (unsigned long long)ps[a], (unsigned long long)pd[a]); shown++; }
+  }
+#endif
+  // 7. work queue: rows by pair work (descending); split rows' work items first
+  COOC_TRY(sp_queue_.reserve(sizeof(SpWork) * size_t(std::max<int64_t>(n_work, 1))));
+  COOC_TRY(split_row_.reserve(sizeof(int32_t) * std::max<int64_t>(n_split, 1)));
+  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * M));
+  {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, order_keys_.as<uint64_t>(),
+                                                              order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
+                                                              order_.as<int32_t>() + M, M, 0, 64, s));
+    k_sp_gather_nwork<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, row_nch_.as<int32_t>(), M,
+                                                      ord_nch_.as<int32_t>());
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
+                                                  M, s));
+    k_sp_queue<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, order_keys_.as<uint64_t>() + M,
+                                              ord_cbase_.as<int32_t>(), gmass, M, T, tot, sp_queue_.as<SpWork>(),
+                                              split_slot_.as<int32_t>(), split_row_.as<int32_t>());
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  SPT("queue");
+  if (n_split > 0) {
+    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
+    COOC_TRY(staging_.reserve(need));
+  }
+  // 8. output region: the expected entries plus slab slack, at most the exact bound
+  size_t free_b = 0, total_b = 0;
+  COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * n_cu_)));
+  const int64_t slack = 2 * int64_t(n_cu_) * slab + M;
+  int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
+  const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
+  cap = std::max<int64_t>(1, std::min(cap, budget));
+  vec_ = false;
+  dense_mode_ = false;
+  last_rows_ = M;
+  COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
+  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(), sp_arena_.as<uint32_t>(),
+                     sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(), sp_pdense_.as<uint64_t>(), est, nullptr,
+                     split_slot_.as<int32_t>(), nullptr, nullptr, bump_.as<unsigned long long>(), 0, slab,
+                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, n_c, U, n};
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kSpLds));
+  for (int attempt = 0; attempt < 2; attempt++) {
+    COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
+    COOC_TRY(cnt_.reserve(sizeof(uint32_t) * size_t(cap + 1)));
+    if (n_split > 0) COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, sizeof(uint32_t) * size_t(n_split) * size_t(M), s));
+    k_sp_reset_run<<<1, 1, 0, s>>>(tot, qctr, bump_.as<unsigned long long>());
+    SpArgs A = proto;
+    A.staging = staging_.as<uint32_t>();
+    A.col_out = col_.as<int32_t>();
+    A.cnt_out = cnt_.as<uint32_t>();
+    A.cap = cap;
+#ifdef COOC_SP_TRACE
+    static unsigned long long *prog = nullptr;
+    if (!prog) hipHostMalloc(reinterpret_cast<void **>(&prog), 8 * 64 * 1024, hipHostMallocDefault);
+    memset(prog, 0xff, 8 * 64 * 1024);
+    prog[2047] = 0;
+    prog[1024] = 0;
+    prog[1536] = 0;
+    A.prog = prog;
+    fprintf(stderr, "[sp] n_work %lld cap %lld slab %lld est %lld bound %lld\n", (long long)n_work, (long long)cap, (long long)slab, (long long)est_nnz, (long long)bound);
+#endif
+    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+    if (n_work > 0) {
+      const int64_t grid = std::min<int64_t>(n_work, n_cu_);
+      k_sp_main<<<unsigned(grid), kSpThreads, kSpLds, s>>>(A);
+      COOC_HIP_TRY(hipGetLastError());
+#ifdef COOC_SP_TRACE
+      for (int it = 0; it < 100 && hipStreamQuery(s) == hipErrorNotReady; it++) usleep(50000);
+      if (hipStreamQuery(s) == hipErrorNotReady) {
+        for (int g = 0; g < grid; g++)
+        {
+          fprintf(stderr, "[sp] wg %d: work %lld phase %lld total %lld nb %lld waves", g, (long long)prog[g * 64], (long long)prog[g * 64 + 1], (long long)prog[g * 64 + 2], (long long)prog[g * 64 + 3]);
+          for (int w = 0; w < 16; w++) fprintf(stderr, " %lld", (long long)prog[g * 64 + 16 + w]);
+          fprintf(stderr, "\n");
+        }
+        for (int tt = 0; tt < 2; tt++) {
+          const unsigned long long *q = prog + 1024 + tt * 512;
+          fprintf(stderr, "[sp] thread %d trace (%llu):", tt * 64, q[0]);
+          for (unsigned long long i = 0; i < q[0] && i < 255; i++) fprintf(stderr, " %llu", q[1 + i]);
+          fprintf(stderr, "\n");
+        }
+        fflush(stderr);
+        _exit(3);
+      }
+      hipStreamSynchronize(s);
+      fprintf(stderr, "[sp] bounds flags %llx\n", prog[2047]);
+#endif
+    }
+    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+  SPT("main");
+    if (n_split > 0) {
+      k_sp_split_finalize<<<unsigned(n_split), kSpThreads, 0, s>>>(
+          split_row_.as<int32_t>(), staging_.as<uint32_t>(), M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
+          cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
+          tot);
+      COOC_HIP_TRY(hipGetLastError());
+    }
+  SPT("finalize");
+    k_sp_nnz_total<<<std::min<unsigned>(nblocks(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
+    COOC_HIP_TRY(hipGetLastError());
+    int64_t err = 0;
+    COOC_HIP_TRY(hipMemcpyAsync(&err, &tot->err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+    if (!(err & 4) || cap >= bound + slack) break;
+    // the expected key count was too low: rerun into a region of the exact bound
+    size_t f2 = 0, t2 = 0;
+    COOC_HIP_TRY(hipMemGetInfo(&f2, &t2));
+    const int64_t budget2 = int64_t((f2 + col_.cap + cnt_.cap) / 10 * 8 / 8);
+    if (budget2 <= cap) break;
+    cap = std::min<int64_t>(bound + slack, budget2);
+  }
+  out->row_base = row_base_.as<int64_t>();
+  out->row_nnz = row_nnz_.as<int32_t>();
+  out->col = col_.as<int32_t>();
+  out->cnt = cnt_.as<uint32_t>();
+  out->dense = nullptr;
+  out->rowsum = rowsum_.as<int64_t>();
+  out->work = work_total;
+  out->observed = work_total - n_c;  // ordered pairs of the counted rows
+  out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
+  return Status::Ok();
+}
+
+}  // namespace cooc

@@ -140,6 +140,101 @@ def config_c3(seed: int = 3, U: int = 10_000_000, M: int = 1_000_000, N: int = 1
                 name=f"C3 Zipf 1B: shard {shard}/{n_shards} ({Us} users, {Ns} interactions, 1e6 items)", seed=seed + shard)
 
 
+# ---- C3, shard-invariant: every user's list is a pure function of (seed, user id) -----------------
+# The generator above draws users sequentially from one PCG64 stream, so a 1-GPU run and an 8-GPU
+# run would process different logs.  c3_users(u0, u1) instead derives user u's length and items from
+# a counter-based hash (splitmix64 of (seed, u) and of (seed, u, j)), so any user range of the same
+# 1B log can be materialised on its own, on the host (numpy) or on a GPU (torch), bit-identically.
+#   n_u   = LEN_TABLE[top 16 bits of h(seed, u)]: 65,536 quantiles of lognormal(sigma = 1) scaled to a
+#           mean of 100, capped at 10,000;
+#   x_uj  = the item of rank searchsorted(Zipf(1.0) CDF over 1e6 items, uniform53(h(seed, u, j))).
+C3_USERS, C3_ITEMS, C3_SEED = 10_000_000, 1_000_000, 3
+_M64 = (1 << 64) - 1
+_GOLD, _MIX1, _MIX2 = 0x9E3779B97F4A7C15, 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+_c3_cache: dict = {}
+
+
+def _c3_tables(M: int = C3_ITEMS, mean: float = 100.0, cap: int = 10_000, sigma: float = 1.0):
+    key = (M, mean, cap, sigma)
+    if key not in _c3_cache:
+        from scipy.special import ndtri
+
+        q = (np.arange(65536, dtype=np.float64) + 0.5) / 65536.0
+        lens = np.clip(np.round(np.exp(sigma * ndtri(q)) * (mean / np.exp(0.5 * sigma * sigma))), 1, cap)
+        _c3_cache[key] = (lens.astype(np.int64), _zipf_cdf(M, 1.0))
+    return _c3_cache[key]
+
+
+def _splitmix_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(_GOLD)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(_MIX1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(_MIX2)
+        return z ^ (z >> np.uint64(31))
+
+
+def _i64(c: int) -> int:  # a uint64 constant as the int64 with the same bits
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _splitmix_torch(x):
+    import torch
+
+    def srl(z, k):  # logical shift right of an int64 tensor
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    z = x + _i64(_GOLD)
+    z = (z ^ srl(z, 30)) * _i64(_MIX1)
+    z = (z ^ srl(z, 27)) * _i64(_MIX2)
+    return z ^ srl(z, 31)
+
+
+def c3_lengths(u0: int, u1: int, seed: int = C3_SEED, device=None):
+    """History lengths of users [u0, u1) of the shard-invariant C3 log."""
+    lens_t, _ = _c3_tables()
+    if device is None:
+        h = _splitmix_np((np.arange(u0, u1, dtype=np.uint64) ^ np.uint64(seed << 40)))
+        return lens_t[(h >> np.uint64(48)).astype(np.int64)]
+    import torch
+
+    h = _splitmix_torch(torch.arange(u0, u1, dtype=torch.int64, device=device) ^ (seed << 40))
+    return torch.as_tensor(lens_t, device=device)[(h >> 48) & 0xFFFF]
+
+
+def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None):
+    """CSR (user_ptr int64[U+1], items int32[N]) of users [u0, u1) of the shard-invariant C3 log:
+    numpy arrays when device is None, else torch tensors built on that device."""
+    lens = c3_lengths(u0, u1, seed, device)
+    _, cdf = _c3_tables()
+    if device is None:
+        user_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        owner = np.repeat(np.arange(u0, u1, dtype=np.uint64), lens)
+        j = np.arange(int(user_ptr[-1]), dtype=np.int64) - np.repeat(user_ptr[:-1], lens)
+        h = _splitmix_np(((owner << np.uint64(14)) | j.astype(np.uint64)) ^ np.uint64((seed << 58) | 0x5A5A))
+        x = (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+        items = np.minimum(np.searchsorted(cdf, x, side="right"), len(cdf) - 1).astype(np.int32)
+        return user_ptr, items
+    import torch
+
+    user_ptr = torch.zeros(u1 - u0 + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=user_ptr[1:])
+    n = int(user_ptr[-1].item())
+    owner = torch.repeat_interleave(torch.arange(u0, u1, dtype=torch.int64, device=device), lens, output_size=n)
+    j = torch.arange(n, dtype=torch.int64, device=device) - torch.repeat_interleave(user_ptr[:-1], lens, output_size=n)
+    h = _splitmix_torch(((owner << 14) | j) ^ ((seed << 58) | 0x5A5A))
+    del owner, j
+    x = ((h >> 11) & ((1 << 53) - 1)).to(torch.float64) * (1.0 / 9007199254740992.0)
+    del h
+    cdf_t = torch.as_tensor(cdf, device=device)
+    items = torch.clamp(torch.searchsorted(cdf_t, x, right=True), max=len(cdf) - 1).to(torch.int32)
+    return user_ptr, items
+
+
+def c3_ordered_pairs(u0: int, u1: int, seed: int = C3_SEED) -> int:
+    n = c3_lengths(u0, u1, seed).astype(np.int64)
+    return int(np.sum(n * (n - 1)))
+
+
 def spread_over_windows(rng, user_ptr: np.ndarray, n_windows: int, window_ms: int) -> np.ndarray:
     """C4: event times spread over n_windows tumbling windows, ascending within each user."""
     n = int(user_ptr[-1])

@@ -18,6 +18,13 @@ reference's keyed data-parallelism:
                                                  row's owner, then an owner-side merge;
 * rowSumStream.broadcast() (:163)             -> one all-reduce of the int64 row-sum vector.
 
+* ``count_owned`` (n_items >= 40,320: the C3 / C5 universes) routes the INPUT: every rank
+  all-gathers the users' histories (input sized, 4 B per interaction), and counts the rows it owns
+  over all of them.  Ownership balances the row work: rows sorted by global item frequency are dealt
+  to the ranks in snake order (Zipf-hot rows spread over every rank).  Nothing is merged.
+
+Every library call runs on torch's current stream (cooc.h stream contract), so collectives and
+kernels are ordered by the stream itself; no device-wide synchronisation is needed.
 The compute (local reduce, pack, merge) runs in libcooc_hip.so; this module only moves buffers.
 """
 from __future__ import annotations
@@ -54,14 +61,12 @@ def count_sharded(core, user_ptr, items, group=None, stream=None) -> ShardResult
     # row sums: all-reduce (the broadcast of the reference's row-sum stream)
     rowsum = torch.empty(M, dtype=torch.int64, device=dev)
     core.copy_rowsum_device(rowsum, stream)
-    _sync(dev, stream)
     work = dist.all_reduce(rowsum, group=group, async_op=True)
     # partial rows -> owners
     send_counts = core.partition_plan(world)
     row_nnz = torch.empty(M, dtype=torch.int32, device=dev)
     entries = torch.empty(int(send_counts.sum()), dtype=torch.int64, device=dev)
     core.partition_pack(world, row_nnz, entries, stream)
-    _sync(dev, stream)
     counts = torch.as_tensor(send_counts, dtype=torch.int64, device=dev)
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
@@ -75,15 +80,11 @@ def count_sharded(core, user_ptr, items, group=None, stream=None) -> ShardResult
     work.wait()
     obs = torch.tensor([res.observed], dtype=torch.int64, device=dev)
     dist.all_reduce(obs, group=group)
-    _sync(dev, stream)
     merged = core.merge_partitions(world, rank, recv_nnz, recv_entries, rowsum, stream)
     return ShardResult(rank, world, merged, rowsum, int(obs.item()), int(res.observed), int(send_counts.sum()),
                        int(sum(recv_counts_h)))
 
 
-def _sync(dev, stream):
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
 
 
 @dataclass
@@ -130,6 +131,68 @@ def count_records(core, user_ptr, items, group=None, stream=None) -> RecordsResu
     obs = torch.tensor([local_obs], dtype=torch.int64, device=dev)
     dist.all_reduce(obs, group=group)
     work.wait()
-    _sync(dev, stream)
     owned = core.shard_count(world, rank, recv_rc, recv_desc, arena_all, stride, stream)
     return RecordsResult(rank, world, owned, int(obs.item()), int(local_obs), n, int(sum(recv_h)), stride)
+
+
+def snake_owner(item_counts: torch.Tensor, world: int) -> torch.Tensor:
+    """Row owner map: rows by descending global frequency dealt 0..W-1, W-1..0, 0..W-1, ... (stable,
+    so every rank computes the same map from the same all-reduced counts)."""
+    M = item_counts.numel()
+    order = torch.argsort(-item_counts, stable=True)
+    pos = torch.arange(M, device=item_counts.device)
+    lap, r = pos // world, pos % world
+    owner = torch.empty(M, dtype=torch.int32, device=item_counts.device)
+    owner[order] = torch.where(lap % 2 == 0, r, world - 1 - r).to(torch.int32)
+    return owner
+
+
+@dataclass
+class OwnedResult:
+    part: int
+    n_parts: int
+    owned: object           # CoocDeviceResult over all n_items rows; rows of other ranks are empty
+    owner: torch.Tensor     # int32 [n_items] row owner map
+    observed: int           # global ordered pairs (sum over ranks of the owned rows' pairs)
+    local_observed: int     # ordered pairs of this rank's owned rows
+    n_users_all: int
+    n_interactions_all: int
+    gathered_bytes: int     # history bytes this rank received
+
+
+def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
+    """One window over this rank's users; histories all-gathered, owned rows counted here."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = items.device
+    M = core.n_items
+    n_users, n = int(user_ptr.numel()) - 1, int(items.numel())
+    # global item frequencies (the planner's column estimate) and the row owner map
+    counts = torch.bincount(items.to(torch.int64), minlength=M)[:M].to(torch.int64)
+    dist.all_reduce(counts, group=group)
+    owner = snake_owner(counts, world)
+    # all-gather the histories: lengths and items, padded to the largest rank's share
+    sizes = torch.tensor([n_users, n], dtype=torch.int64, device=dev)
+    all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(all_sizes, sizes, group=group)
+    sz = all_sizes.view(world, 2).cpu().tolist()
+    max_u, max_n = max(s[0] for s in sz), max(max(s[1] for s in sz), 1)
+    lens = torch.zeros(max_u, dtype=torch.int64, device=dev)
+    lens[:n_users] = user_ptr[1:] - user_ptr[:-1]
+    lens_all = torch.empty(world * max_u, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(lens_all, lens, group=group)
+    it_pad = torch.zeros(max_n, dtype=torch.int32, device=dev)
+    it_pad[:n] = items
+    it_all = torch.empty(world * max_n, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(it_all, it_pad, group=group)
+    lens_cat = torch.cat([lens_all[r * max_u:r * max_u + sz[r][0]] for r in range(world)])
+    items_cat = torch.cat([it_all[r * max_n:r * max_n + sz[r][1]] for r in range(world)])
+    del it_all, it_pad
+    up_all = torch.zeros(lens_cat.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens_cat, 0, out=up_all[1:])
+    n_all = int(items_cat.numel())
+    res = core.count_device_owned(up_all, items_cat, owner, rank, counts, n_all, stream)
+    obs = torch.tensor([res.observed], dtype=torch.int64, device=dev)
+    dist.all_reduce(obs, group=group)
+    return OwnedResult(rank, world, res, owner, int(obs.item()), int(res.observed), int(lens_cat.numel()), n_all,
+                       4 * (n_all - n) + 8 * (int(lens_cat.numel()) - n_users))

@@ -36,6 +36,13 @@
  *    views are produced by the copy functions ("ref_compat").
  *  - There is no CPU fallback: without a usable HIP device every compute entry point fails with
  *    COOC_ERR_HIP.
+ *  - Streams.  An entry point that takes device pointers and a `hip_stream` runs its kernels on that
+ *    stream; NULL is the HIP null stream (which orders with hipMemcpy and with torch's default
+ *    stream).  The caller must have ENQUEUED the work producing the inputs on the same stream (or
+ *    ordered it before, e.g. with an event); the library never reads caller buffers from another
+ *    stream.  Entry points that return host values (sizes, counts) synchronise that stream first.
+ *  - No C++ exception crosses this boundary: host allocation failures return COOC_ERR_OOM, any
+ *    other internal exception COOC_ERR_STATE, with the message in cooc_last_error.
  */
 #ifndef COOC_H_
 #define COOC_H_
@@ -128,12 +135,22 @@ COOC_API const char *cooc_last_error(const cooc_ctx *ctx);
 
 /* ---- stateless one-window batch over a device CSR (the benchmarked unit) ----------------------
  * d_user_ptr: int64[n_users+1] offsets into d_items (device memory); d_items: int32[n_interactions]
- * in per-user arrival order.  hip_stream: a hipStream_t (NULL = the context's own stream).
+ * in per-user arrival order.  hip_stream: a hipStream_t (NULL = the HIP null stream).
  * Computes C = sum over users of the ordered position pairs (p != q) -> (x_p, x_q), i.e. exactly
  * what NonSampled...java:113-165 emits for users whose histories start empty, reduced by
  * ItemRowAggregator/RowSumAggregator.  Does not touch the context's streaming state. */
 COOC_API int cooc_count_device(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
                       int64_t n_interactions, void *hip_stream, cooc_device_result *out);
+/* Multi-GPU for large item universes (n_items >= 40,320, the C3 / C5 configs): the keyBy(itemA) of
+ * FlinkCooccurrences.java:152 as row ownership.  Counts only the rows a with d_owner[a] == part, over
+ * every user given (the all-gathered log of all parts); rows owned by other parts come out empty.
+ * d_item_counts int64[n_items]: the global log's item frequencies (n_total interactions in all),
+ * which size the planner; out->observed = the ordered pairs of the owned rows (their sum over the
+ * parts is the log's sum_u n_u (n_u - 1)).  Same borrowed padded-CSR result as cooc_count_device. */
+COOC_API int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                                     int64_t n_interactions, const int32_t *d_owner, int32_t part,
+                                     const int64_t *d_item_counts, int64_t n_total, void *hip_stream,
+                                     cooc_device_result *out);
 /* Same from host buffers; afterwards cooc_copy_batch copies the packed CSR out. */
 COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
                     cooc_window_info *info);

@@ -850,3 +850,82 @@ EXPORT int64_t oc_batch_dense(int64_t n_users, const int64_t *user_ptr, const in
   }
   return observed;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Multithreaded one-window restatement (bench.py's cpu_baseline; BASELINE.md: "CPU restatement, */
+/* not the JVM reference").  The job's keyed data-parallelism with threads for subtasks: thread t  */
+/* owns the rows a with a mod n_threads == t (keyBy(ItemCooccurrences::getItem),                  */
+/* FlinkCooccurrences.java:152) and expands every user's window record by record                 */
+/* (NonSampled:129-161, empty histories), keeping the (row, other) increments of its own rows in  */
+/* Int2ShortOpenHashMap restatements (ItemRowAggregator.java:26-31).  Returns the distinct keys;  */
+/* *pairs = the ordered pairs seen (each counted once, by its row's owner).                      */
+/* ------------------------------------------------------------------------------------------ */
+#include <pthread.h>
+
+typedef struct {
+  int64_t n_users;
+  const int64_t *user_ptr;
+  const int32_t *items;
+  int32_t n_items, n_threads, t;
+  int64_t nnz, pairs;
+} mt_job;
+
+static void *mt_run(void *arg) {
+  mt_job *j = (mt_job *)arg;
+  const int32_t T = j->n_threads, t = j->t;
+  const int32_t n_own = (j->n_items - t + T - 1) / T;
+  rowmap *rows = (rowmap *)calloc((size_t)(n_own > 0 ? n_own : 1), sizeof(rowmap));
+  char *live = (char *)calloc((size_t)(n_own > 0 ? n_own : 1), 1);
+  int64_t pairs = 0;
+  for (int64_t u = 0; u < j->n_users; u++) {
+    const int32_t *h = j->items + j->user_ptr[u];
+    const int64_t n = j->user_ptr[u + 1] - j->user_ptr[u];
+    for (int64_t p = 1; p < n; p++) { /* item x = h[p] against its history h[0..p) */
+      const int32_t x = h[p];
+      for (int64_t q = 0; q < p; q++) {
+        const int32_t o = h[q];
+        if (x % T == t) { /* record (x, history, +1), NonSampled:138-139 */
+          rowmap *r = &rows[x / T];
+          if (!live[x / T]) { rowmap_init(r); live[x / T] = 1; }
+          rowmap_add_to(r, o, 1, 1);
+          pairs++;
+        }
+        if (o % T == t) { /* record (o, x, +1), NonSampled:144-147 */
+          rowmap *r = &rows[o / T];
+          if (!live[o / T]) { rowmap_init(r); live[o / T] = 1; }
+          rowmap_add_to(r, x, 1, 1);
+          pairs++;
+        }
+      }
+    }
+  }
+  int64_t nnz = 0;
+  for (int32_t i = 0; i < n_own; i++)
+    if (live[i]) { nnz += rows[i].n; rowmap_free(&rows[i]); }
+  free(rows);
+  free(live);
+  j->nnz = nnz;
+  j->pairs = pairs;
+  return NULL;
+}
+
+EXPORT int64_t oc_count_batch_mt(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int32_t n_items,
+                                 int32_t n_threads, int64_t *pairs) {
+  if (n_threads < 1) n_threads = 1;
+  mt_job *jobs = (mt_job *)calloc((size_t)n_threads, sizeof(mt_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+  for (int32_t t = 0; t < n_threads; t++) {
+    jobs[t] = (mt_job){n_users, user_ptr, items, n_items, n_threads, t, 0, 0};
+    pthread_create(&th[t], NULL, mt_run, &jobs[t]);
+  }
+  int64_t nnz = 0, pr = 0;
+  for (int32_t t = 0; t < n_threads; t++) {
+    pthread_join(th[t], NULL);
+    nnz += jobs[t].nnz;
+    pr += jobs[t].pairs;
+  }
+  free(jobs);
+  free(th);
+  if (pairs) *pairs = pr;
+  return nnz;
+}

@@ -95,6 +95,7 @@ def lib():
         "oc_global_n_rowsums": (ctypes.c_int32, [vp]),
         "oc_global_rowsums": (None, [vp, i32p, i32p, i64p]),
         "oc_batch_dense": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, i64p, i64p]),
+        "oc_count_batch_mt": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, ctypes.c_int32, i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -314,6 +315,16 @@ def batch_dense(user_ptr: np.ndarray, items: np.ndarray, n_items: int):
     obs = lib().oc_batch_dense(len(user_ptr) - 1, _p(user_ptr, i64p), _p(items, i32p), n_items,
                                _p(counts, i64p), _p(rowsums, i64p))
     return counts, rowsums, int(obs)
+
+
+def count_batch_mt(user_ptr: np.ndarray, items: np.ndarray, n_items: int, n_threads: int):
+    """Multithreaded record-by-record restatement of one window (threads own rows a mod n_threads):
+    -> (distinct keys, ordered pairs).  The CPU baseline of bench.py."""
+    up = np.ascontiguousarray(user_ptr, np.int64)
+    it = np.ascontiguousarray(items, np.int32)
+    pairs = np.zeros(1, np.int64)
+    nnz = lib().oc_count_batch_mt(len(up) - 1, _p(up, i64p), _p(it, i32p), n_items, n_threads, _p(pairs, i64p))
+    return int(nnz), int(pairs[0])
 
 
 def cut_csr(user_ptr: np.ndarray, items: np.ndarray, user_cut: int):
