@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark: item-pair co-occurrences counted per second on MI355X (BASELINE.json metric).
 
-A step = one pass of the hot path over one window of synthetic input already resident in HBM:
-pair expansion + keyed (itemA, itemB) count reduction + row sums (cooc_count_device), from the
-CSR of user histories to the final counts in HBM.  Workload at N=1: BASELINE configs[1], the
-MovieLens-20M-shaped log (138,493 users x 26,744 items, 20,000,263 interactions), numpy PCG64
-seed 2.  With --gpus N (one process per GPU, torchrun), every rank expands its own C2-shaped
-user shard (seed 2 + rank): users are independent units, so the per-GPU work is fixed ("weak").
+A step = one pass of the hot path over one window of synthetic input already resident in HBM: pair
+expansion + keyed (itemA, itemB) count reduction + row sums, from the CSR of user histories to the
+final counts in HBM (padded CSR).
 
-Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (k_acc_batch, timed with
-HIP events on the stream it runs on) and a CPU baseline (the oracle's record-by-record
-restatement of the reference path, timed on a bounded sample of the same workload).
+Workload (default --config c3): the north star's Zipf-skewed 1B log (BASELINE configs[2]: 1e7
+users x 1e6 items, 1e9 interactions), generated shard-invariantly (datagen.c3_users: every user's
+list is a function of (seed, user id)) directly on each GPU.  Rank r of N holds users
+[r U/8, (r+1) U/8): per-GPU work is fixed ("weak" scaling) and at N = 8 the ranks hold the whole
+1B log.  N = 1 therefore runs one GPU's 1/8 share of C3 (1.25e6 users, 1.25e8 interactions,
+3.36e10 ordered pairs).  N > 1: the ranks all-gather the histories over RCCL and each counts the
+rows it owns (sharding.count_owned, the keyBy(itemA) of FlinkCooccurrences.java:152); the
+all-gather, the item-frequency all-reduce and the owner map are inside the timed step.
+--config c2: the MovieLens-20M-shaped log (configs[1]) per rank, records exchange for N > 1.
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on the stream
+it runs on) and a CPU baseline (the oracle's multithreaded record-by-record restatement on a
+bounded sample of the same log, all the host threads of this GPU's share).
 """
 from __future__ import annotations
 
@@ -26,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "item-pair co-occurrences counted/sec (node) at 1/2/4/8 GPUs; achieved HBM GB/s"
 
 
 def algorithmic_bytes(P: int, N: int, U: int, D: int) -> int:
@@ -34,44 +42,54 @@ def algorithmic_bytes(P: int, N: int, U: int, D: int) -> int:
     return 4 * P + 4 * N + 8 * (U + 1) + 12 * D
 
 
-def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, budget_pairs: int = 80_000_000) -> dict:
-    """The oracle's record-by-record restatement (NonSampled...java:113-165 -> ItemRowAggregator ->
-    RowSumAggregator, one window) on the first users of the workload, ~10-20 s of one core."""
+def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: str, target_s: float = 12.0) -> dict:
+    """The oracle's multithreaded record-by-record restatement (threads own rows a mod T, every
+    thread expands every user's records, NonSampled...java:129-161 -> ItemRowAggregator addTo) on
+    the first users of the same log: a calibration run sizes a sample of ~target_s seconds."""
     from oracle import oracle
 
+    threads = max(1, min(16, os.cpu_count() or 1))
     n = np.diff(user_ptr)
     cum = np.cumsum(n * (n - 1))
-    nu = int(np.searchsorted(cum, budget_pairs)) + 1
-    sub_up = user_ptr[: nu + 1]
-    sub_it = items[: sub_up[-1]]
-    P = int(cum[nu - 1])
-    users = np.repeat(np.arange(nu, dtype=np.int32), n[:nu])
-    s = oracle.OracleStream(1000, 0)
+
+    def sample(pairs: int):
+        nu = min(len(n), int(np.searchsorted(cum, pairs)) + 1)
+        up = user_ptr[: nu + 1]
+        return nu, up, items[: up[-1]]
+
+    nu, up, it = sample(20_000_000)
     t0 = time.perf_counter()
-    s.process_elements(users, sub_it, np.zeros(len(sub_it), np.int64))
-    w = s.process_watermark(1 << 62)
+    oracle.count_batch_mt(up, it, n_items, threads)
+    rate = max(1.0, float(cum[nu - 1]) / (time.perf_counter() - t0))
+    nu, up, it = sample(int(min(1.5e9, rate * target_s)))
+    P = int(cum[nu - 1])
+    t0 = time.perf_counter()
+    nnz, pairs = oracle.count_batch_mt(up, it, n_items, threads)
     dt = time.perf_counter() - t0
-    assert w and w[0].observed == P
-    return {"value": P / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"first {nu} users of the same C2 log ({len(sub_it)} interactions, {P} ordered pairs), "
-                      f"one window, {dt:.1f} s"}
+    assert pairs == P
+    return {"value": P / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "label": "CPU restatement, not the JVM reference (BASELINE.md)",
+            "sample": f"first {nu} users of {what} ({len(it)} interactions, {P} ordered pairs, {nnz} keys), "
+                      f"one window, {threads} threads, {dt:.1f} s"}
 
 
-def core_last_nnz(core) -> int:
-    """Distinct keys of this rank's local (pre-exchange) result."""
-    return int(core.partition_plan(1)[0])
+def load_pmc(path: str) -> dict:
+    if os.path.exists(path):
+        try:
+            with open(path) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+    return {}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=["c3", "c2"], default="c3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--exchange", choices=["records", "partials"], default="records",
-                    help="N > 1: route pair records to owner(a) (default) or partial counts (sharding.py)")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_k_acc_batch.json"),
-                    help="rocprofv3 PMC summary of k_acc_batch (HBM traffic per launch), if collected")
     args = ap.parse_args()
 
     import torch
@@ -80,23 +98,39 @@ def main():
     import __graft_entry__
 
     pkg = __graft_entry__.load_package()
-    from flink_cooccurrence_amd import datagen
+    from flink_cooccurrence_amd import datagen, sharding
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    from flink_cooccurrence_amd import sharding
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
-    d = datagen.config_c2(seed=2 + rank)
-    up_h, it_h, M = d["user_ptr"], d["items"], d["n_items"]
-    U, N = len(up_h) - 1, int(up_h[-1])
-    P = datagen.ordered_pairs(up_h)
-    up = torch.from_numpy(up_h).to(dev)
-    it = torch.from_numpy(it_h).to(dev)
+    if args.config == "c3":
+        U8 = datagen.C3_USERS // 8
+        u0, u1 = rank * U8, (rank + 1) * U8
+        up, it = datagen.c3_users(u0, u1, device=dev)
+        M = datagen.C3_ITEMS
+        P_local = datagen.c3_ordered_pairs(u0, u1)
+        kernel = "k_sp_main"
+        pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_sp_main.json"))
+        workload = ("C3 Zipf-skewed 1B log (BASELINE configs[2]), shard-invariant generator "
+                    f"datagen.c3_users seed {datagen.C3_SEED}: users [r*1.25e6, (r+1)*1.25e6) on rank r "
+                    f"(1/8 of 1e7 users per GPU; the whole 1e9-interaction log at 8 GPUs), 1e6 items, Zipf(1.0) "
+                    "with replacement, lognormal lengths of mean 100, one window")
+    else:
+        d = datagen.config_c2(seed=2 + rank)
+        up = torch.from_numpy(d["user_ptr"]).to(dev)
+        it = torch.from_numpy(d["items"]).to(dev)
+        M = d["n_items"]
+        P_local = datagen.ordered_pairs(d["user_ptr"])
+        kernel = "k_acc_batch"
+        pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_acc_batch.json"))
+        workload = ("C2 MovieLens-20M-shaped: 138,493 users x 26,744 items, 20,000,263 interactions per GPU, "
+                    "Zipf(0.9) without replacement, one window, numpy PCG64 seed 2 (+rank)")
+    U, N = int(up.numel()) - 1, int(it.numel())
     torch.cuda.synchronize()
 
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
@@ -104,11 +138,10 @@ def main():
 
     def step():
         if world == 1:
-            return core.count_device(up, it)  # returns after the stream drained (errors are checked)
-        # users sharded over ranks; rows owned by a mod world (keyBy(itemA), FlinkCooccurrences.java:152)
-        if args.exchange == "records":
-            return sharding.count_records(core, up, it)
-        return sharding.count_sharded(core, up, it)
+            return core.count_device(up, it)  # on torch's current stream; returns after it drained
+        if args.config == "c3":
+            return sharding.count_owned(core, up, it)
+        return sharding.count_records(core, up, it)
 
     for _ in range(args.warmup):
         step()
@@ -125,38 +158,34 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world == 1:
-        assert res.observed == P, "pair count mismatch"
-        D = int(res.nnz)
-    else:
-        assert res.local_observed == P, "pair count mismatch"
-        D = int(res.owned.nnz) if args.exchange == "records" else int(core_last_nnz(core))
 
-    stats = torch.tensor([elapsed, float(P), float(algorithmic_bytes(P, N, U, D))], dtype=torch.float64, device=dev)
+    if world == 1:
+        assert res.observed == P_local, "pair count mismatch"
+        D, P_counted, N_seen, U_seen = int(res.nnz), int(res.observed), N, U
+    elif args.config == "c3":
+        D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.local_observed), res.n_interactions_all, res.n_users_all
+    else:
+        D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.owned.observed), N, U
+    stats = torch.tensor([elapsed, float(P_local), float(D)], dtype=torch.float64, device=dev)
     if world > 1:
         t = stats[:1].clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         s = stats[1:].clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        elapsed, p_total = float(t.item()), float(s[0].item())
+        elapsed, p_total, d_total = float(t.item()), float(s[0].item()), float(s[1].item())
+        if args.config == "c3":
+            assert int(round(p_total)) == res.observed, "global pair count mismatch"
     else:
-        p_total = float(P)
+        p_total, d_total = float(P_local), float(D)
     ms_per_step = elapsed / args.steps * 1e3
     value = p_total * args.steps / elapsed
 
-    k_ms = float(np.mean(kernel_ms))
-    b_alg = algorithmic_bytes(P, N, U, D)
+    k_ms = float(np.median(kernel_ms))
+    b_alg = algorithmic_bytes(P_counted, N_seen, U_seen, D)
     achieved = b_alg / (k_ms * 1e-3) / 1e9
-    traffic, pmc = None, {}
-    if os.path.exists(args.pmc_file):
-        try:
-            with open(args.pmc_file) as f:
-                pmc = json.load(f)
-            traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic, pmc = None, {}
+    traffic = pmc.get("hbm_bytes_per_launch")
     out = {
-        "metric": "item-pair co-occurrences counted/sec (node)",
+        "metric": METRIC,
         "value": value,
         "unit": "pairs/s",
         "n_gpus": world,
@@ -169,47 +198,43 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": "C2 MovieLens-20M-shaped: 138,493 users x 26,744 items, 20,000,263 interactions, "
-                        "Zipf(0.9) without replacement, one window, numpy PCG64 seed 2 (+rank)",
-            "users_per_gpu": U, "items": M, "interactions_per_gpu": N, "ordered_pairs_per_gpu": P,
-            "distinct_keys_per_gpu": D,
-            "output": "dense uint32 [items x items] in HBM" if world == 1 and res.dense else "padded CSR in HBM",
+            "workload": workload,
+            "users_per_gpu": U, "items": M, "interactions_per_gpu": N, "ordered_pairs_total": int(p_total),
+            "distinct_keys_total": int(d_total),
+            "output": "padded CSR (row_base, row_nnz, col int32, cnt uint32) in HBM, exact counts",
             "parallelism": f"users sharded over {world} GPU(s)" + (
-                f"; rows owned by a mod N, exchange over RCCL: {args.exchange}" if world > 1 else ""),
+                "; rows owned by frequency-snake order, histories all-gathered over RCCL" if world > 1 and
+                args.config == "c3" else "; rows owned by a mod N, records exchange over RCCL" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_acc_batch",
+            "kernel": kernel,
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_gbps": (traffic / (k_ms * 1e-3) / 1e9) if traffic else None,
+            "hbm_frac_measured": (traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
             "lds_util": pmc.get("lds_util"),
             "lds_bank_conflict_frac": pmc.get("lds_bank_conflict_frac"),
             "kernel_ms": k_ms,
             "algorithmic_bytes_per_launch": b_alg,
-            "note": "B_alg = 4P + 4N + 8(U+1) + 12D (SURVEY.md §8(d)). frac > 1 flags cache reuse: every "
-                    "partner-id list is re-read once per item in it from L2 / Infinity Cache (2 B per id "
-                    "here). traffic = HBM-side bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + "
-                    "WRITE_SIZE, profiles/pmc_k_acc_batch.json); the kernel is bound by LDS atomics "
-                    "(lds_util, lds_bank_conflict_frac), see DESIGN.md §4",
+            "units_per_launch": {"ordered_pairs": P_counted, "interactions": N_seen, "users": U_seen,
+                                 "distinct_keys": D},
+            "note": "B_alg = 4P + 4N + 8(U+1) + 12D per launch of the dominant kernel (SURVEY.md §8(d)), "
+                    "divided by its time from HIP events on its stream; frac > 1 would flag cache reuse. "
+                    "traffic = HBM-side bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, "
+                    "profiles/pmc_<kernel>.json) when collected; see DESIGN.md §4",
         },
         "cpu_baseline": None,
     }
-    if world > 1 and args.exchange == "records":
-        out["config"]["exchange"] = {
-            "mode": "pair records to owner(a) = a mod N: all-gather of u16 histories + all-to-all of 8-B "
-                    "descriptors; owners reduce complete rows (no partial counts, no merge)",
-            "records_sent_rank0": res.sent_records, "records_recv_rank0": res.recv_records,
-            "arena_bytes_per_rank": 2 * res.arena_stride, "global_ordered_pairs_per_step": res.observed}
-    elif world > 1:
-        out["config"]["exchange"] = {"mode": "partial rows to owner(a) = a mod N, owner merge",
-                                     "entries_sent_rank0": res.sent_entries, "entries_recv_rank0": res.recv_entries,
-                                     "bytes_per_entry": 8, "global_ordered_pairs_per_step": res.observed}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(up_h, it_h)
+        if args.config == "c3":
+            bu, bi = datagen.c3_users(0, 200_000)
+            out["cpu_baseline"] = cpu_baseline(bu, bi, M, "the same C3 log")
+        else:
+            out["cpu_baseline"] = cpu_baseline(d["user_ptr"], d["items"], M, "the same C2 log")
     if rank == 0:
         print(json.dumps(out), flush=True)
     core.close()

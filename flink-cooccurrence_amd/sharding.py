@@ -135,15 +135,32 @@ def count_records(core, user_ptr, items, group=None, stream=None) -> RecordsResu
     return RecordsResult(rank, world, owned, int(obs.item()), int(local_obs), n, int(sum(recv_h)), stride)
 
 
-def snake_owner(item_counts: torch.Tensor, world: int) -> torch.Tensor:
-    """Row owner map: rows by descending global frequency dealt 0..W-1, W-1..0, 0..W-1, ... (stable,
-    so every rank computes the same map from the same all-reduced counts)."""
+def snake_owner(item_counts: torch.Tensor, world: int, head: int = 4096) -> torch.Tensor:
+    """Row owner map balancing the row work (~ the item's frequency): the `head` most frequent rows
+    are placed greedily on the least loaded rank (largest first), the rest are dealt in snake order
+    (0..W-1, W-1..0, ...).  Deterministic (stable sort, fixed tie order), so every rank computes the
+    same map from the same all-reduced counts."""
+    import heapq
+
     M = item_counts.numel()
     order = torch.argsort(-item_counts, stable=True)
-    pos = torch.arange(M, device=item_counts.device)
-    lap, r = pos // world, pos % world
     owner = torch.empty(M, dtype=torch.int32, device=item_counts.device)
-    owner[order] = torch.where(lap % 2 == 0, r, world - 1 - r).to(torch.int32)
+    h = min(head, M)
+    top = item_counts[order[:h]].cpu().tolist()
+    load = [(0, r) for r in range(world)]
+    heapq.heapify(load)
+    head_own = []
+    for wgt in top:
+        l, r = heapq.heappop(load)
+        head_own.append(r)
+        heapq.heappush(load, (l + int(wgt), r))
+    owner[order[:h]] = torch.tensor(head_own, dtype=torch.int32, device=item_counts.device)
+    # the tail: snake order, starting from the least loaded rank's side
+    pos = torch.arange(M - h, device=item_counts.device)
+    lap, r = pos // world, pos % world
+    rank_by_load = torch.tensor([r_ for _, r_ in sorted(load)], dtype=torch.int64, device=item_counts.device)
+    slot = torch.where(lap % 2 == 0, r, world - 1 - r)
+    owner[order[h:]] = rank_by_load[slot].to(torch.int32)
     return owner
 
 

@@ -129,6 +129,38 @@ class FakeRecordsCore:
         return rows
 
 
+class FakeOwnedCore:
+    """numpy double of cooc_count_device_owned (include/cooc.h): the rows a with owner[a] == part of
+    the closed form over every user given; returns {row: dense counts} plus the owned rows' pairs."""
+
+    def __init__(self, n_items):
+        self.n_items = n_items
+
+    def count_device_owned(self, user_ptr, items, owner, part, item_counts, n_total, stream=None):
+        from oracle import oracle
+
+        M = self.n_items
+        up, it = user_ptr.numpy(), items.numpy()
+        assert int(item_counts.sum()) == n_total == len(it)
+        assert np.array_equal(item_counts.numpy(), np.bincount(it, minlength=M))
+        rp, cols, data, rowsums, _ = oracle.closed_form(up, it, M)
+        own = owner.numpy()
+
+        class R:
+            pass
+
+        r = R()
+        r.rows = {}
+        for a in range(M):
+            if own[a] == part:
+                v = np.zeros(M, np.int64)
+                v[cols[rp[a]:rp[a + 1]]] = data[rp[a]:rp[a + 1]]
+                r.rows[a] = v
+        r.observed = int(sum(rowsums[a] for a in r.rows))
+        r.nnz = int(sum(np.count_nonzero(v) for v in r.rows.values()))
+        return r
+
+
 def _worker(rank, world, port, up_all, it_all, M, out_q, mode="partials"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -146,7 +178,12 @@ def _worker(rank, world, port, up_all, it_all, M, out_q, mode="partials"):
     lo, hi = rank * U // world, (rank + 1) * U // world
     up = up_all[lo:hi + 1] - up_all[lo]
     it = it_all[up_all[lo]:up_all[hi]]
-    if mode == "records":
+    if mode == "owned":
+        res = sharding.count_owned(FakeOwnedCore(M), torch.from_numpy(up), torch.from_numpy(it))
+        rows, rs = res.owned.rows, None
+        owner = res.owner.numpy()
+        assert all(owner[a] == rank for a in rows)
+    elif mode == "records":
         res = sharding.count_records(FakeRecordsCore(M), torch.from_numpy(up), torch.from_numpy(it))
         rows, rs = res.owned, None
     else:
@@ -164,7 +201,21 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,mode", [(2, "partials"), (3, "partials"), (2, "records"), (3, "records")])
+def test_snake_owner_balances_zipf(pkg):
+    """Rows by descending frequency dealt in snake order: Zipf-hot rows land on different ranks and the
+    ranks' frequency mass is close to equal."""
+    from flink_cooccurrence_amd import sharding
+
+    counts = torch.tensor(np.round(1e7 / np.arange(1, 100_001)).astype(np.int64))
+    for W in (2, 4, 8):
+        own = sharding.snake_owner(counts, W).numpy()
+        assert sorted(own[:W].tolist()) == list(range(W))
+        mass = np.bincount(own, weights=counts.numpy(), minlength=W)
+        assert mass.max() / mass.mean() < 1.03
+
+
+@pytest.mark.parametrize("world,mode", [(2, "partials"), (3, "partials"), (2, "records"), (3, "records"), (2, "owned"),
+                                        (3, "owned")])
 def test_count_sharded_gloo(oracle, pkg, world, mode):
     rng = np.random.default_rng(3)
     U, M = 90, 23
@@ -191,7 +242,9 @@ def test_count_sharded_gloo(oracle, pkg, world, mode):
         if rs is not None:
             assert np.array_equal(np.array(rs), rowsums)
         for a, v in rows.items():
-            assert a % world == rank
+            if mode != "owned":
+                assert a % world == rank
             assert np.array_equal(np.array(v), C[a])
+            assert a not in seen
             seen.add(a)
     assert seen == set(range(M))
