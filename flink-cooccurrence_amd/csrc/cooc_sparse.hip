@@ -41,6 +41,13 @@
 #include <cstring>
 #include <vector>
 #include <unistd.h>
+#ifdef COOC_SP_STATS
+#define STAT_CLOCK() wall_clock64()
+#define STAT_ADD(k, v) do { if (threadIdx.x == 0) st_[k] += (v); } while (0)
+#else
+#define STAT_CLOCK() 0ull
+#define STAT_ADD(k, v) do {} while (0)
+#endif
 #ifdef COOC_SP_TRACE
 #define SPT(msg) do { hipStreamSynchronize(s); fprintf(stderr, "[sp] %s\n", msg); } while (0)
 #else
@@ -84,8 +91,9 @@ struct SpArgs {
   const uint32_t *vals;     // contributions: user index, item-sorted
   const int64_t *row_ptr;   // [M + 1] into vals
   const int64_t *up;        // [U + 1] user_ptr
-  const int32_t *tb;        // [U x (T + 1)] tile starts inside each user's list
-  const uint32_t *tarena;   // tile-grouped lists, user u at up[u]
+  const int32_t *tb;        // [U x (T + 1)] padded tile starts inside each user's padded list
+  const int64_t *pbase;     // [U + 1] padded list bases (multiples of 4 ids)
+  const uint32_t *tarena;   // tile-grouped, padded lists: user u at pbase[u]
   const int64_t *row_w;     // [M] pair work W_a = sum of the contributions' list lengths
   const uint64_t *pstart;   // [M] bit t: a chunk starts at tile t
   const uint64_t *pdense;   // [M] bit t: tile t is a dense chunk
@@ -101,6 +109,7 @@ struct SpArgs {
   int32_t *row_nnz;
   int32_t M, T;
   unsigned long long *prog;  // COOC_SP_TRACE: per-workgroup progress in pinned host memory
+  unsigned long long *stats;  // COOC_SP_STATS: per-phase clocks and counts
   int64_t n_contrib, n_users, n_arena;
 };
 
@@ -180,10 +189,12 @@ __device__ inline float est_distinct(const float *est, int t, int64_t W) {
 // ---- planner kernels ------------------------------------------------------------------------------
 // One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
 // item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and regroups the list by
-// column tile: tarena[up[u] + ...] = the list tile by tile, tb[u][t] = offset of tile t (tb[u][T] = n_u).
+// column tile: every (user, tile) segment is padded to a multiple of 4 ids (16 B) with the sink id,
+// tb[u][t] = offset of tile t's segment from the user's padded base, tb[u][T] = plen[u] = the user's
+// padded length (the bases are its prefix; k_sp_scatter fills the arena).
 __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
                                                       const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                      uint32_t *__restrict__ tarena, int32_t *__restrict__ tb,
+                                                      int64_t *__restrict__ plen, int32_t *__restrict__ tb,
                                                       uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                                                       const int32_t *__restrict__ owner, int32_t part,
                                                       int32_t *__restrict__ ownc, PlanTotals *__restrict__ tot) {
@@ -225,23 +236,51 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
       for (int32_t t = 0; t <= T; t++) {
         const int32_t x = c[t];
         c[t] = run;
-        run += x;
+        run += (x + 3) & ~3;
       }
+      plen[j] = run;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  }
+  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
+}
+
+// The padded tile arena: user j's list tile by tile at pbase[j] (a multiple of 4 ids), each tile's
+// segment padded with kSink to a multiple of 4.  One wave per user, tile cursors in LDS.
+constexpr uint32_t kSink = 0xFFFFFFFFu;
+__global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__restrict__ up,
+                                                    const int32_t *__restrict__ items, int32_t M, int32_t T,
+                                                    const int64_t *__restrict__ pbase, const int32_t *__restrict__ tb,
+                                                    uint32_t *__restrict__ tarena) {
+  __shared__ int32_t cur[4][kSpMaxTiles + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t *c = cur[wave];
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up[j];
+    const int32_t n = int32_t(up[j + 1] - s);
+    const int32_t *tbj = tb + j * (T + 1);
+    uint32_t *o = tarena + pbase[j];
+    for (int32_t t = lane; t <= T; t += 64) c[t] = tbj[t];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int32_t p = lane; p < n; p += 64) {
       int32_t it = items[s + p];
-      if (uint32_t(it) >= uint32_t(M)) it = 0;
-      tarena[s + atomicAdd(&c[it >> kTShift], 1)] = uint32_t(it);
+      if (uint32_t(it) >= uint32_t(M)) it = 0;  // (reported by k_sp_partition)
+      o[atomicAdd(&c[it >> kTShift], 1)] = uint32_t(it);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    for (int32_t t = lane; t < T; t += 64)  // pads: from the tile's last id to the next segment
+      for (int32_t q = c[t]; q < tbj[t + 1]; q++) o[q] = kSink;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
-  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
 }
 
 // Owner-filtered contributions (multi-GPU: this part's rows only): user j's owned interactions at
@@ -511,19 +550,20 @@ __device__ inline void sp_apply(const SpShared &L, SpStatic &S_, const WalkOp &o
 // walkers of S lanes (S from the mean segment length) own equal contiguous shares of the batch's
 // virtual range and step S ids at a time, kSpU loads in flight per lane.  Returns early (uniformly)
 // when *flag is raised.
-__device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0, int t1,
-                               bool full, const WalkOp &op) {
+__device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0,
+                                   int t1, bool full, const WalkOp &op) {
+  uint64_t walked = 0;
   const int tid = threadIdx.x;
-  const uint32_t *__restrict__ ar = A.tarena;
+  const uint4 *__restrict__ ar = reinterpret_cast<const uint4 *>(A.tarena);
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
     uint32_t len = 0;
     int64_t start = 0;
     if (tid < nb) {
       const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] : 0u;
-      const int64_t base = BCHK(A, u < A.n_users, 2) ? A.up[u] : 0;
+      const int64_t base = BCHK(A, u < A.n_users, 2) ? A.pbase[u] : 0;
       if (full) {
-        len = uint32_t(A.up[u + 1] - base);
+        len = uint32_t(A.pbase[u + 1] - base);
         start = base;
       } else {
         const int32_t *tbu = A.tb + int64_t(u) * (A.T + 1);
@@ -532,12 +572,15 @@ __device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_,
         len = okt ? uint32_t(tbu[t1] - s0) : 0u;
         start = base + s0;
       }
+      len >>= 2;     // in 4-id groups (16 B)
+      start >>= 2;
     }
     uint32_t total;
     const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
     if (total == 0) continue;  // uniform (scalar branch): no barrier is skipped by part of the block
+    walked += total;
     const uint32_t mean = total / uint32_t(nb);
-    const uint32_t S = mean >= 48 ? 64u : mean >= 12 ? 16u : 4u;
+    const uint32_t S = mean >= 12 ? 16u : 4u;
     const uint32_t nW = kSpThreads / S;
     if (tid < nb) {
       L.vst[tid] = ex;
@@ -557,7 +600,7 @@ __device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_,
       int32_t cur = L.qstart[q];
       uint32_t next = L.vst[cur + 1];
       int64_t base = L.seg[cur];
-      uint32_t v[kSpU] = {};
+      uint4 v[kSpU] = {};
       bool ok[kSpU];
 #pragma unroll
       for (int k = 0; k < kSpU; k++) {
@@ -569,11 +612,11 @@ __device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_,
             next = L.vst[cur + 1];
             base = L.seg[cur];
           }
-          v[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_arena, 8) ? ar[base + gk] : 0u;
+          v[k] = BCHK(A, base + gk >= 0 && 4 * (base + gk) < A.n_arena, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
         }
       }
       for (; g < hi; g += S * kSpU) {
-        uint32_t vn[kSpU] = {};
+        uint4 vn[kSpU] = {};
         bool okn[kSpU];
 #pragma unroll
         for (int k = 0; k < kSpU; k++) {
@@ -585,12 +628,17 @@ __device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_,
               next = L.vst[cur + 1];
               base = L.seg[cur];
             }
-            vn[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_arena, 16) ? ar[base + gk] : 0u;
+            vn[k] = BCHK(A, base + gk >= 0 && 4 * (base + gk) < A.n_arena, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
           }
         }
 #pragma unroll
         for (int k = 0; k < kSpU; k++)
-          if (ok[k]) sp_apply(L, S_, op, v[k]);
+          if (ok[k]) {
+            if (v[k].x != kSink) sp_apply(L, S_, op, v[k].x);
+            if (v[k].y != kSink) sp_apply(L, S_, op, v[k].y);
+            if (v[k].z != kSink) sp_apply(L, S_, op, v[k].z);
+            if (v[k].w != kSink) sp_apply(L, S_, op, v[k].w);
+          }
 #pragma unroll
         for (int k = 0; k < kSpU; k++) {
           v[k] = vn[k];
@@ -601,6 +649,7 @@ __device__ inline void sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_,
     __syncthreads();
     if (uni(S_.flag)) break;
   }
+  return walked;
 }
 
 // Output space for n more entries of the current row (thread-uniform call).  Moves the row's
@@ -814,6 +863,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     S_.flag = 0u;
   }
   const int64_t n_work = A.tot->n_chunks;
+#ifdef COOC_SP_STATS
+  unsigned long long st_[16] = {};
+  const unsigned long long t_start = STAT_CLOCK();
+#endif
   __syncthreads();
   for (;;) {
     if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -873,8 +926,14 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         S_.claims = 0u;
       }
       __syncthreads();
-      sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+      const unsigned long long c_walk = STAT_CLOCK();
+      const uint64_t walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+      const unsigned long long c_walked = STAT_CLOCK();
+      STAT_ADD(split ? 4 : dense ? 0 : 1, c_walked - c_walk);
+      STAT_ADD(dense ? 9 : 10, walked);
+      STAT_ADD(dense ? 5 : 6, 1);
       if (!dense && uni(S_.flag)) {
+        STAT_ADD(H < kHashMax ? 7 : 8, 1);
         // overflow: clear the table; retry with a 4x table, at the largest size as dense tiles
         for (int32_t j = tid; j < H; j += kSpThreads) {
           L.R[j] = 0u;
@@ -904,6 +963,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         if (tid == 0 && a >= c0 && a < c1) L.R[a - c0] -= self;
         __syncthreads();
         sp_dense_compact(A, L, S_, c1 - c0, c0);
+        STAT_ADD(2, STAT_CLOCK() - c_walked);
       } else {
         if (tid == 0 && a >= c0 && a < c1) {
           uint32_t h = (uint32_t(a) * 0x9E3779B1u) >> op.hshift;
@@ -917,15 +977,24 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         }
         __syncthreads();
         sp_hash_compact(A, L, S_, H, c0, c1);
+        STAT_ADD(3, STAT_CLOCK() - c_walked);
+        STAT_ADD(14, H);
       }
       t = t1;
       H = 0;
     }
+    STAT_ADD(split ? 12 : 11, 1);
     if (!split && tid == 0) {
       A.row_base[a] = S_.row_n ? S_.row_begin : 0;
       A.row_nnz[a] = int32_t(S_.row_n);
     }
   }
+#ifdef COOC_SP_STATS
+  if (tid == 0) {
+    st_[13] = STAT_CLOCK() - t_start;
+    for (int k = 0; k < 16; k++) atomicAdd(A.stats + k, st_[k]);
+  }
+#endif
 }
 
 // Split rows: the staging row (self term applied on the fly) compacted in column order into an
@@ -1045,7 +1114,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
-  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * (n1 + 4)));
+  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(4 * n1 + 16)));  // padded: <= 4 ids per id
+  COOC_TRY(sp_pbase_.reserve(sizeof(int64_t) * size_t(2 * U1 + 2)));    // plen [U], pbase [U + 1]
   COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 1)));
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
@@ -1084,6 +1154,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   tmp = std::max(tmp, q);
   COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, q, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), M, s));
   tmp = std::max(tmp, q);
+  int64_t *plen = sp_pbase_.as<int64_t>(), *pbase = plen + U1;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, pbase + 1, int(U1), s));
+  tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
 
   // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
@@ -1093,9 +1166,16 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
   }
   if (U > 0) {
-    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_arena_.as<uint32_t>(),
-                                                           sp_tb_.as<int32_t>(), keys_in, vals_in, owner, part,
-                                                           sp_ownc_.as<int32_t>(), tot);
+    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, sp_tb_.as<int32_t>(), keys_in,
+                                                           vals_in, owner, part, sp_ownc_.as<int32_t>(), tot);
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(int64_t), s));
+  if (U > 0) {
+    size_t b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
+    k_sp_scatter<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, pbase, sp_tb_.as<int32_t>(),
+                                                         sp_arena_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows
@@ -1199,10 +1279,11 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   dense_mode_ = false;
   last_rows_ = M;
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
-  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(), sp_arena_.as<uint32_t>(),
+  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(), pbase,
+                     sp_arena_.as<uint32_t>(),
                      sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(), sp_pdense_.as<uint64_t>(), est, nullptr,
                      split_slot_.as<int32_t>(), nullptr, nullptr, bump_.as<unsigned long long>(), 0, slab,
-                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, n_c, U, n};
+                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, nullptr, n_c, U, 4 * n1 + 16};
   COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    kSpLds));
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1224,6 +1305,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     prog[1536] = 0;
     A.prog = prog;
     fprintf(stderr, "[sp] n_work %lld cap %lld slab %lld est %lld bound %lld\n", (long long)n_work, (long long)cap, (long long)slab, (long long)est_nnz, (long long)bound);
+#endif
+#ifdef COOC_SP_STATS
+    static unsigned long long *d_stats = nullptr;
+    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 16 * 8);
+    hipMemsetAsync(d_stats, 0, 16 * 8, s);
+    A.stats = d_stats;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     if (n_work > 0) {
@@ -1267,6 +1354,18 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     int64_t err = 0;
     COOC_HIP_TRY(hipMemcpyAsync(&err, &tot->err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     COOC_HIP_TRY(hipStreamSynchronize(s));
+#ifdef COOC_SP_STATS
+    {
+      unsigned long long h[16];
+      hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
+      const double g = double(std::min<int64_t>(n_work, n_cu_));
+      fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
+              "compact hash %.0f | chunks dense %llu hash %llu retries %llu fallbacks %llu | pairs dense %.3g hash %.3g | "
+              "rows %llu split items %llu | mean H %.0f\n",
+              h[13] / 100.0 / g, h[0] / 100.0 / g, h[1] / 100.0 / g, h[4] / 100.0 / g, h[2] / 100.0 / g, h[3] / 100.0 / g,
+              h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0);
+    }
+#endif
     if (!(err & 4) || cap >= bound + slack) break;
     // the expected key count was too low: rerun into a region of the exact bound
     size_t f2 = 0, t2 = 0;

@@ -16,7 +16,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_k_acc_batch.json"
 vals = collections.defaultdict(list)
 kernel = None
-for f in sorted(glob.glob(os.path.join(root, "p*", "pmc_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         kernel = (__import__("re").search(r"(k_\w+)", r["Kernel_Name"]) or [None, r["Kernel_Name"]])[1]
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
