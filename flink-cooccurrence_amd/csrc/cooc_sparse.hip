@@ -71,15 +71,17 @@ constexpr int kSpDb = 512;                             // contribution descripto
 constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
 constexpr int kSpU = 4;                                // partner loads in flight per lane
 constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
-constexpr int64_t kSplitWork = int64_t(1) << 25;       // rows above this pair work are split
+constexpr int64_t kSplitWork = int64_t(1) << 23;       // rows above this pair work are split
 constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
+constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups)
+constexpr int kGatherMinChunks = 3;                    // rows with this many chunks gather their tails
 constexpr float kHashFill = 0.5f * kHashMax;           // expected distinct keys per hash chunk
 constexpr float kDensePairs = 65536.f;                 // a tile with more expected pairs is dense
 constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + 256 * 4;
 
 struct SpWork {
   int32_t row;
-  int32_t tile;  // < 0: the whole row (chunk plan from pstart / pdense); else a split work item
+  int32_t tile;  // -1: the whole row (chunk plan from pstart / pdense); -2: a share of a split row
   int32_t sub;   // contribution share sub of nsub
   int32_t nsub;
 };
@@ -92,8 +94,7 @@ struct SpArgs {
   const int64_t *row_ptr;   // [M + 1] into vals
   const int64_t *up;        // [U + 1] user_ptr
   const int32_t *tb;        // [U x (T + 1)] padded tile starts inside each user's padded list
-  const int64_t *pbase;     // [U + 1] padded list bases (multiples of 4 ids)
-  const uint32_t *tarena;   // tile-grouped, padded lists: user u at pbase[u]
+  const uint4 *tarena;      // tile-grouped, padded lists in 16-B groups
   const int64_t *row_w;     // [M] pair work W_a = sum of the contributions' list lengths
   const uint64_t *pstart;   // [M] bit t: a chunk starts at tile t
   const uint64_t *pdense;   // [M] bit t: tile t is a dense chunk
@@ -110,7 +111,9 @@ struct SpArgs {
   int32_t M, T;
   unsigned long long *prog;  // COOC_SP_TRACE: per-workgroup progress in pinned host memory
   unsigned long long *stats;  // COOC_SP_STATS: per-phase clocks and counts
-  int64_t n_contrib, n_users, n_arena;
+  int64_t n_contrib, n_users, n_groups;
+  uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
+  int64_t scr_cap;          // 0: gather mode off
 };
 
 #ifdef COOC_SP_TRACE
@@ -186,12 +189,19 @@ __device__ inline float est_distinct(const float *est, int t, int64_t W) {
   return lo + f * (hi - lo);
 }
 
+// Work items of a split row: shares of about kSubWork pairs whose expected tails (the pairs outside
+// tile 0, mass 1 - g0) fit a gather scratch.
+__device__ inline int32_t sp_split_shares(int64_t W, float g0) {
+  const float tail = float(W) * fmaxf(0.f, 1.f - g0);
+  return max(int32_t((W + kSubWork - 1) / kSubWork), int32_t(ceilf(tail / float(kScrGroups))));
+}
+
 // ---- planner kernels ------------------------------------------------------------------------------
 // One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
 // item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and regroups the list by
 // column tile: every (user, tile) segment is padded to a multiple of 4 ids (16 B) with the sink id,
 // tb[u][t] = offset of tile t's segment from the user's padded base, tb[u][T] = plen[u] = the user's
-// padded length (the bases are its prefix; k_sp_scatter fills the arena).
+// padded length (the bases are its prefix; k_sp_scatter fills the arena and makes tb absolute).
 __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
                                                       const int32_t *__restrict__ items, int32_t M, int32_t T,
                                                       int64_t *__restrict__ plen, int32_t *__restrict__ tb,
@@ -250,11 +260,13 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
 }
 
 // The padded tile arena: user j's list tile by tile at pbase[j] (a multiple of 4 ids), each tile's
-// segment padded with kSink to a multiple of 4.  One wave per user, tile cursors in LDS.
+// segment padded with kSink to a multiple of 4.  One wave per user, tile cursors in LDS.  Leaves
+// tb[j][t] = the absolute 16-B group index of tile t's segment (tb[j][T] = the end of j's list), so
+// that a walk needs one descriptor line per user.
 constexpr uint32_t kSink = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__restrict__ up,
                                                     const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                    const int64_t *__restrict__ pbase, const int32_t *__restrict__ tb,
+                                                    const int64_t *__restrict__ pbase, int32_t *__restrict__ tb,
                                                     uint32_t *__restrict__ tarena) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -278,6 +290,10 @@ __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__
     __builtin_amdgcn_wave_barrier();
     for (int32_t t = lane; t < T; t += 64)  // pads: from the tile's last id to the next segment
       for (int32_t q = c[t]; q < tbj[t + 1]; q++) o[q] = kSink;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int32_t *tbw = tb + j * (T + 1);
+    for (int32_t t = lane; t <= T; t += 64) tbw[t] = int32_t((pbase[j] + tbw[t]) >> 2);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
@@ -375,7 +391,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
                                                  PlanTotals *__restrict__ tot) {
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0;
+  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -393,12 +409,10 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
       float e_tot = 0.f;
       if (W > kSplitWork) {
         n_split = 1;
-        for (int t = 0; t < T; t++) {
-          e_tot += est_distinct(est, t, W);
-          const float g = gmass[t];
-          if (g > 0.f) nw += max(1, int32_t(ceilf(float(W) * g / float(kSubWork))));
-        }
+        for (int t = 0; t < T; t++) e_tot += est_distinct(est, t, W);
+        nw = sp_split_shares(W, gmass[0]);
         split_work = uint64_t(nw);
+        max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]) / float(nw));
       } else {
         float cur = 0.f;
         int n_in = 0;
@@ -422,6 +436,10 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
             n_in++;
           }
         }
+        if (T < 64 && (dn & 1ull) && __popcll(st) >= kGatherMinChunks) {  // gather mode (k_sp_main)
+          dn |= uint64_t(1) << 63;
+          max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]));
+        }
       }
       est_sum = uint64_t(e_tot) + 1;
     }
@@ -436,7 +454,11 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     if (lane == 0) s_red[i][w] = v[i];
   }
   uint64_t act = n_active;
-  for (int o = 32; o > 0; o >>= 1) act += __shfl_xor(act, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    act += __shfl_xor(act, o, 64);
+    max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
+  }
+  if (lane == 0 && max_tail) atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_tail), (unsigned long long)max_tail);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t r[4];
@@ -470,13 +492,9 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
   if (r < n_split) {
     split_slot[a] = r;
     split_row[r] = a;
-    int64_t q = wbase[r];
-    for (int t = 0; t < T; t++) {
-      const float g = gmass[t];
-      if (g <= 0.f) continue;
-      const int32_t ns = max(1, int32_t(ceilf(float(W) * g / float(kSubWork))));
-      for (int32_t s = 0; s < ns; s++) queue[q++] = SpWork{a, t, s, ns};
-    }
+    const int64_t q = wbase[r];
+    const int32_t ns = sp_split_shares(W, gmass[0]);
+    for (int32_t s = 0; s < ns; s++) queue[q + s] = SpWork{a, -2, s, ns};
   } else {
     queue[n_split_work + (r - n_split)] = SpWork{a, -1, 0, 0};
   }
@@ -506,6 +524,9 @@ struct SpStatic {
   uint32_t flag, claims;
   int64_t slab_cur, slab_end, row_begin, row_n, pos, copy_from, copy_n;
   float dt[kSpMaxTiles];
+  uint32_t bcnt[kSpMaxTiles];       // gather mode: tail groups per tile
+  uint32_t bstart[kSpMaxTiles + 1]; // ... their bucket starts in the workgroup's scratch
+  uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
 };
 
 // Insert one partner id into the LDS table (keys store id + 1; 0 = empty).  Linear probing from a
@@ -534,8 +555,9 @@ __device__ inline void sp_hash_insert(uint32_t *keys, uint32_t *cnts, uint32_t i
 }
 
 struct WalkOp {
-  int mode;  // 0: dense counters R[id - c0]; 1: hash insert
+  int mode;  // 0: dense counters R[id - c0]; 1: hash insert; 2: gather (tile 0 dense, other tiles to buckets)
   uint32_t c0, hshift, hmask, limit;
+  int64_t sbase;  // gather: the workgroup's scratch
 };
 
 __device__ inline void sp_apply(const SpShared &L, SpStatic &S_, const WalkOp &op, uint32_t id) {
@@ -543,6 +565,30 @@ __device__ inline void sp_apply(const SpShared &L, SpStatic &S_, const WalkOp &o
     atomicAdd(&L.R[id - op.c0], 1u);
   else
     sp_hash_insert(L.R, L.R + kHashMax, id, op.hshift, op.hmask, op.limit, S_);
+}
+
+// One 16-B group of partner ids (one tile's; kSink pads).  Gather mode: a group of tile 0 is counted
+// in the dense tile, any other is appended to its tile's bucket in the workgroup's scratch.
+__device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStatic &S_, const WalkOp &op,
+                                      const uint4 &v) {
+  if (v.x == kSink) return;  // (the first id of a group is never a pad)
+  if (op.mode == 2) {
+    const uint32_t t = v.x >> kTShift;
+    if (t == 0) {
+      atomicAdd(&L.R[v.x], 1u);
+      if (v.y != kSink) atomicAdd(&L.R[v.y], 1u);
+      if (v.z != kSink) atomicAdd(&L.R[v.z], 1u);
+      if (v.w != kSink) atomicAdd(&L.R[v.w], 1u);
+    } else {
+      const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
+      A.scratch[op.sbase + S_.bstart[t] + slot] = v;
+    }
+    return;
+  }
+  sp_apply(L, S_, op, v.x);
+  if (v.y != kSink) sp_apply(L, S_, op, v.y);
+  if (v.z != kSink) sp_apply(L, S_, op, v.z);
+  if (v.w != kSink) sp_apply(L, S_, op, v.w);
 }
 
 // Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
@@ -554,26 +600,18 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
   const int tid = threadIdx.x;
-  const uint4 *__restrict__ ar = reinterpret_cast<const uint4 *>(A.tarena);
+  const uint4 *__restrict__ ar = A.tarena;
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
     uint32_t len = 0;
     int64_t start = 0;
-    if (tid < nb) {
+    if (tid < nb) {  // the segment of tiles [t0, t1) (full: the whole list) in 16-B groups
       const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] : 0u;
-      const int64_t base = BCHK(A, u < A.n_users, 2) ? A.pbase[u] : 0;
-      if (full) {
-        len = uint32_t(A.pbase[u + 1] - base);
-        start = base;
-      } else {
-        const int32_t *tbu = A.tb + int64_t(u) * (A.T + 1);
-        const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
-        const int32_t s0 = okt ? tbu[t0] : 0;
-        len = okt ? uint32_t(tbu[t1] - s0) : 0u;
-        start = base + s0;
-      }
-      len >>= 2;     // in 4-id groups (16 B)
-      start >>= 2;
+      const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
+      const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
+      const int32_t s0 = okt ? tbu[full ? 0 : t0] : 0;
+      len = okt ? uint32_t(tbu[full ? A.T : t1] - s0) : 0u;
+      start = s0;
     }
     uint32_t total;
     const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
@@ -612,7 +650,7 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
             next = L.vst[cur + 1];
             base = L.seg[cur];
           }
-          v[k] = BCHK(A, base + gk >= 0 && 4 * (base + gk) < A.n_arena, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
+          v[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_groups, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
         }
       }
       for (; g < hi; g += S * kSpU) {
@@ -628,17 +666,12 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
               next = L.vst[cur + 1];
               base = L.seg[cur];
             }
-            vn[k] = BCHK(A, base + gk >= 0 && 4 * (base + gk) < A.n_arena, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
+            vn[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_groups, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
           }
         }
 #pragma unroll
         for (int k = 0; k < kSpU; k++)
-          if (ok[k]) {
-            if (v[k].x != kSink) sp_apply(L, S_, op, v[k].x);
-            if (v[k].y != kSink) sp_apply(L, S_, op, v[k].y);
-            if (v[k].z != kSink) sp_apply(L, S_, op, v[k].z);
-            if (v[k].w != kSink) sp_apply(L, S_, op, v[k].w);
-          }
+          if (ok[k]) sp_apply_group(A, L, S_, op, v[k]);
 #pragma unroll
         for (int k = 0; k < kSpU; k++) {
           v[k] = vn[k];
@@ -650,6 +683,69 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
     if (uni(S_.flag)) break;
   }
   return walked;
+}
+
+// Walk n contiguous groups of the workgroup's scratch (a gathered tile range), applying op (0 or 1)
+// to every id; kSpU loads in flight per thread.  Ends with a barrier.
+__device__ inline void sp_walk_range(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t g0, uint32_t n,
+                                     const WalkOp &op) {
+  const uint4 *__restrict__ src = A.scratch + g0;
+  const uint4 sink = make_uint4(kSink, kSink, kSink, kSink);
+  for (uint32_t g = threadIdx.x; g < n; g += kSpThreads * kSpU) {
+    uint4 v[kSpU];
+#pragma unroll
+    for (int k = 0; k < kSpU; k++) {
+      const uint32_t gk = g + k * kSpThreads;
+      v[k] = gk < n ? src[gk] : sink;
+    }
+#pragma unroll
+    for (int k = 0; k < kSpU; k++) sp_apply_group(A, L, S_, op, v[k]);
+  }
+  __syncthreads();
+}
+
+// Gather mode, pass 1: the tail groups (tiles 1 .. T-1) of contributions [k0, k1), per tile, from the
+// users' descriptor lines (lanes = tiles, two users per wave when T < 32), scanned into bucket starts
+// S_.bstart[1 .. T] with zero cursors.  Returns the total (uniform).  Requires T < 64.
+__device__ inline uint32_t sp_tail_sizes(const SpArgs &A, SpStatic &S_, int64_t k0, int64_t k1) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = A.T;
+  if (tid < kSpMaxTiles) S_.bcnt[tid] = 0u;
+  __syncthreads();
+  const bool half = T < 32;
+  const int per = half ? 2 : 1, sub = half ? lane >> 5 : 0, t = half ? lane & 31 : lane;
+  const int width = half ? 32 : 64;
+  const int64_t step = int64_t(kSpWaves) * per;
+  constexpr int kU = 4;
+  uint32_t acc = 0;
+  for (int64_t kb = k0 + wave * per; kb < k1; kb += step * kU) {  // uniform per wave
+    uint32_t x[kU];
+#pragma unroll
+    for (int j = 0; j < kU; j++) {
+      const int64_t k = kb + sub + j * step;
+      const uint32_t u = k < k1 ? A.vals[k] : ~0u;
+      x[j] = (u != ~0u && t <= T) ? uint32_t(A.tb[int64_t(u) * (T + 1) + t]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kU; j++) {
+      const uint32_t nx = __shfl_down(x[j], 1, width);
+      if (t >= 1 && t < T) acc += nx - x[j];
+    }
+  }
+  if (half) acc += __shfl_down(acc, 32, 64);
+  if (t >= 1 && t < T && (!half || lane < 32)) atomicAdd(&S_.bcnt[t], acc);
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t c = lane >= 1 && lane < T ? S_.bcnt[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(c);
+    if (lane < T) {
+      S_.bstart[lane] = inc - c;
+      S_.bcur[lane] = 0u;
+    }
+    if (lane == T - 1) S_.bstart[T] = inc;
+  }
+  __syncthreads();
+  return uni(S_.bstart[T]);
 }
 
 // Output space for n more entries of the current row (thread-uniform call).  Moves the row's
@@ -876,19 +972,21 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     const SpWork it = A.queue[w];
     const int32_t a = it.row;
     const int64_t r0 = A.row_ptr[a], r1 = A.row_ptr[a + 1];
-    const bool split = it.tile >= 0;
+    const bool split = it.tile == -2;  // a share of a split row's contributions, every tile, into staging
     int64_t k0 = r0, k1 = r1;
-    int t = 0, t_end = A.T;
+    int t = 0;
+    const int t_end = A.T;
     uint64_t st = 0, dn = 0;
-    if (split) {  // tile `tile` of a share of the row's contributions
+    bool gather = false;
+    if (split) {
       k0 = r0 + (r1 - r0) * it.sub / it.nsub;
       k1 = r0 + (r1 - r0) * (it.sub + 1) / it.nsub;
-      t = it.tile;
-      t_end = t + 1;
+      gather = A.scr_cap > 0;
     } else {
       const int64_t W = A.row_w[a];
       st = A.pstart[a];
       dn = A.pdense[a];
+      gather = A.scr_cap > 0 && ((dn >> 63) & 1ull);  // (bit 63: the planner's gather mark, T < 64)
       if (tid < A.T) S_.dt[tid] = est_distinct(A.est, tid, W);
       if (tid == 0) {
         S_.row_begin = S_.slab_cur;
@@ -896,6 +994,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       }
       __syncthreads();  // dt[] is read by every thread below
     }
+    // gather mode (rows with many chunks, split shares): the lists are walked once; tile 0 is counted
+    // on the way and every other tile's groups go to a bucket that its chunk then reads contiguously
+    // (instead of one walk of every contribution per chunk).  Off when the tails exceed the scratch.
+    if (uni(uint32_t(gather))) gather = uni(uint32_t(sp_tail_sizes(A, S_, k0, k1) <= uint32_t(A.scr_cap))) != 0u;
     int dense_until = split ? t_end : -1;  // tiles below it go dense (split items; hash overflow fallback)
     int32_t H = 0;                         // 0: table size from the estimate
     while (t < t_end) {
@@ -927,7 +1029,18 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       }
       __syncthreads();
       const unsigned long long c_walk = STAT_CLOCK();
-      const uint64_t walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+      op.sbase = int64_t(blockIdx.x) * A.scr_cap;
+      uint64_t walked;
+      if (gather && t == 0) {  // tile 0 (a dense chunk) counted, the other tiles' groups to their buckets
+        op.mode = 2;
+        walked = sp_walk(A, L, S_, k0, k1, 0, A.T, true, op);
+      } else if (gather) {     // a gathered tile range: contiguous in the scratch
+        const uint32_t g0 = uni(S_.bstart[t]), g1 = uni(S_.bstart[t1]);
+        sp_walk_range(A, L, S_, op.sbase + g0, g1 - g0, op);
+        walked = g1 - g0;
+      } else {
+        walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+      }
       const unsigned long long c_walked = STAT_CLOCK();
       STAT_ADD(split ? 4 : dense ? 0 : 1, c_walked - c_walk);
       STAT_ADD(dense ? 9 : 10, walked);
@@ -1267,6 +1380,17 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
     COOC_TRY(staging_.reserve(need));
   }
+  // gather scratch: a bucket region per workgroup for the largest expected tail (+25%); a work item
+  // whose exact tail is larger walks per chunk instead.  Skipped when memory is short.
+  const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_work, 1), n_cu_);
+  int64_t scr_cap = 0;
+  if (h_tot_->max_tail > 0 && T < 64) {
+    scr_cap = std::min<int64_t>(kScrGroups, h_tot_->max_tail + h_tot_->max_tail / 4 + 4096);
+    const size_t need = sizeof(uint4) * size_t(grid) * size_t(scr_cap);
+    size_t f0 = 0, t0 = 0;
+    COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
+    if (need > sp_scr_.cap && (need > (f0 + sp_scr_.cap) / 4 || !sp_scr_.reserve(need).ok())) scr_cap = 0;
+  }
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -1279,11 +1403,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   dense_mode_ = false;
   last_rows_ = M;
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
-  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(), pbase,
-                     sp_arena_.as<uint32_t>(),
+  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(),
+                     sp_arena_.as<uint4>(),
                      sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(), sp_pdense_.as<uint64_t>(), est, nullptr,
                      split_slot_.as<int32_t>(), nullptr, nullptr, bump_.as<unsigned long long>(), 0, slab,
-                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, nullptr, n_c, U, 4 * n1 + 16};
+                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, nullptr, n_c, U, n1 + 4,
+                     scr_cap ? sp_scr_.as<uint4>() : nullptr, scr_cap};
   COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    kSpLds));
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1314,7 +1439,6 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     if (n_work > 0) {
-      const int64_t grid = std::min<int64_t>(n_work, n_cu_);
       k_sp_main<<<unsigned(grid), kSpThreads, kSpLds, s>>>(A);
       COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_TRACE

@@ -1,0 +1,206 @@
+"""The large-universe path (n_items >= 40,320: cooc_sparse.hip) against the closed form and against
+rows summed directly from the users' lists.  Needs an MI355X.
+
+Covers every chunk kind of k_sp_main: hash chunks, dense tiles, gather mode (rows of many chunks whose
+tails go through the per-workgroup buckets), split rows (shares of a row's contributions into a staging
+row, finalize with the uint32 overflow check), and the C3 log itself at 1/64 of the 1B-interaction
+config through size-independent properties (observed == P, sum of row sums == P, symmetry of sampled
+entries, sorted keys) plus exact sampled rows.  Bar: bit-exact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _d2h(ptr, n, dtype, offset=0):
+    out = np.zeros(n, dtype)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        src = ctypes.c_void_p(ptr + offset * out.itemsize)
+        assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), src, ctypes.c_size_t(out.nbytes), ctypes.c_int(2)) == 0
+    return out
+
+
+class _Rows:
+    """Rows of a count_device result, read back one at a time."""
+
+    def __init__(self, res, M):
+        self.res, self.M = res, M
+        self.base = _d2h(res.row_base, M, np.int64)
+        self.nnz = _d2h(res.row_nnz, M, np.int32)
+        self.rowsum = _d2h(res.rowsum, M, np.int64)
+
+    def row(self, a):
+        n, b = int(self.nnz[a]), int(self.base[a])
+        return _d2h(self.res.col, n, np.int32, b), _d2h(self.res.cnt, n, np.uint32, b).astype(np.int64)
+
+
+class _Brute:
+    """C[a, :] = sum over the users u holding a of m_u(a) * (u's list as counts), minus m_u(a) at a
+    (NonSampled...java:129-161 summed per row; the closed form of SURVEY.md §0.3 restricted to a)."""
+
+    def __init__(self, up, it, M):
+        self.up, self.it, self.M = np.asarray(up, np.int64), np.asarray(it, np.int64), M
+        self.lens = np.diff(self.up)
+        self.users = np.repeat(np.arange(len(self.lens)), self.lens)
+        self.order = np.argsort(self.it, kind="stable")
+        self.sorted = self.it[self.order]
+
+    def row(self, a):
+        lo, hi = np.searchsorted(self.sorted, [a, a + 1])
+        us, mult = np.unique(self.users[self.order[lo:hi]], return_counts=True)
+        if len(us) == 0:
+            return np.zeros(0, np.int32), np.zeros(0, np.int64)
+        starts, lens = self.up[us], self.lens[us]
+        idx = np.repeat(starts - np.cumsum(np.concatenate([[0], lens[:-1]])), lens) + np.arange(lens.sum())
+        row = np.bincount(self.it[idx], weights=np.repeat(mult, lens).astype(np.float64), minlength=self.M)
+        row = np.rint(row).astype(np.int64)
+        row[a] -= int(mult.sum())
+        nz = np.nonzero(row)[0]
+        return nz.astype(np.int32), row[nz]
+
+
+def _structured_log(U=20_000, F=200, K=100, R=300, M=300_000, seed=11):
+    """Users hold the shared items 0..F-1 (rows of U * ~(F + R) > 2^23 pairs: split rows), every third
+    user also K medium items F..F+K-1 (rows of ~4e6 pairs, tile 0 dense plus ~8 dense tail tiles:
+    gather mode), and R random tail items (with replacement) in [32768, M)."""
+    rng = np.random.default_rng(seed)
+    lists = []
+    for u in range(U):
+        parts = [np.arange(F), rng.integers(32768, M, R)]
+        if u % 3 == 0:
+            parts.append(np.arange(F, F + K))
+        lists.append(rng.permutation(np.concatenate(parts)))
+    up = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+    return up, np.concatenate(lists).astype(np.int32), M
+
+
+def _check_rows(rows, brute, sample):
+    for a in sample:
+        gc, gn = rows.row(int(a))
+        wc, wn = brute.row(int(a))
+        assert np.array_equal(gc, wc), f"row {a}: key set differs"
+        assert np.array_equal(gn, wn), f"row {a}: counts differ"
+        assert int(gn.sum()) == int(rows.rowsum[a])
+
+
+def test_gather_and_split_rows_vs_brute(pkg, torch_cuda):
+    torch = torch_cuda
+    up, it, M = _structured_log()
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        torch.cuda.current_stream().synchronize()
+        lens = np.diff(up)
+        assert res.observed == int(np.sum(lens * (lens - 1)))
+        rows = _Rows(res, M)
+        assert int(rows.nnz.sum()) == res.nnz
+        assert int(rows.rowsum.sum()) == res.observed
+        brute = _Brute(up, it, M)
+        rng = np.random.default_rng(3)
+        tail = np.unique(it[it >= 32768])
+        sample = np.concatenate([[0, 1, 57, 199], [200, 201, 250, 299], rng.choice(tail, 40, replace=False),
+                                 [300, 32767]])
+        _check_rows(rows, brute, sample)
+
+
+def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda):
+    """The first 1,500 users of the shard-invariant C3 log (1e6 items): the whole CSR vs scipy."""
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.c3_users(0, 1500)
+    M = datagen.C3_ITEMS
+    with pkg.CooccurrenceCore(n_items=M) as core:
+        got = core.count(up, it)
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert got.observed == observed
+    assert np.array_equal(got.row_ptr, rp)
+    assert np.array_equal(got.cols, cols)
+    assert np.array_equal(got.cnt.astype(np.int64), data)
+    assert np.array_equal(got.rowsum, rowsums)
+
+
+def test_c3_sixty_fourth_properties(pkg, torch_cuda):
+    """1/64 of C3 (156,250 users, ~1.6e7 interactions, ~4e9 ordered pairs) generated on the GPU:
+    observed == P and sum(rowsum) == P from the generator's lengths, sum(row_nnz) == nnz, sampled rows
+    sorted and exact (hot, mid and tail items), sampled entries symmetric (C[a, b] == C[b, a])."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    U = datagen.C3_USERS // 64
+    M = datagen.C3_ITEMS
+    dev = torch.device("cuda")
+    up_d, it_d = datagen.c3_users(0, U, device=dev)
+    P = datagen.c3_ordered_pairs(0, U)
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(up_d, it_d)
+        torch.cuda.current_stream().synchronize()
+        assert res.observed == P
+        rows = _Rows(res, M)
+        assert int(rows.rowsum.sum()) == P
+        assert int(rows.nnz.sum()) == res.nnz
+        up, it = up_d.cpu().numpy(), it_d.cpu().numpy()
+        brute = _Brute(up, it, M)
+        rng = np.random.default_rng(5)
+        sample = np.concatenate([[0, 3, 40, 700], rng.integers(1000, 40_000, 8), rng.integers(40_000, M, 24)])
+        _check_rows(rows, brute, sample)
+        # symmetry of sampled entries of sampled rows
+        for a in rng.integers(0, 50_000, 12):
+            ca, na = rows.row(int(a))
+            assert np.all(np.diff(ca) > 0)
+            for j in rng.integers(0, len(ca), min(8, len(ca))):
+                b = int(ca[j])
+                cb, nb = rows.row(b)
+                k = np.searchsorted(cb, a)
+                assert k < len(cb) and cb[k] == a and nb[k] == na[j], f"C[{a},{b}] != C[{b},{a}]"
+
+
+def test_owned_parts_union_is_whole(pkg, torch_cuda):
+    """count_device_owned over 3 parts of a large-universe log on one GPU: every row is counted by
+    exactly its owner and equals the unpartitioned result (the multi-GPU row ownership)."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen, sharding
+
+    up, it = datagen.c3_users(0, 3000)
+    M = datagen.C3_ITEMS
+    dev = torch.device("cuda")
+    up_d, it_d = torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev)
+    freq = np.bincount(it, minlength=M).astype(np.int64)
+    freq_d = torch.from_numpy(freq).to(dev)
+    owner_d = sharding.snake_owner(freq_d, 3)
+    owner = owner_d.cpu().numpy()
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        whole = core.count_device(up_d, it_d)
+        torch.cuda.current_stream().synchronize()
+        w = _Rows(whole, M)
+        want = {a: w.row(a) for a in range(0, M, 997)}
+        want.update({a: w.row(a) for a in range(0, 64)})
+        w_nnz, w_rowsum = w.nnz.copy(), w.rowsum.copy()
+    nnz_total = 0
+    for part in range(3):
+        with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+            res = core.count_device_owned(up_d, it_d, owner_d, part, freq_d, int(len(it)))
+            torch.cuda.current_stream().synchronize()
+            r = _Rows(res, M)
+            mine = owner == part
+            assert np.array_equal(r.nnz[mine], w_nnz[mine])
+            assert np.all(r.nnz[~mine] == 0)
+            assert np.array_equal(r.rowsum[mine], w_rowsum[mine])
+            nnz_total += res.nnz
+            for a, (wc, wn) in want.items():
+                if owner[a] == part:
+                    gc, gn = r.row(a)
+                    assert np.array_equal(gc, wc) and np.array_equal(gn, wn)
+    assert nnz_total == whole.nnz
