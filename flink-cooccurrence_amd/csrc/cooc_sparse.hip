@@ -79,11 +79,15 @@ constexpr float kHashFill = 0.5f * kHashMax;           // expected distinct keys
 constexpr float kDensePairs = 65536.f;                 // a tile with more expected pairs is dense
 constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + 256 * 4;
 
+// One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
 struct SpWork {
+  int64_t k0, k1;   // contribution range (row-sorted)
+  uint64_t st, dn;  // chunk plan: bit t of st = a chunk starts at tile t, of dn = tile t is dense
+  uint64_t hz[2];   // 2 bits per chunk-start tile: its hash table has kHashMin << code slots
   int32_t row;
-  int32_t tile;  // -1: the whole row (chunk plan from pstart / pdense); -2: a share of a split row
-  int32_t sub;   // contribution share sub of nsub
-  int32_t nsub;
+  int32_t kind;     // -1: a whole row; -2: a share of a split row (every tile, into its staging row)
+  int32_t gslot;    // gather mode: row of bucket starts in SpArgs::bst (k_sp_tail_*); -1: none
+  int32_t pad;
 };
 
 struct SpArgs {
@@ -91,14 +95,9 @@ struct SpArgs {
   PlanTotals *tot;
   int32_t *qctr;
   const uint32_t *vals;     // contributions: user index, item-sorted
-  const int64_t *row_ptr;   // [M + 1] into vals
-  const int64_t *up;        // [U + 1] user_ptr
-  const int32_t *tb;        // [U x (T + 1)] padded tile starts inside each user's padded list
+  const int32_t *tb;        // [U x (T + 1)] absolute 16-B group index of each tile segment of a user
   const uint4 *tarena;      // tile-grouped, padded lists in 16-B groups
-  const int64_t *row_w;     // [M] pair work W_a = sum of the contributions' list lengths
-  const uint64_t *pstart;   // [M] bit t: a chunk starts at tile t
-  const uint64_t *pdense;   // [M] bit t: tile t is a dense chunk
-  const float *est;         // [T x kEstK] expected distinct keys per tile
+  const uint32_t *bst;      // [gather slots x (T + 1)] bucket starts of tiles 1 .. T-1 (+ the total)
   uint32_t *staging;        // [n_split x M]
   const int32_t *split_slot;
   int32_t *col_out;
@@ -109,7 +108,7 @@ struct SpArgs {
   int64_t *row_base;
   int32_t *row_nnz;
   int32_t M, T;
-  unsigned long long *prog;  // COOC_SP_TRACE: per-workgroup progress in pinned host memory
+  unsigned long long *prog;   // COOC_SP_TRACE: per-workgroup progress in pinned host memory
   unsigned long long *stats;  // COOC_SP_STATS: per-phase clocks and counts
   int64_t n_contrib, n_users, n_groups;
   uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
@@ -385,13 +384,14 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
                                                  const int64_t *__restrict__ epre, const float *__restrict__ est,
                                                  const float *__restrict__ gmass, int64_t *__restrict__ rowsum,
                                                  int64_t *__restrict__ row_w, uint64_t *__restrict__ pstart,
-                                                 uint64_t *__restrict__ pdense, uint64_t *__restrict__ skey,
+                                                 uint64_t *__restrict__ pdense, uint64_t *__restrict__ hz,
+                                                 uint64_t *__restrict__ skey,
                                                  int32_t *__restrict__ order, int32_t *__restrict__ nwork,
                                                  int32_t *__restrict__ row_nnz, int64_t *__restrict__ row_base,
                                                  PlanTotals *__restrict__ tot) {
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0;
+  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     row_base[a] = 0;
     order[a] = a;
     skey[a] = uint64_t(W);
-    uint64_t st = 0, dn = 0;
+    uint64_t st = 0, dn = 0, h0 = 0, h1 = 0;
     int32_t nw = 0;
     if (c > 0) {
       n_active = 1;
@@ -415,20 +415,28 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
         max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]) / float(nw));
       } else {
         float cur = 0.f;
-        int n_in = 0;
-        bool open = false;
+        int n_in = 0, cs = -1;
+        // a hash chunk's table: the smallest power of two >= 2 E[distinct] + 64 slots (kHashMin..kHashMax)
+        auto close = [&]() {
+          if (cs < 0) return;
+          uint64_t code = 0;
+          for (int H = kHashMin; H < kHashMax && float(H) < 2.f * cur + 64.f; H <<= 1) code++;
+          if (cs < 32) h0 |= code << (2 * cs); else h1 |= code << (2 * (cs - 32));
+          cs = -1;
+        };
         for (int t = 0; t < T; t++) {
           const float d = est_distinct(est, t, W);
           const float e = float(W) * gmass[t];
           e_tot += d;
           if (d > kHashFill || e > kDensePairs) {
+            close();
             st |= uint64_t(1) << t;
             dn |= uint64_t(1) << t;
-            open = false;
           } else {
-            if (!open || cur + d > kHashFill || n_in == kHashMaxTiles) {
+            if (cs < 0 || cur + d > kHashFill || n_in == kHashMaxTiles) {
+              close();
               st |= uint64_t(1) << t;
-              open = true;
+              cs = t;
               cur = 0.f;
               n_in = 0;
             }
@@ -436,15 +444,19 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
             n_in++;
           }
         }
+        close();
         if (T < 64 && (dn & 1ull) && __popcll(st) >= kGatherMinChunks) {  // gather mode (k_sp_main)
           dn |= uint64_t(1) << 63;
           max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]));
+          n_gather = 1;
         }
       }
       est_sum = uint64_t(e_tot) + 1;
     }
     pstart[a] = st;
     pdense[a] = dn;
+    hz[2 * a] = h0;
+    hz[2 * a + 1] = h1;
     nwork[a] = nw;
   }
   uint64_t v[4] = {est_sum, bound, n_split, split_work};
@@ -456,6 +468,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   uint64_t act = n_active;
   for (int o = 32; o > 0; o >>= 1) {
     act += __shfl_xor(act, o, 64);
+    n_gather += __shfl_xor(n_gather, o, 64);
     max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
   }
   if (lane == 0 && max_tail) atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_tail), (unsigned long long)max_tail);
@@ -469,6 +482,8 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     if (r[3]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_split_work), (unsigned long long)r[3]);
   }
   if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
+  if (lane == 0 && n_gather)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_gather_rows), (unsigned long long)n_gather);
 }
 
 __global__ void k_sp_gather_nwork(const int32_t *__restrict__ order, const int32_t *__restrict__ nwork, int32_t M,
@@ -477,10 +492,13 @@ __global__ void k_sp_gather_nwork(const int32_t *__restrict__ order, const int32
   if (r < M) out[r] = nwork[order[r]];
 }
 
-// Work queue: the split rows' work items (they are the heaviest rows, so the first n_split rows of
-// the W-descending order), then every other row with contributions, heaviest first.
+// Work queue: the split rows' shares (they are the heaviest rows, so the first n_split rows of the
+// W-descending order), then every other row with contributions, heaviest first.  Gather items get a
+// row of bucket starts (gslot).
 __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__restrict__ skey,
-                           const int32_t *__restrict__ wbase, const float *__restrict__ gmass, int32_t M, int32_t T,
+                           const int32_t *__restrict__ wbase, const float *__restrict__ gmass,
+                           const int64_t *__restrict__ row_ptr, const uint64_t *__restrict__ pstart,
+                           const uint64_t *__restrict__ pdense, const uint64_t *__restrict__ hz, int32_t M, int32_t T,
                            PlanTotals *__restrict__ tot, SpWork *__restrict__ queue, int32_t *__restrict__ split_slot,
                            int32_t *__restrict__ split_row) {
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -489,14 +507,85 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
   const int32_t a = order[r];
   const int64_t W = int64_t(skey[r]);
   if (W <= 0) return;
+  const int64_t r0 = row_ptr[a], r1 = row_ptr[a + 1];
+  unsigned long long *ng = reinterpret_cast<unsigned long long *>(&tot->n_gather);
   if (r < n_split) {
     split_slot[a] = r;
     split_row[r] = a;
     const int64_t q = wbase[r];
     const int32_t ns = sp_split_shares(W, gmass[0]);
-    for (int32_t s = 0; s < ns; s++) queue[q + s] = SpWork{a, -2, s, ns};
+    for (int32_t s = 0; s < ns; s++) {
+      SpWork x{};
+      x.k0 = r0 + (r1 - r0) * s / ns;
+      x.k1 = r0 + (r1 - r0) * (s + 1) / ns;
+      x.row = a;
+      x.kind = -2;
+      x.gslot = T < 64 ? int32_t(atomicAdd(ng, 1ull)) : -1;
+      queue[q + s] = x;
+    }
   } else {
-    queue[n_split_work + (r - n_split)] = SpWork{a, -1, 0, 0};
+    SpWork x{};
+    x.k0 = r0;
+    x.k1 = r1;
+    x.st = pstart[a];
+    x.dn = pdense[a];
+    x.hz[0] = hz[2 * a];
+    x.hz[1] = hz[2 * a + 1];
+    x.row = a;
+    x.kind = -1;
+    x.gslot = (x.dn >> 63) & 1ull ? int32_t(atomicAdd(ng, 1ull)) : -1;
+    queue[n_split_work + (r - n_split)] = x;
+  }
+}
+
+// Gather mode, bucket sizes: the 16-B groups of tiles 1 .. T-1 over a gather item's contributions,
+// per tile, from the users' descriptor lines (lanes = tiles, two users per wave when T < 32), added
+// into cnt[gslot][t].  Blocks stride over the queue (x) and over 1,024-contribution pieces of an item (y).
+__global__ __launch_bounds__(256) void k_sp_tail_count(const SpWork *__restrict__ queue, int64_t n_work,
+                                                       const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb,
+                                                       int32_t T, uint32_t *__restrict__ cnt) {
+  constexpr int kPiece = 1024, kU = 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool half = T < 32;
+  const int per = half ? 2 : 1, sub = half ? lane >> 5 : 0, t = half ? lane & 31 : lane;
+  const int width = half ? 32 : 64;
+  const int64_t step = int64_t(blockDim.x >> 6) * per;
+  for (int64_t w = blockIdx.x; w < n_work; w += gridDim.x) {
+    const SpWork it = queue[w];
+    if (it.gslot < 0) continue;
+    uint32_t acc = 0;
+    for (int64_t p0 = it.k0 + int64_t(blockIdx.y) * kPiece; p0 < it.k1; p0 += int64_t(gridDim.y) * kPiece) {
+      const int64_t p1 = min(it.k1, p0 + kPiece);
+      for (int64_t kb = p0 + wave * per; kb < p1; kb += step * kU) {  // uniform per wave
+        uint32_t x[kU];
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+          const int64_t k = kb + sub + j * step;
+          const uint32_t u = k < p1 ? vals[k] : ~0u;
+          x[j] = (u != ~0u && t <= T) ? uint32_t(tb[int64_t(u) * (T + 1) + t]) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+          const uint32_t nx = __shfl_down(x[j], 1, width);
+          if (t >= 1 && t < T) acc += nx - x[j];
+        }
+      }
+    }
+    if (half) acc += __shfl_down(acc, 32, 64);
+    if (acc && t >= 1 && t < T && (!half || lane < 32)) atomicAdd(cnt + int64_t(it.gslot) * (T + 1) + t, acc);
+  }
+}
+
+// ... scanned in place into bucket starts (tile 0 has none; entry T = the total).  One wave per slot.
+__global__ void k_sp_tail_scan(const PlanTotals *__restrict__ tot, int32_t T, uint32_t *__restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = tot->n_gather;
+  for (int64_t g = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; g < n; g += (int64_t(gridDim.x) * blockDim.x) >> 6) {
+    uint32_t *row = cnt + g * (T + 1);
+    const uint32_t c = lane >= 1 && lane < T ? row[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(c);
+    if (lane < T) row[lane] = inc - c;
+    if (lane == T - 1) row[T] = inc;
   }
 }
 
@@ -523,9 +612,7 @@ struct SpStatic {
   int32_t work;
   uint32_t flag, claims;
   int64_t slab_cur, slab_end, row_begin, row_n, pos, copy_from, copy_n;
-  float dt[kSpMaxTiles];
-  uint32_t bcnt[kSpMaxTiles];       // gather mode: tail groups per tile
-  uint32_t bstart[kSpMaxTiles + 1]; // ... their bucket starts in the workgroup's scratch
+  uint32_t bstart[kSpMaxTiles + 1]; // gather mode: bucket starts in the workgroup's scratch
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
 };
 
@@ -702,50 +789,6 @@ __device__ inline void sp_walk_range(const SpArgs &A, const SpShared &L, SpStati
     for (int k = 0; k < kSpU; k++) sp_apply_group(A, L, S_, op, v[k]);
   }
   __syncthreads();
-}
-
-// Gather mode, pass 1: the tail groups (tiles 1 .. T-1) of contributions [k0, k1), per tile, from the
-// users' descriptor lines (lanes = tiles, two users per wave when T < 32), scanned into bucket starts
-// S_.bstart[1 .. T] with zero cursors.  Returns the total (uniform).  Requires T < 64.
-__device__ inline uint32_t sp_tail_sizes(const SpArgs &A, SpStatic &S_, int64_t k0, int64_t k1) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = A.T;
-  if (tid < kSpMaxTiles) S_.bcnt[tid] = 0u;
-  __syncthreads();
-  const bool half = T < 32;
-  const int per = half ? 2 : 1, sub = half ? lane >> 5 : 0, t = half ? lane & 31 : lane;
-  const int width = half ? 32 : 64;
-  const int64_t step = int64_t(kSpWaves) * per;
-  constexpr int kU = 4;
-  uint32_t acc = 0;
-  for (int64_t kb = k0 + wave * per; kb < k1; kb += step * kU) {  // uniform per wave
-    uint32_t x[kU];
-#pragma unroll
-    for (int j = 0; j < kU; j++) {
-      const int64_t k = kb + sub + j * step;
-      const uint32_t u = k < k1 ? A.vals[k] : ~0u;
-      x[j] = (u != ~0u && t <= T) ? uint32_t(A.tb[int64_t(u) * (T + 1) + t]) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < kU; j++) {
-      const uint32_t nx = __shfl_down(x[j], 1, width);
-      if (t >= 1 && t < T) acc += nx - x[j];
-    }
-  }
-  if (half) acc += __shfl_down(acc, 32, 64);
-  if (t >= 1 && t < T && (!half || lane < 32)) atomicAdd(&S_.bcnt[t], acc);
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t c = lane >= 1 && lane < T ? S_.bcnt[lane] : 0u;
-    const uint32_t inc = wave_incl_scan(c);
-    if (lane < T) {
-      S_.bstart[lane] = inc - c;
-      S_.bcur[lane] = 0u;
-    }
-    if (lane == T - 1) S_.bstart[T] = inc;
-  }
-  __syncthreads();
-  return uni(S_.bstart[T]);
 }
 
 // Output space for n more entries of the current row (thread-uniform call).  Moves the row's
@@ -963,41 +1006,35 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   unsigned long long st_[16] = {};
   const unsigned long long t_start = STAT_CLOCK();
 #endif
+  if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
   __syncthreads();
   for (;;) {
-    if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
-    __syncthreads();
     const int32_t w = uni(S_.work);
     if (w >= n_work) break;
+    // the next item is dequeued now and read at the end of this one (its latency hides behind the work)
+    uint32_t next = 0;
+    if (tid == 0) next = atomicAdd(A.qctr, 1);
     const SpWork it = A.queue[w];
     const int32_t a = it.row;
-    const int64_t r0 = A.row_ptr[a], r1 = A.row_ptr[a + 1];
-    const bool split = it.tile == -2;  // a share of a split row's contributions, every tile, into staging
-    int64_t k0 = r0, k1 = r1;
+    const bool split = it.kind == -2;  // a share of a split row's contributions, every tile, into staging
+    const int64_t k0 = it.k0, k1 = it.k1;
     int t = 0;
     const int t_end = A.T;
-    uint64_t st = 0, dn = 0;
-    bool gather = false;
-    if (split) {
-      k0 = r0 + (r1 - r0) * it.sub / it.nsub;
-      k1 = r0 + (r1 - r0) * (it.sub + 1) / it.nsub;
-      gather = A.scr_cap > 0;
-    } else {
-      const int64_t W = A.row_w[a];
-      st = A.pstart[a];
-      dn = A.pdense[a];
-      gather = A.scr_cap > 0 && ((dn >> 63) & 1ull);  // (bit 63: the planner's gather mark, T < 64)
-      if (tid < A.T) S_.dt[tid] = est_distinct(A.est, tid, W);
-      if (tid == 0) {
-        S_.row_begin = S_.slab_cur;
-        S_.row_n = 0;
-      }
-      __syncthreads();  // dt[] is read by every thread below
-    }
+    const uint64_t st = it.st, dn = it.dn, hz0 = it.hz[0], hz1 = it.hz[1];
     // gather mode (rows with many chunks, split shares): the lists are walked once; tile 0 is counted
     // on the way and every other tile's groups go to a bucket that its chunk then reads contiguously
     // (instead of one walk of every contribution per chunk).  Off when the tails exceed the scratch.
-    if (uni(uint32_t(gather))) gather = uni(uint32_t(sp_tail_sizes(A, S_, k0, k1) <= uint32_t(A.scr_cap))) != 0u;
+    bool gather = A.scr_cap > 0 && it.gslot >= 0;
+    if (!split && tid == 0) {
+      S_.row_begin = S_.slab_cur;
+      S_.row_n = 0;
+    }
+    if (gather) {
+      if (tid <= A.T) S_.bstart[tid] = A.bst[int64_t(it.gslot) * (A.T + 1) + tid];
+      if (tid < A.T) S_.bcur[tid] = 0u;
+    }
+    __syncthreads();
+    gather = gather && uni(S_.bstart[A.T]) <= uint32_t(A.scr_cap);
     int dense_until = split ? t_end : -1;  // tiles below it go dense (split items; hash overflow fallback)
     int32_t H = 0;                         // 0: table size from the estimate
     while (t < t_end) {
@@ -1007,13 +1044,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       if (!dense) {
         const uint64_t rest = t + 1 < 64 ? st >> (t + 1) : 0ull;
         t1 = rest ? min(t_end, t + __ffsll((long long)rest)) : t_end;
-        if (H == 0) {
-          float e = 0.f;
-          for (int x = t; x < t1; x++) e += S_.dt[x];
-          H = kHashMin;
-          while (H < kHashMax && float(H) < 2.f * e + 64.f) H <<= 1;
-          H = uni(H);
-        }
+        if (H == 0) H = kHashMin << (((t < 32 ? hz0 : hz1) >> (2 * (t & 31))) & 3u);  // the planner's size
       }
       const int32_t c0 = t * kTW, c1 = min(A.M, t1 * kTW);
       WalkOp op;
@@ -1101,6 +1132,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       A.row_base[a] = S_.row_n ? S_.row_begin : 0;
       A.row_nnz[a] = int32_t(S_.row_n);
     }
+    if (tid == 0) S_.work = next;
+    __syncthreads();
   }
 #ifdef COOC_SP_STATS
   if (tid == 0) {
@@ -1238,6 +1271,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sp_roww_.reserve(sizeof(int64_t) * M));
   COOC_TRY(sp_pstart_.reserve(sizeof(uint64_t) * M));
   COOC_TRY(sp_pdense_.reserve(sizeof(uint64_t) * M));
+  COOC_TRY(sp_hz_.reserve(sizeof(uint64_t) * 2 * M));
   COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * 2 * M));
   COOC_TRY(order_.reserve(sizeof(int32_t) * 2 * M));
   COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));           // work items per row (split rows)
@@ -1327,7 +1361,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   SPT("est");
   k_sp_plan<<<nblocks(M, 256), 256, 0, s>>>(M, T, row_ptr, epre, est, gmass, rowsum_.as<int64_t>(),
                                             sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(),
-                                            sp_pdense_.as<uint64_t>(), order_keys_.as<uint64_t>(),
+                                            sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
+                                            order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
                                             row_base_.as<int64_t>(), tot);
   k_sp_totals<<<1, 1, 0, s>>>(tot, epre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
@@ -1371,7 +1406,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
                                                   M, s));
     k_sp_queue<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, order_keys_.as<uint64_t>() + M,
-                                              ord_cbase_.as<int32_t>(), gmass, M, T, tot, sp_queue_.as<SpWork>(),
+                                              ord_cbase_.as<int32_t>(), gmass, row_ptr, sp_pstart_.as<uint64_t>(),
+                                              sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(), M, T, tot,
+                                              sp_queue_.as<SpWork>(),
                                               split_slot_.as<int32_t>(), split_row_.as<int32_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
@@ -1391,6 +1428,16 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
     if (need > sp_scr_.cap && (need > (f0 + sp_scr_.cap) / 4 || !sp_scr_.reserve(need).ok())) scr_cap = 0;
   }
+  const int64_t n_gather = T < 64 ? h_tot_->n_gather_rows + h_tot_->n_split_work : 0;  // bucket-start slots
+  if (scr_cap > 0 && n_gather > 0) {
+    const size_t nb = sizeof(uint32_t) * size_t(n_gather) * size_t(T + 1);
+    COOC_TRY(sp_bst_.reserve(nb));
+    COOC_HIP_TRY(hipMemsetAsync(sp_bst_.p, 0, nb, s));
+    k_sp_tail_count<<<dim3(1024, 8), 256, 0, s>>>(sp_queue_.as<SpWork>(), n_work, vals, sp_tb_.as<int32_t>(), T,
+                                                  sp_bst_.as<uint32_t>());
+    k_sp_tail_scan<<<unsigned(std::min<int64_t>(4096, (n_gather + 3) / 4)), 256, 0, s>>>(tot, T, sp_bst_.as<uint32_t>());
+    COOC_HIP_TRY(hipGetLastError());
+  }
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -1403,12 +1450,26 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   dense_mode_ = false;
   last_rows_ = M;
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
-  const SpArgs proto{sp_queue_.as<SpWork>(), tot, qctr, vals, row_ptr, up, sp_tb_.as<int32_t>(),
-                     sp_arena_.as<uint4>(),
-                     sp_roww_.as<int64_t>(), sp_pstart_.as<uint64_t>(), sp_pdense_.as<uint64_t>(), est, nullptr,
-                     split_slot_.as<int32_t>(), nullptr, nullptr, bump_.as<unsigned long long>(), 0, slab,
-                     row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), M, T, nullptr, nullptr, n_c, U, n1 + 4,
-                     scr_cap ? sp_scr_.as<uint4>() : nullptr, scr_cap};
+  SpArgs proto{};
+  proto.queue = sp_queue_.as<SpWork>();
+  proto.tot = tot;
+  proto.qctr = qctr;
+  proto.vals = vals;
+  proto.tb = sp_tb_.as<int32_t>();
+  proto.tarena = sp_arena_.as<uint4>();
+  proto.bst = sp_bst_.as<uint32_t>();
+  proto.split_slot = split_slot_.as<int32_t>();
+  proto.bump = bump_.as<unsigned long long>();
+  proto.slab = slab;
+  proto.row_base = row_base_.as<int64_t>();
+  proto.row_nnz = row_nnz_.as<int32_t>();
+  proto.M = M;
+  proto.T = T;
+  proto.n_contrib = n_c;
+  proto.n_users = U;
+  proto.n_groups = n1 + 4;
+  proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
+  proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    kSpLds));
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1485,9 +1546,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       const double g = double(std::min<int64_t>(n_work, n_cu_));
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
               "compact hash %.0f | chunks dense %llu hash %llu retries %llu fallbacks %llu | pairs dense %.3g hash %.3g | "
-              "rows %llu split items %llu | mean H %.0f\n",
+              "rows %llu split items %llu | mean H %.0f | tail sizes %.0f\n",
               h[13] / 100.0 / g, h[0] / 100.0 / g, h[1] / 100.0 / g, h[4] / 100.0 / g, h[2] / 100.0 / g, h[3] / 100.0 / g,
-              h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0);
+              h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0,
+              h[15] / 100.0 / g);
     }
 #endif
     if (!(err & 4) || cap >= bound + slack) break;

@@ -23,12 +23,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards", type=int, default=8, help="C3 users / this many are counted (8: one GPU's share)")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="another build of libcooc_hip.so (e.g. the statistics build)")
     args = ap.parse_args()
     import torch
 
     import __graft_entry__
 
+
     pkg = __graft_entry__.load_package()
+    if args.lib:  # before the first call loads the library
+        sys.modules["flink_cooccurrence_amd._lib"].LIB_PATH = os.path.abspath(args.lib)
     from flink_cooccurrence_amd import datagen
 
     dev = torch.device("cuda", 0)
