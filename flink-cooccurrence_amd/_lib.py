@@ -75,6 +75,8 @@ _SIGS = {
     "cooc_abi_version": (ctypes.c_int, []),
     "cooc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "cooc_create": (ctypes.c_int, [ctypes.POINTER(CoocConfig), ctypes.POINTER(vp)]),
+    "cooc_create_on": (ctypes.c_int, [ctypes.POINTER(CoocConfig), i32p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(vp)]),
     "cooc_destroy": (None, [vp]),
     "cooc_last_error": (ctypes.c_char_p, [vp]),
     "cooc_count_device": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
@@ -85,6 +87,8 @@ _SIGS = {
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
     "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
     "cooc_copy_topk_batch": (ctypes.c_int, [vp, i32p, i32p, f64p]),
+    "cooc_llr": (ctypes.c_int, [vp, ctypes.c_int64, i64p, f64p]),
+    "cooc_topk_items": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p, i32p, i32p, f64p]),
     "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),
     "cooc_finish_window": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_window_delta": (ctypes.c_int, [vp, i32p, i64p, i32p, u32p, i16p]),

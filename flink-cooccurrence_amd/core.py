@@ -89,7 +89,8 @@ class CooccurrenceCore:
     """One context of the C-ABI (one Flink subtask)."""
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
-                 exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0):
+                 exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0,
+                 devices=None, subtask: int = 0):
         """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
         planner: "auto" (the batch planner below 40,320 items) or "general" (the sort-based planner).
         user_cut: kMax, 0 = off; else only the first user_cut interactions of every user are expanded
@@ -104,7 +105,11 @@ class CooccurrenceCore:
         flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner == "general" else 0
         cfg = CoocConfig(device, n_items, topk, flags, window_size_ms, user_cut, 0)
         h = ctypes.c_void_p()
-        check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
+        if devices is None:
+            check(L.cooc_create(ctypes.byref(cfg), ctypes.byref(h)), None)
+        else:  # create(cfg{devices[]}): this subtask's GPU is devices[subtask % len(devices)]
+            devs = np.ascontiguousarray(devices, np.int32)
+            check(L.cooc_create_on(ctypes.byref(cfg), _p(devs, i32p), len(devs), int(subtask), ctypes.byref(h)), None)
         self._h = h
         self.n_items = n_items
         self.topk = topk
@@ -176,6 +181,25 @@ class CooccurrenceCore:
         vals = np.zeros((M, topk), np.int32)
         scores = np.zeros((M, topk), np.float64)
         check(L.cooc_copy_topk_batch(self._h, _p(sizes, i32p), _p(vals, i32p), _p(scores, f64p)), self._h)
+        return sizes, vals, scores
+
+    def llr(self, k4) -> np.ndarray:
+        """LogLikelihood.logLikelihoodRatio of each (k11, k12, k21, k22) row, on the device."""
+        k = np.ascontiguousarray(k4, np.int64).reshape(-1, 4)
+        out = np.zeros(len(k), np.float64)
+        check(_lib.load().cooc_llr(self._h, len(k), _p(k, i64p), _p(out, f64p)), self._h)
+        return out
+
+    def topk_items(self, items, k: int, exact_scores: bool = False):
+        """topk(handle, items[], k) of SURVEY §8(b): the top-k of the given rows of the last batch ->
+        (sizes [n], values [n, k], scores [n, k]), heap layout as topk_batch."""
+        its = np.ascontiguousarray(items, np.int32)
+        n = len(its)
+        sizes = np.zeros(n, np.int32)
+        vals = np.zeros((n, k), np.int32)
+        scores = np.zeros((n, k), np.float64)
+        check(_lib.load().cooc_topk_items(self._h, k, _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0, n,
+                                          _p(its, i32p), _p(sizes, i32p), _p(vals, i32p), _p(scores, f64p)), self._h)
         return sizes, vals, scores
 
     # ---- sharding layer (owner-partitioned exchange of partial rows) -----------------------------

@@ -72,6 +72,26 @@ int cooc_create(const cooc_config *cfg, cooc_ctx **out) {
   });
 }
 
+int cooc_create_on(const cooc_config *cfg, const int32_t *devices, int32_t n_devices, int32_t subtask,
+                   cooc_ctx **out) {
+  return guarded(nullptr, [&]() -> int {
+    if (!cfg || !out || !devices || n_devices <= 0 || subtask < 0) {
+      cooc_ctx::create_error() = "cooc_create_on: bad devices / subtask arguments";
+      return COOC_ERR_ARG;
+    }
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess) n_dev = 0;
+    for (int32_t i = 0; i < n_devices; i++)
+      if (devices[i] < 0 || devices[i] >= n_dev) {
+        cooc_ctx::create_error() = "device " + std::to_string(devices[i]) + " is not in [0, " + std::to_string(n_dev) + ")";
+        return COOC_ERR_ARG;
+      }
+    cooc_config c = *cfg;
+    c.device = devices[subtask % n_devices];
+    return cooc_create(&c, out);
+  });
+}
+
 void cooc_destroy(cooc_ctx *ctx) { delete ctx; }
 
 const char *cooc_last_error(const cooc_ctx *ctx) {
@@ -135,6 +155,26 @@ int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double 
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;
     Status s = ctx->copy_topk_batch(sizes, values, scores);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_llr(cooc_ctx *ctx, int64_t n, const int64_t *k, double *out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    if (n < 0 || (n > 0 && (!k || !out))) return fail(ctx, COOC_ERR_ARG, "bad llr arguments");
+    Status s = ctx->llr(n, k, out);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_topk_items(cooc_ctx *ctx, int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *out_sizes,
+                    int32_t *out_items, double *out_scores) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    if (n < 0 || (n > 0 && (!items || !out_sizes || !out_items || !out_scores)))
+      return fail(ctx, COOC_ERR_ARG, "bad topk_items arguments");
+    Status s = ctx->topk_items(k, flags, n, items, out_sizes, out_items, out_scores);
     return s.ok() ? COOC_OK : fail(ctx, s);
   });
 }

@@ -227,6 +227,43 @@ Status cooc_ctx::topk_batch(int32_t topk, int32_t flags, hipStream_t s) {
                                       b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(), b_tk_score.as<double>()));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   batch_topk = topk;
+  batch_topk_flags = flags & COOC_FLAG_EXACT_SCORES;
+  return Status::Ok();
+}
+
+Status cooc_ctx::llr(int64_t n, const int64_t *k, double *out) {
+  if (n == 0) return Status::Ok();
+  COOC_HIP_TRY(hipSetDevice(device));
+  cooc::DevBuf dk, dout;
+  Status st = [&]() -> Status {
+    COOC_TRY(dk.reserve(sizeof(int64_t) * 4 * size_t(n)));
+    COOC_TRY(dout.reserve(sizeof(double) * size_t(n)));
+    COOC_HIP_TRY(hipMemcpyAsync(dk.p, k, sizeof(int64_t) * 4 * size_t(n), hipMemcpyHostToDevice, batch_stream));
+    COOC_TRY(cooc::launch_llr(batch_stream, n, dk.as<int64_t>(), dout.as<double>()));
+    COOC_HIP_TRY(hipMemcpyAsync(out, dout.p, sizeof(double) * size_t(n), hipMemcpyDeviceToHost, batch_stream));
+    COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+    return Status::Ok();
+  }();
+  dk.release();
+  dout.release();
+  return st;
+}
+
+Status cooc_ctx::topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,
+                            int32_t *values, double *scores) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  const int32_t M = cfg.n_items;
+  for (int32_t i = 0; i < n; i++)
+    if (items[i] < 0 || items[i] >= M) return Status{COOC_ERR_ARG, std::to_string(items[i]) + " is not an item"};
+  if (batch_topk != k || batch_topk_flags != (flags & COOC_FLAG_EXACT_SCORES)) COOC_TRY(topk_batch(k, flags, batch_stream));
+  COOC_HIP_TRY(hipSetDevice(device));
+  const size_t kk = size_t(k);
+  for (int32_t i = 0; i < n; i++) {
+    const size_t a = size_t(items[i]);
+    COOC_HIP_TRY(hipMemcpy(sizes + i, b_tk_size.as<int32_t>() + a, sizeof(int32_t), hipMemcpyDeviceToHost));
+    COOC_HIP_TRY(hipMemcpy(values + i * kk, b_tk_val.as<int32_t>() + a * kk, sizeof(int32_t) * kk, hipMemcpyDeviceToHost));
+    COOC_HIP_TRY(hipMemcpy(scores + i * kk, b_tk_score.as<double>() + a * kk, sizeof(double) * kk, hipMemcpyDeviceToHost));
+  }
   return Status::Ok();
 }
 

@@ -113,6 +113,9 @@ struct cooc_ctx {
                           int32_t *rowsum32);
   cooc::Status topk_batch(int32_t topk, int32_t flags, hipStream_t s);
   cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
+  cooc::Status llr(int64_t n, const int64_t *k, double *out);
+  cooc::Status topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,
+                          int32_t *values, double *scores);
 
   static std::string &create_error();
 
@@ -132,6 +135,7 @@ struct cooc_ctx {
   // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
   cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
   int32_t batch_topk = 0;
+  int32_t batch_topk_flags = 0;
   bool have_batch = false;
   int64_t batch_observed = 0;
   int64_t batch_nnz = 0;

@@ -260,6 +260,20 @@ __global__ void k_observed(const int64_t *__restrict__ rowsum, int32_t M, int64_
 
 }  // namespace
 
+namespace {
+__global__ void k_llr(int64_t n, const int64_t *__restrict__ k, double *__restrict__ out) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = llr(k[4 * i], k[4 * i + 1], k[4 * i + 2], k[4 * i + 3]);
+}
+}  // namespace
+
+Status launch_llr(hipStream_t s, int64_t n, const int64_t *d_k4, double *d_out) {
+  if (n <= 0) return Status::Ok();
+  k_llr<<<unsigned((n + 255) / 256), 256, 0, s>>>(n, d_k4, d_out);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
 Status launch_relocate(hipStream_t s, int64_t n, const int64_t *reloc, int32_t *arena) {
   if (n > 0) k_relocate<<<std::min<unsigned>(blocks_for(n * 64, 256), 4096), 256, 0, s>>>(n, reloc, arena);
   COOC_HIP_TRY(hipGetLastError());

@@ -1,0 +1,74 @@
+package com.github.uce.flinkcooccurrences;
+
+/**
+ * JNI mirror of include/cooc.h (libcooc_jni.so, built from ../../../../../../jni/cooc_jni.c, links
+ * libcooc_hip.so).  One handle per Flink subtask; a handle is not thread-safe, handles are
+ * independent.  Every native throws IllegalArgumentException for COOC_ERR_ARG and
+ * IllegalStateException for any other non-zero status, with cooc_last_error() as the message --
+ * the reference's error behaviour (e.g. ItemRowRescorerTwoInputStreamOperator.java:52-54,72-79).
+ *
+ * Uncompiled in the build container (no JDK); every entry point it binds is exercised through the
+ * same C-ABI by the Python ctypes tests (tests/test_gpu_parity.py, flink-cooccurrence_amd/_lib.py).
+ */
+final class CoocNative {
+
+  static {
+    System.loadLibrary("cooc_jni");
+  }
+
+  static final int FLAG_EXACT_SCORES = 1;  // COOC_FLAG_EXACT_SCORES
+
+  private CoocNative() {
+  }
+
+  /** cooc_create_on: the handle of subtask {@code subtask} binds to devices[subtask % devices.length]. */
+  static native long create(int[] devices, int subtask, int nItems, int topK, int flags, long windowSizeMs,
+      short userCut);
+
+  /** cooc_destroy. */
+  static native void destroy(long handle);
+
+  /**
+   * cooc_op_process_elements: one buffered batch of Tuple3(user, item, timestamp) as parallel arrays
+   * (the first n entries).  Late records (timestamp <= the current watermark, NonSampled...java:89-91)
+   * are dropped; returns how many.
+   */
+  static native long processElements(long handle, int n, int[] users, int[] items, long[] timestamps);
+
+  /**
+   * cooc_op_process_watermark: fires the next window whose maxTimestamp <= watermark, if any.  On
+   * true, info = {ts, nnz, observed, nRows, topK, nTopK} (cooc_window_info) sizes the copy calls.
+   */
+  static native boolean processWatermark(long handle, long watermark, long[] info);
+
+  /**
+   * cooc_copy_window_delta of the fired window: rows int[nRows], rowPtr long[nRows + 1], cols int[nnz],
+   * cnt16 short[nnz] -- the window's reduced ItemRowAggregator rows (Int2ShortOpenHashMap values).
+   */
+  static native void copyDelta(long handle, int[] rows, long[] rowPtr, int[] cols, short[] cnt16);
+
+  /** cooc_copy_window_rowsums: items int[nRows], delta32 int[nRows] (RowSumAggregator values). */
+  static native void copyRowSums(long handle, int[] items, int[] delta32);
+
+  /** cooc_copy_window_topk: rows int[nTopK], sizes int[nTopK], values int[nTopK * topK], scores double[...]. */
+  static native void copyTopK(long handle, int[] rows, int[] sizes, int[] values, double[] scores);
+
+  /**
+   * cooc_op_counters: {UserInteractionCounterLateElements, UserInteractionCounterObservedCooccurrences,
+   * RowSumProcessWindowRowSum, ItemRowRescorerRescoredItems, rescorer observed}.
+   */
+  static native void counters(long handle, long[] out5);
+
+  /**
+   * cooc_count_host: one stateless window over CSR histories (userPtr long[nUsers + 1] into items).
+   * Returns {nnz, observed}; the result stays on the handle for copyBatch / topKItems.
+   */
+  static native long[] countBatch(long handle, long[] userPtr, int[] items);
+
+  /** cooc_copy_batch: rowPtr long[nItems + 1], cols int[nnz], cnt16 short[nnz], rowSums32 int[nItems]. */
+  static native void copyBatch(long handle, long[] rowPtr, int[] cols, short[] cnt16, int[] rowSums32);
+
+  /** cooc_topk_items: topk(handle, items[], k) of the last batch; sizes int[n], values/scores [n * k]. */
+  static native void topKItems(long handle, int k, int flags, int[] items, int[] sizes, int[] values,
+      double[] scores);
+}

@@ -130,6 +130,11 @@ typedef struct cooc_device_result {
 COOC_API int cooc_abi_version(void);
 COOC_API const char *cooc_status_string(int status);
 COOC_API int cooc_create(const cooc_config *cfg, cooc_ctx **out);
+/* create(cfg{devices[]}) of SURVEY §8(b): one handle per Flink subtask over the node's GPUs.  The
+ * handle binds to devices[subtask % n_devices] (cfg->device is ignored); every other field as in
+ * cooc_create.  A device ordinal outside [0, hipGetDeviceCount()) is COOC_ERR_ARG. */
+COOC_API int cooc_create_on(const cooc_config *cfg, const int32_t *devices, int32_t n_devices, int32_t subtask,
+                            cooc_ctx **out);
 COOC_API void cooc_destroy(cooc_ctx *ctx);
 COOC_API const char *cooc_last_error(const cooc_ctx *ctx);
 
@@ -167,6 +172,17 @@ COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uin
  * (heap positions 1..size, least score first; rows without entries have size 0). */
 COOC_API int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream);
 COOC_API int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores);
+/* LogLikelihood.logLikelihoodRatio (LogLikelihood.java:41-57) evaluated by the device function the
+ * rescoring kernels use: k = host int64[n][4] of (k11, k12, k21, k22), out = host double[n].  For
+ * known-answer tests of the device scores (LogLikelihoodTest.java:14-16). */
+COOC_API int cooc_llr(cooc_ctx *ctx, int64_t n, const int64_t *k, double *out);
+/* The SURVEY §8(b) query topk(handle, items[], k): the top-k of the rows `items` (n of them) of the
+ * last batch result, computing the batch top-k first when it has not run with this (k, flags).
+ * out_sizes int32[n], out_items int32[n*k], out_scores double[n*k] (heap positions 1..size as in
+ * cooc_copy_topk_batch).  The rescorer's per-row query (ItemRowRescorer...java:195-241 for the
+ * given rows only); an item outside [0, n_items) is COOC_ERR_ARG. */
+COOC_API int cooc_topk_items(cooc_ctx *ctx, int32_t k, int32_t flags, int32_t n, const int32_t *items,
+                             int32_t *out_sizes, int32_t *out_items, double *out_scores);
 
 /* ---- streaming (resident per-user histories, global rows, row sums) ------------------------
  * cooc_submit_batch stages the interactions of one tumbling window: n_users users with their

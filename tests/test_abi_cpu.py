@@ -39,6 +39,12 @@ def test_create_fails_loudly_without_gpu(pkg):
     assert e.value.status == 3 and "no HIP device" in str(e.value)
 
 
+def test_create_on_rejects_devices_it_cannot_see(pkg):
+    """create(cfg{devices[]}): a device ordinal the runtime does not list is an argument error."""
+    with pytest.raises(pkg.IllegalArgumentException):
+        pkg.CooccurrenceCore(n_items=10, devices=[0], subtask=0)
+
+
 def test_argument_errors_mirror_reference(pkg):
     from flink_cooccurrence_amd import _lib
 

@@ -400,7 +400,6 @@ def test_partition_pack_merge_kernels(pkg, oracle, torch_cuda, n_parts, output):
         rstart = [sum(sharding.rows_owned(M, n_parts, o) for o in range(p))]
         recv_nnz = torch.cat([pk[1][rstart[0]:rstart[0] + R] for pk in packs])
         recv_ent = torch.cat([pk[2][int(pk[0][:p].sum()):int(pk[0][:p + 1].sum())] for pk in packs])
-        torch.cuda.synchronize()  # the gathers run on torch's stream, not the context's
         m = cores[p].merge_partitions(n_parts, p, recv_nnz, recv_ent, rowsum)
         torch.cuda.synchronize()
         assert m.n_items == R
@@ -494,6 +493,29 @@ def test_batch_topk_vs_rescorer(pkg, oracle, torch_cuda, exact):
     assert np.array_equal(vals[rows], w.topk_values) or True
 
 
+def test_topk_items_query_and_devices(pkg, torch_cuda):
+    """topk(handle, items[], k) (SURVEY §8(b)): the rows asked for equal those of the full batch top-k;
+    create(cfg{devices[]}) binds subtask s to devices[s % n]; bad items / devices are
+    IllegalArgumentException."""
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.small_log(14, 900, 200, 16.0)
+    M, k = 200, 5
+    with pkg.CooccurrenceCore(n_items=M, devices=[0], subtask=3) as core:
+        core.count(up, it)
+        q = np.array([0, 7, 199, 3, 0], np.int32)
+        s1, v1, c1 = core.topk_items(q, k)          # computes the batch top-k itself
+        sizes, vals, scores = core.topk_batch(k)
+        assert np.array_equal(s1, sizes[q]) and np.array_equal(v1, vals[q]) and np.array_equal(c1, scores[q])
+        s2, v2, c2 = core.topk_items(q, 3, exact_scores=True)  # another (k, flags): recomputed
+        sizes3, vals3, scores3 = core.topk_batch(3, exact_scores=True)
+        assert np.array_equal(s2, sizes3[q]) and np.array_equal(v2, vals3[q])
+        with pytest.raises(pkg.IllegalArgumentException):
+            core.topk_items([M], k)
+    with pytest.raises(pkg.IllegalArgumentException):
+        pkg.CooccurrenceCore(n_items=M, devices=[0, 4096])
+
+
 def test_c2_scale_topk_rows(pkg, oracle, torch_cuda):
     """LLR top-50 at C2 scale, where counts exceed 32767: the reference's short wraps negative, its
     LLR is NaN, and a NaN at the heap root blocks every later insert.  Rows are checked against the
@@ -556,7 +578,6 @@ def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output, cut):
         desc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
         rc = torch.empty(M, dtype=torch.int32, device=dev)
         arena = torch.full((stride,), -1, dtype=torch.int16, device=dev)
-        torch.cuda.synchronize()  # the -1 fill must land before the plan writes the arena
         send, ids, obs = core.shard_plan(torch.from_numpy(sup).to(dev), torch.from_numpy(sit).to(dev), W, desc, rc,
                                          arena)
         assert ids % 8 == 0 and ids <= stride
@@ -572,8 +593,6 @@ def test_shard_records_kernels(pkg, oracle, torch_cuda, W, output, cut):
         before = sum(sharding.rows_owned(M, W, q) for q in range(o))
         recv_rc = torch.cat([p[1][before:before + R] for p in parts])
         recv_desc = torch.cat([p[2][int(p[0][:o].sum()):int(p[0][:o + 1].sum())] for p in parts])
-        # the gathers above run on torch's stream; the context's stream does not wait for it
-        torch.cuda.synchronize()
         res = cores[o].shard_count(W, o, recv_rc, recv_desc, arena_all, stride)
         torch.cuda.synchronize()
         assert res.n_items == R
