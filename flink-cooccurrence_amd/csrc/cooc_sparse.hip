@@ -58,14 +58,20 @@ namespace cooc {
 
 namespace {
 
-constexpr int kSpThreads = 1024;
+#ifndef COOC_SP_THREADS
+#define COOC_SP_THREADS 512
+#endif
+#ifndef COOC_SP_TSHIFT
+#define COOC_SP_TSHIFT 14
+#endif
+constexpr int kSpThreads = COOC_SP_THREADS;  // 512: two workgroups per CU
 constexpr int kSpWaves = kSpThreads / 64;
-constexpr int kTW = 32768;  // dense tile width (uint32 LDS counters: 128 KB)
-constexpr int kTShift = 15;
+constexpr int kTShift = COOC_SP_TSHIFT;
+constexpr int kTW = 1 << kTShift;  // dense tile width (16384: 64 KB of uint32 LDS counters)
 constexpr int kSpMaxTiles = 64;                        // per-row plans are 64-bit tile masks
 constexpr int kHashMax = 8192;                        // slots: keys + counts = the dense tile's 128 KB
 constexpr int kHashMin = 1024;                         // one slot per thread at least
-constexpr int kHashMaxTiles = 32;                      // a hash chunk spans <= 2^20 columns ...
+constexpr int kHashMaxTiles = (1 << 20) / kTW;          // a hash chunk spans <= 2^20 columns ...
 constexpr int kL1Words = kHashMaxTiles * kTW / 1024;   // ... so its block bitmap is <= 1024 words
 constexpr int kSpDb = 512;                             // contribution descriptors per batch
 constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
@@ -76,8 +82,8 @@ constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work i
 constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups)
 constexpr int kGatherMinChunks = 3;                    // rows with this many chunks gather their tails
 constexpr float kHashFill = 0.5f * kHashMax;           // expected distinct keys per hash chunk
-constexpr float kDensePairs = 65536.f;                 // a tile with more expected pairs is dense
-constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + 256 * 4;
+constexpr float kDensePairs = 2.f * kTW;                 // a tile with more expected pairs is dense
+constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + kSpThreads;
 
 // One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
 struct SpWork {
@@ -87,7 +93,7 @@ struct SpWork {
   int32_t row;
   int32_t kind;     // -1: a whole row; -2: a share of a split row (every tile, into its staging row)
   int32_t gslot;    // gather mode: row of bucket starts in SpArgs::bst (k_sp_tail_*); -1: none
-  int32_t pad;
+  int32_t est;      // a whole row's expected keys (planner estimate; sizes its output region)
 };
 
 struct SpArgs {
@@ -452,6 +458,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
         }
       }
       est_sum = uint64_t(e_tot) + 1;
+      row_nnz[a] = int32_t(min(est_sum, uint64_t(INT32_MAX)));  // carried to the queue record (k_sp_queue)
     }
     pstart[a] = st;
     pdense[a] = dn;
@@ -500,7 +507,7 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
                            const int64_t *__restrict__ row_ptr, const uint64_t *__restrict__ pstart,
                            const uint64_t *__restrict__ pdense, const uint64_t *__restrict__ hz, int32_t M, int32_t T,
                            PlanTotals *__restrict__ tot, SpWork *__restrict__ queue, int32_t *__restrict__ split_slot,
-                           int32_t *__restrict__ split_row) {
+                           int32_t *__restrict__ split_row, const int32_t *__restrict__ row_nnz) {
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= M) return;
   const int64_t n_split = tot->n_split, n_split_work = tot->n_split_work;
@@ -534,6 +541,7 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
     x.row = a;
     x.kind = -1;
     x.gslot = (x.dn >> 63) & 1ull ? int32_t(atomicAdd(ng, 1ull)) : -1;
+    x.est = row_nnz[a];
     queue[n_split_work + (r - n_split)] = x;
   }
 }
@@ -612,6 +620,8 @@ struct SpStatic {
   int32_t work;
   uint32_t flag, claims;
   int64_t slab_cur, slab_end, row_begin, row_n, pos, copy_from, copy_n;
+  int64_t saved_cur, saved_end;  // the workgroup's slab while a big row fills a region of its own
+  uint32_t own;
   uint32_t bstart[kSpMaxTiles + 1]; // gather mode: bucket starts in the workgroup's scratch
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
 };
@@ -791,6 +801,20 @@ __device__ inline void sp_walk_range(const SpArgs &A, const SpShared &L, SpStati
   __syncthreads();
 }
 
+// Global stores of this workgroup made visible to its own later global loads.  __syncthreads() only
+// drains LDS traffic (s_waitcnt lgkmcnt(0)), and the CU's vector L1 is write-through without
+// keeping its lines in step with later stores: a line loaded earlier -- by this workgroup, or by the
+// other workgroup resident on the CU reading its own data next to ours -- can still hold what the
+// line had before.  So every wave waits for all its memory operations (s_waitcnt 0), the barrier,
+// then the L1 is invalidated (agent-scope acquire: buffer_inv sc1) and the loads that follow read
+// the XCD's L2, where the stores are.  Used where the kernel reads back what it wrote: a row moving
+// to a new slab, the gather buckets.
+__device__ inline void sp_global_sync() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 // Output space for n more entries of the current row (thread-uniform call).  Moves the row's
 // entries so far to a new slab when the workgroup's slab is exhausted.  Returns the write position
 // (-1 when the output region is exhausted: the host reruns with a larger region).
@@ -800,7 +824,7 @@ __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
     S_.copy_n = 0;
     if (S_.slab_cur + n > S_.slab_end) {
       const int64_t need = S_.row_n + n;
-      const int64_t take = max(A.slab, need);
+      const int64_t take = max(A.slab, need + need / 2);  // a growing row moves O(log) times
       int64_t b = int64_t(atomicAdd(A.bump, (unsigned long long)take));
       if (b + take > A.cap) {
         atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 4ull);
@@ -823,6 +847,7 @@ __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
   __syncthreads();
   const int64_t cn = uni(S_.copy_n);
   if (cn > 0) {  // the row's earlier entries follow it to the new slab (rare)
+    sp_global_sync();  // they were just stored by other waves
     const int64_t from = S_.copy_from, to = S_.row_begin;
     for (int64_t i = tid; i < cn; i += kSpThreads) {
       if (BCHK(A, to + i < A.cap && from + i < A.cap && from >= 0, 32)) {
@@ -936,9 +961,21 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   __syncthreads();
   uint32_t nblk;
   {
-    const uint32_t x = tid < nL1 ? uint32_t(__popc(L.L1[tid])) : 0u;
+    static_assert(kL1Words % kSpThreads == 0, "L1 words per thread");
+    constexpr int kW = kL1Words / kSpThreads;  // consecutive L1 words per thread
+    uint32_t pc[kW], x = 0;
+#pragma unroll
+    for (int i = 0; i < kW; i++) {
+      pc[i] = kW * tid + i < nL1 ? uint32_t(__popc(L.L1[kW * tid + i])) : 0u;
+      x += pc[i];
+    }
     const uint32_t p = block_excl_scan(x, &nblk, S_.wtot);
-    if (tid < nL1) L.L1pre[tid] = p;
+    uint32_t run = p;
+#pragma unroll
+    for (int i = 0; i < kW; i++) {
+      if (kW * tid + i < nL1) L.L1pre[kW * tid + i] = run;
+      run += pc[i];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -978,7 +1015,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     keys[r] = 0u;
     cnts[r] = 0u;
   }
-  if (tid < nL1) L.L1[tid] = 0u;
+  for (int32_t i = tid; i < nL1; i += kSpThreads) L.L1[i] = 0u;
   __syncthreads();
 }
 
@@ -1026,6 +1063,21 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     // (instead of one walk of every contribution per chunk).  Off when the tails exceed the scratch.
     bool gather = A.scr_cap > 0 && it.gslot >= 0;
     if (!split && tid == 0) {
+      // a row expected to fill much of a slab gets a region of its own (est + 1/8), so it neither
+      // moves nor strands the workgroup's slab; the slab is resumed after it
+      const int64_t e = it.est;
+      S_.own = 0u;
+      if (e > A.slab / 4 && e + e / 8 > S_.slab_end - S_.slab_cur) {
+        const int64_t take = e + e / 8 + 1024;
+        const int64_t b = int64_t(atomicAdd(A.bump, (unsigned long long)take));
+        if (b + take <= A.cap) {
+          S_.saved_cur = S_.slab_cur;
+          S_.saved_end = S_.slab_end;
+          S_.own = 1u;
+          S_.slab_cur = b;
+          S_.slab_end = b + take;
+        }
+      }
       S_.row_begin = S_.slab_cur;
       S_.row_n = 0;
     }
@@ -1065,6 +1117,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       if (gather && t == 0) {  // tile 0 (a dense chunk) counted, the other tiles' groups to their buckets
         op.mode = 2;
         walked = sp_walk(A, L, S_, k0, k1, 0, A.T, true, op);
+        sp_global_sync();  // the buckets are read back by other waves (and this item's lines are new)
       } else if (gather) {     // a gathered tile range: contiguous in the scratch
         const uint32_t g0 = uni(S_.bstart[t]), g1 = uni(S_.bstart[t1]);
         sp_walk_range(A, L, S_, op.sbase + g0, g1 - g0, op);
@@ -1131,6 +1184,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     if (!split && tid == 0) {
       A.row_base[a] = S_.row_n ? S_.row_begin : 0;
       A.row_nnz[a] = int32_t(S_.row_n);
+      if (S_.own) {
+        S_.slab_cur = S_.saved_cur;
+        S_.slab_end = S_.saved_end;
+      }
     }
     if (tid == 0) S_.work = next;
     __syncthreads();
@@ -1409,7 +1466,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                               ord_cbase_.as<int32_t>(), gmass, row_ptr, sp_pstart_.as<uint64_t>(),
                                               sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(), M, T, tot,
                                               sp_queue_.as<SpWork>(),
-                                              split_slot_.as<int32_t>(), split_row_.as<int32_t>());
+                                              split_slot_.as<int32_t>(), split_row_.as<int32_t>(),
+                                              row_nnz_.as<int32_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
   SPT("queue");
@@ -1419,7 +1477,11 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   }
   // gather scratch: a bucket region per workgroup for the largest expected tail (+25%); a work item
   // whose exact tail is larger walks per chunk instead.  Skipped when memory is short.
-  const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_work, 1), n_cu_);
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kSpLds));
+  int per_cu = 1;
+  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sp_main, kSpThreads, kSpLds));
+  const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_work, 1), int64_t(n_cu_) * std::max(1, per_cu));
   int64_t scr_cap = 0;
   if (h_tot_->max_tail > 0 && T < 64) {
     scr_cap = std::min<int64_t>(kScrGroups, h_tot_->max_tail + h_tot_->max_tail / 4 + 4096);
@@ -1441,8 +1503,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * n_cu_)));
-  const int64_t slack = 2 * int64_t(n_cu_) * slab + M;
+  const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * grid)));
+  const int64_t slack = 2 * grid * slab + M;
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
   cap = std::max<int64_t>(1, std::min(cap, budget));
@@ -1470,8 +1532,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.n_groups = n1 + 4;
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
-  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kSpLds));
+  int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
     COOC_TRY(cnt_.reserve(sizeof(uint32_t) * size_t(cap + 1)));
@@ -1543,15 +1604,18 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     {
       unsigned long long h[16];
       hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
-      const double g = double(std::min<int64_t>(n_work, n_cu_));
+      const double g = double(grid);
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
               "compact hash %.0f | chunks dense %llu hash %llu retries %llu fallbacks %llu | pairs dense %.3g hash %.3g | "
               "rows %llu split items %llu | mean H %.0f | tail sizes %.0f\n",
               h[13] / 100.0 / g, h[0] / 100.0 / g, h[1] / 100.0 / g, h[4] / 100.0 / g, h[2] / 100.0 / g, h[3] / 100.0 / g,
               h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0,
               h[15] / 100.0 / g);
+      fprintf(stderr, "[sp stats] attempt %d: cap %lld slab %lld grid %lld err %lld scr_cap %lld n_gather %lld\n", attempt,
+              (long long)cap, (long long)slab, (long long)grid, (long long)err, (long long)A.scr_cap, (long long)n_gather);
     }
 #endif
+    last_err = err;
     if (!(err & 4) || cap >= bound + slack) break;
     // the expected key count was too low: rerun into a region of the exact bound
     size_t f2 = 0, t2 = 0;
@@ -1560,6 +1624,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     if (budget2 <= cap) break;
     cap = std::min<int64_t>(bound + slack, budget2);
   }
+  if (last_err & 4)  // rows were cut short: never hand out a partial result
+    return Status{4, "the output region (" + std::to_string(cap) + " entries) was exhausted"};
   out->row_base = row_base_.as<int64_t>();
   out->row_nnz = row_nnz_.as<int32_t>();
   out->col = col_.as<int32_t>();

@@ -48,6 +48,14 @@ def main():
     base = d2h(res.row_base, M, np.int64)
     nnz = d2h(res.row_nnz, M, np.int32)
     print("nnz", res.nnz, "sum row_nnz", int(nnz.sum()), flush=True)
+    nzr = np.nonzero(nnz)[0]
+    order = nzr[np.argsort(base[nzr], kind="stable")]
+    ends = base[order] + nnz[order]
+    ov = np.nonzero(base[order][1:] < ends[:-1])[0]
+    print("rows with entries", len(nzr), "overlapping row regions", len(ov), flush=True)
+    for k in ov[:10]:
+        print("  overlap: row %d [%d, %d) and row %d [%d, %d)" % (order[k], base[order[k]], ends[k], order[k + 1],
+                                                                base[order[k + 1]], ends[k + 1]), flush=True)
     rng = np.random.default_rng(1)
     sample = np.unique(np.concatenate([np.arange(0, 200), rng.integers(0, M, args.rows)]))
     bad = []
@@ -56,6 +64,16 @@ def main():
         if len(cols) > 1 and not np.all(np.diff(cols) > 0):
             k = int(np.argmax(np.diff(cols) <= 0))
             bad.append((int(a), int(c[a]), int(nnz[a]), k, int(cols[k]), int(cols[k + 1]), int(base[a])))
+            if len(bad) <= 3:
+                cnt = d2h(res.cnt, int(nnz[a]), np.uint32, int(base[a]))
+                z = np.nonzero(cols[k + 1:] == 0)[0]
+                nzt = np.nonzero(cols[k + 1:] != 0)[0]
+                print("  row %d: zero cols after first-bad %d, nonzero after %d (first at +%s, last col %d), "
+                      "cnt zeros in gap %d" % (a, len(z), len(nzt), nzt[0] if len(nzt) else "-", int(cols[-1]),
+                                               int((cnt[k + 1:][cols[k + 1:] == 0] == 0).sum())), flush=True)
+                if len(nzt):
+                    j = k + 1 + nzt[0]
+                    print("  resumes at", j, "cols", cols[j:j + 4].tolist(), "gap", j - k - 1, flush=True)
     print("checked", len(sample), "bad", len(bad), flush=True)
     for b in bad[:40]:
         print("row %d contribs %d nnz %d first-bad %d (%d -> %d) base %d" % b, flush=True)
