@@ -73,6 +73,26 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
                       f"one window, {threads} threads, {dt:.1f} s"}
 
 
+def limiter(pmc: dict, traffic, k_ms: float):
+    """What the PMC counters (profiles/pmc_<kernel>.json, collected by scripts/pmc_sparse.sh) say
+    bounds the kernel: HBM when the measured HBM-side bytes run near the peak, LDS when the LDS is
+    busy most cycles, else memory latency (waves waiting on outstanding loads with both far from
+    their peaks)."""
+    if not pmc or not traffic:
+        return None
+    hbm = traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+    lds = pmc.get("lds_util") or 0.0
+    wait = pmc.get("wave_wait_frac") or 0.0
+    if hbm >= 0.7:
+        kind = "hbm"
+    elif lds >= 0.6:
+        kind = "lds"
+    else:
+        kind = "latency"
+    return (f"{kind}: measured HBM traffic at {hbm:.0%} of peak, LDS busy {lds:.0%} of cycles, waves waiting "
+            f"{wait:.0%} of their cycles (PMC of the same kernel, profiles/pmc_{pmc.get('kernel', 'kernel')}.json)")
+
+
 def load_pmc(path: str) -> dict:
     if os.path.exists(path):
         try:
@@ -218,6 +238,9 @@ def main():
             "hbm_frac_measured": (traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
             "lds_util": pmc.get("lds_util"),
             "lds_bank_conflict_frac": pmc.get("lds_bank_conflict_frac"),
+            "l2_hit_rate": pmc.get("l2_hit_rate"),
+            "wave_wait_frac": pmc.get("wave_wait_frac"),
+            "limiter": limiter(pmc, traffic, k_ms),
             "kernel_ms": k_ms,
             "algorithmic_bytes_per_launch": b_alg,
             "units_per_launch": {"ordered_pairs": P_counted, "interactions": N_seen, "users": U_seen,

@@ -214,7 +214,7 @@ class Counter {
   bool dense_mode_ = false;           // the last run's output is dense_
   DevBuf dense_, send_, witems_;
   // large-universe path: tile-grouped arena, tile starts, per-row work and plan, estimates, queue
-  DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_, sp_pbase_, sp_scr_, sp_hz_, sp_bst_;
+  DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_, sp_pbase_, sp_scr_, sp_hz_;
   bool general_only_ = false;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
   static constexpr int64_t chunk_work_ = int64_t(1) << 22;  // pairs per chunk of the batch planner

@@ -43,7 +43,7 @@
 #include <unistd.h>
 #ifdef COOC_SP_STATS
 #define STAT_CLOCK() wall_clock64()
-#define STAT_ADD(k, v) do { if (threadIdx.x == 0) st_[k] += (v); } while (0)
+#define STAT_ADD(k, v) do { if (threadIdx.x == 0) S_.st[k] += (v); } while (0)  // LDS: keeps occupancy
 #else
 #define STAT_CLOCK() 0ull
 #define STAT_ADD(k, v) do {} while (0)
@@ -92,7 +92,7 @@ struct SpWork {
   uint64_t hz[2];   // 2 bits per chunk-start tile: its hash table has kHashMin << code slots
   int32_t row;
   int32_t kind;     // -1: a whole row; -2: a share of a split row (every tile, into its staging row)
-  int32_t gslot;    // gather mode: row of bucket starts in SpArgs::bst (k_sp_tail_*); -1: none
+  int32_t gslot;    // >= 0: the item runs in gather mode (its tails go through buckets)
   int32_t est;      // a whole row's expected keys (planner estimate; sizes its output region)
 };
 
@@ -103,8 +103,10 @@ struct SpArgs {
   const uint32_t *vals;     // contributions: user index, item-sorted
   const int32_t *tb;        // [U x (T + 1)] absolute 16-B group index of each tile segment of a user
   const uint4 *tarena;      // tile-grouped, padded lists in 16-B groups
-  const uint32_t *bst;      // [gather slots x (T + 1)] bucket starts of tiles 1 .. T-1 (+ the total)
-  uint32_t *staging;        // [n_split x M]
+  const int64_t *epre;      // [n_contrib + 1] prefix of the contributions' list lengths (pair work)
+  const float *gmass;       // [T] share of the interactions in each tile
+  uint32_t *staging;        // [n_split x sstride]
+  int64_t sstride;          // staging row stride: M rounded up to 4 (16-B aligned rows)
   const int32_t *split_slot;
   int32_t *col_out;
   uint32_t *cnt_out;
@@ -546,57 +548,6 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
   }
 }
 
-// Gather mode, bucket sizes: the 16-B groups of tiles 1 .. T-1 over a gather item's contributions,
-// per tile, from the users' descriptor lines (lanes = tiles, two users per wave when T < 32), added
-// into cnt[gslot][t].  Blocks stride over the queue (x) and over 1,024-contribution pieces of an item (y).
-__global__ __launch_bounds__(256) void k_sp_tail_count(const SpWork *__restrict__ queue, int64_t n_work,
-                                                       const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb,
-                                                       int32_t T, uint32_t *__restrict__ cnt) {
-  constexpr int kPiece = 1024, kU = 8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool half = T < 32;
-  const int per = half ? 2 : 1, sub = half ? lane >> 5 : 0, t = half ? lane & 31 : lane;
-  const int width = half ? 32 : 64;
-  const int64_t step = int64_t(blockDim.x >> 6) * per;
-  for (int64_t w = blockIdx.x; w < n_work; w += gridDim.x) {
-    const SpWork it = queue[w];
-    if (it.gslot < 0) continue;
-    uint32_t acc = 0;
-    for (int64_t p0 = it.k0 + int64_t(blockIdx.y) * kPiece; p0 < it.k1; p0 += int64_t(gridDim.y) * kPiece) {
-      const int64_t p1 = min(it.k1, p0 + kPiece);
-      for (int64_t kb = p0 + wave * per; kb < p1; kb += step * kU) {  // uniform per wave
-        uint32_t x[kU];
-#pragma unroll
-        for (int j = 0; j < kU; j++) {
-          const int64_t k = kb + sub + j * step;
-          const uint32_t u = k < p1 ? vals[k] : ~0u;
-          x[j] = (u != ~0u && t <= T) ? uint32_t(tb[int64_t(u) * (T + 1) + t]) : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kU; j++) {
-          const uint32_t nx = __shfl_down(x[j], 1, width);
-          if (t >= 1 && t < T) acc += nx - x[j];
-        }
-      }
-    }
-    if (half) acc += __shfl_down(acc, 32, 64);
-    if (acc && t >= 1 && t < T && (!half || lane < 32)) atomicAdd(cnt + int64_t(it.gslot) * (T + 1) + t, acc);
-  }
-}
-
-// ... scanned in place into bucket starts (tile 0 has none; entry T = the total).  One wave per slot.
-__global__ void k_sp_tail_scan(const PlanTotals *__restrict__ tot, int32_t T, uint32_t *__restrict__ cnt) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n = tot->n_gather;
-  for (int64_t g = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; g < n; g += (int64_t(gridDim.x) * blockDim.x) >> 6) {
-    uint32_t *row = cnt + g * (T + 1);
-    const uint32_t c = lane >= 1 && lane < T ? row[lane] : 0u;
-    const uint32_t inc = wave_incl_scan(c);
-    if (lane < T) row[lane] = inc - c;
-    if (lane == T - 1) row[T] = inc;
-  }
-}
-
 __global__ void k_sp_totals(PlanTotals *__restrict__ tot, const int64_t *__restrict__ epre, int64_t n,
                             int32_t *__restrict__ qctr) {
   tot->n_chunks = tot->n_split_work + (tot->n_active - tot->n_split);
@@ -624,6 +575,10 @@ struct SpStatic {
   uint32_t own;
   uint32_t bstart[kSpMaxTiles + 1]; // gather mode: bucket starts in the workgroup's scratch
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
+  uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
+#ifdef COOC_SP_STATS
+  unsigned long long st[16];
+#endif
 };
 
 // Insert one partner id into the LDS table (keys store id + 1; 0 = empty).  Linear probing from a
@@ -678,7 +633,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
       if (v.w != kSink) atomicAdd(&L.R[v.w], 1u);
     } else {
       const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
-      A.scratch[op.sbase + S_.bstart[t] + slot] = v;
+      if (slot < S_.bstart[t + 1] - S_.bstart[t]) A.scratch[op.sbase + S_.bstart[t] + slot] = v;  // else overflow
     }
     return;
   }
@@ -693,11 +648,86 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
 // walkers of S lanes (S from the mean segment length) own equal contiguous shares of the batch's
 // virtual range and step S ids at a time, kSpU loads in flight per lane.  Returns early (uniformly)
 // when *flag is raised.
+// One batch of segments: this thread's segment (tid < nb) is len 16-B groups at src[start ..).  The
+// lengths are block-scanned into virtual starts; walkers of S lanes (S from the mean segment length)
+// own equal contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight
+// per lane, applying op to every id.  Returns the batch's groups (uniform); ends with a barrier.
+__device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
+                                         int64_t nsrc, int nb, uint32_t len, int64_t start, const WalkOp &op) {
+  const int tid = threadIdx.x;
+  uint32_t total;
+  const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
+  if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
+  const uint32_t mean = total / uint32_t(nb);
+  const uint32_t S = mean >= 12 ? 16u : 4u;
+  const uint32_t nW = kSpThreads / S;
+  if (tid < nb) {
+    L.vst[tid] = ex;
+    L.seg[tid] = start - int64_t(ex);
+    if (len) {
+      const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
+      const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
+      for (uint32_t q = q0; q < q1 && q < nW; q++) L.qstart[q] = tid;
+    }
+  }
+  if (tid == 0) L.vst[nb] = total;
+  __syncthreads();
+  const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
+  const uint32_t lo = uint32_t(uint64_t(total) * q / nW), hi = uint32_t(uint64_t(total) * (q + 1) / nW);
+  uint32_t g = lo + ql;
+  if (g < hi) {
+    int32_t cur = L.qstart[q];
+    uint32_t next = L.vst[cur + 1];
+    int64_t base = L.seg[cur];
+    uint4 v[kSpU] = {};
+    bool ok[kSpU];
+#pragma unroll
+    for (int k = 0; k < kSpU; k++) {
+      const uint32_t gk = g + S * k;
+      ok[k] = gk < hi;
+      if (ok[k]) {
+        while (gk >= next) {
+          cur++;
+          next = L.vst[cur + 1];
+          base = L.seg[cur];
+        }
+        v[k] = BCHK(A, base + gk >= 0 && base + gk < nsrc, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
+      }
+    }
+    for (; g < hi; g += S * kSpU) {
+      uint4 vn[kSpU] = {};
+      bool okn[kSpU];
+#pragma unroll
+      for (int k = 0; k < kSpU; k++) {
+        const uint32_t gk = g + S * (kSpU + k);
+        okn[k] = gk < hi;
+        if (okn[k]) {
+          while (gk >= next) {
+            cur++;
+            next = L.vst[cur + 1];
+            base = L.seg[cur];
+          }
+          vn[k] = BCHK(A, base + gk >= 0 && base + gk < nsrc, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kSpU; k++)
+        if (ok[k]) sp_apply_group(A, L, S_, op, v[k]);
+#pragma unroll
+      for (int k = 0; k < kSpU; k++) {
+        v[k] = vn[k];
+        ok[k] = okn[k];
+      }
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
 __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0,
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
   const int tid = threadIdx.x;
-  const uint4 *__restrict__ ar = A.tarena;
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
     uint32_t len = 0;
@@ -710,95 +740,10 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
       len = okt ? uint32_t(tbu[full ? A.T : t1] - s0) : 0u;
       start = s0;
     }
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
-    if (total == 0) continue;  // uniform (scalar branch): no barrier is skipped by part of the block
-    walked += total;
-    const uint32_t mean = total / uint32_t(nb);
-    const uint32_t S = mean >= 12 ? 16u : 4u;
-    const uint32_t nW = kSpThreads / S;
-    if (tid < nb) {
-      L.vst[tid] = ex;
-      L.seg[tid] = start - int64_t(ex);
-      if (len) {
-        const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
-        const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
-        for (uint32_t q = q0; q < q1 && q < nW; q++) L.qstart[q] = tid;
-      }
-    }
-    if (tid == 0) L.vst[nb] = total;
-    __syncthreads();
-    const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
-    const uint32_t lo = uint32_t(uint64_t(total) * q / nW), hi = uint32_t(uint64_t(total) * (q + 1) / nW);
-    uint32_t g = lo + ql;
-    if (g < hi) {
-      int32_t cur = L.qstart[q];
-      uint32_t next = L.vst[cur + 1];
-      int64_t base = L.seg[cur];
-      uint4 v[kSpU] = {};
-      bool ok[kSpU];
-#pragma unroll
-      for (int k = 0; k < kSpU; k++) {
-        const uint32_t gk = g + S * k;
-        ok[k] = gk < hi;
-        if (ok[k]) {
-          while (gk >= next) {
-            cur++;
-            next = L.vst[cur + 1];
-            base = L.seg[cur];
-          }
-          v[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_groups, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
-        }
-      }
-      for (; g < hi; g += S * kSpU) {
-        uint4 vn[kSpU] = {};
-        bool okn[kSpU];
-#pragma unroll
-        for (int k = 0; k < kSpU; k++) {
-          const uint32_t gk = g + S * (kSpU + k);
-          okn[k] = gk < hi;
-          if (okn[k]) {
-            while (gk >= next) {
-              cur++;
-              next = L.vst[cur + 1];
-              base = L.seg[cur];
-            }
-            vn[k] = BCHK(A, base + gk >= 0 && base + gk < A.n_groups, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kSpU; k++)
-          if (ok[k]) sp_apply_group(A, L, S_, op, v[k]);
-#pragma unroll
-        for (int k = 0; k < kSpU; k++) {
-          v[k] = vn[k];
-          ok[k] = okn[k];
-        }
-      }
-    }
-    __syncthreads();
+    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, len, start, op);
     if (uni(S_.flag)) break;
   }
   return walked;
-}
-
-// Walk n contiguous groups of the workgroup's scratch (a gathered tile range), applying op (0 or 1)
-// to every id; kSpU loads in flight per thread.  Ends with a barrier.
-__device__ inline void sp_walk_range(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t g0, uint32_t n,
-                                     const WalkOp &op) {
-  const uint4 *__restrict__ src = A.scratch + g0;
-  const uint4 sink = make_uint4(kSink, kSink, kSink, kSink);
-  for (uint32_t g = threadIdx.x; g < n; g += kSpThreads * kSpU) {
-    uint4 v[kSpU];
-#pragma unroll
-    for (int k = 0; k < kSpU; k++) {
-      const uint32_t gk = g + k * kSpThreads;
-      v[k] = gk < n ? src[gk] : sink;
-    }
-#pragma unroll
-    for (int k = 0; k < kSpU; k++) sp_apply_group(A, L, S_, op, v[k]);
-  }
-  __syncthreads();
 }
 
 // Global stores of this workgroup made visible to its own later global loads.  __syncthreads() only
@@ -1040,7 +985,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   }
   const int64_t n_work = A.tot->n_chunks;
 #ifdef COOC_SP_STATS
-  unsigned long long st_[16] = {};
+  if (threadIdx.x < 16) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -1081,9 +1026,24 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       S_.row_begin = S_.slab_cur;
       S_.row_n = 0;
     }
-    if (gather) {
-      if (tid <= A.T) S_.bstart[tid] = A.bst[int64_t(it.gslot) * (A.T + 1) + tid];
-      if (tid < A.T) S_.bcur[tid] = 0u;
+    if (gather && tid < 64) {
+      // bucket capacity of tile t >= 1 from the item's pair work Wi and contributions ci: a user
+      // holds lambda = Wi g_t / ci of its ids on average, a (user, tile) segment of x ids takes
+      // ceil(x / 4) groups, ~ P(x > 0) + (lambda - 1)^+ / 4 for Poisson x (an upper bound for a
+      // mixture of users); 10% + 32 groups of slack.  A bucket that still overflows only sends its
+      // tile's chunk back to walking the lists.
+      const float Wi = float(A.epre[k1] - A.epre[k0]), ci = float(max<int64_t>(1, k1 - k0));
+      uint32_t cap = 0;
+      if (tid >= 1 && tid < A.T) {
+        const float lam = Wi * A.gmass[tid] / ci;
+        cap = uint32_t(1.1f * ci * ((1.f - __expf(-lam)) + 0.25f * fmaxf(0.f, lam - 1.f))) + 32u;
+      }
+      const uint32_t inc = wave_incl_scan(cap);
+      if (tid < A.T) {
+        S_.bstart[tid] = inc - cap;
+        S_.bcur[tid] = 0u;
+      }
+      if (tid == A.T - 1) S_.bstart[A.T] = inc;
     }
     __syncthreads();
     gather = gather && uni(S_.bstart[A.T]) <= uint32_t(A.scr_cap);
@@ -1117,12 +1077,19 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       if (gather && t == 0) {  // tile 0 (a dense chunk) counted, the other tiles' groups to their buckets
         op.mode = 2;
         walked = sp_walk(A, L, S_, k0, k1, 0, A.T, true, op);
+        if (tid < 64) {
+          const bool o = tid >= 1 && tid < A.T && S_.bcur[tid] > S_.bstart[tid + 1] - S_.bstart[tid];
+          const uint64_t m = __ballot(o);
+          if (tid == 0) S_.ovf = m;
+        }
         sp_global_sync();  // the buckets are read back by other waves (and this item's lines are new)
-      } else if (gather) {     // a gathered tile range: contiguous in the scratch
-        const uint32_t g0 = uni(S_.bstart[t]), g1 = uni(S_.bstart[t1]);
-        sp_walk_range(A, L, S_, op.sbase + g0, g1 - g0, op);
-        walked = g1 - g0;
-      } else {
+      } else if (gather && !(uint64_t(uni(int64_t(S_.ovf))) & (((t1 < 64 ? (1ull << t1) : 0ull) - 1ull) & ~((1ull << t) - 1ull)))) {
+        // a gathered tile range: the filled parts of its tiles' buckets, walked as one batch
+        const int nb = t1 - t;
+        const uint32_t len = tid < nb ? S_.bcur[t + tid] : 0u;
+        const int64_t start = tid < nb ? op.sbase + S_.bstart[t + tid] : 0;
+        walked = sp_walk_batch(A, L, S_, A.scratch, int64_t(gridDim.x) * A.scr_cap, nb, len, start, op);
+      } else {  // (also a gathered chunk whose bucket overflowed)
         walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
       }
       const unsigned long long c_walked = STAT_CLOCK();
@@ -1147,7 +1114,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       }
       const uint32_t self = uint32_t(k1 - k0);  // the -1 at column a per contribution (whole rows)
       if (split) {
-        uint32_t *dst = A.staging + int64_t(A.split_slot[a]) * A.M + c0;
+        uint32_t *dst = A.staging + int64_t(A.split_slot[a]) * A.sstride + c0;
         for (int32_t i = tid; i < c1 - c0; i += kSpThreads) {
           const uint32_t v = L.R[i];
           if (v) {
@@ -1194,53 +1161,76 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   }
 #ifdef COOC_SP_STATS
   if (tid == 0) {
-    st_[13] = STAT_CLOCK() - t_start;
-    for (int k = 0; k < 16; k++) atomicAdd(A.stats + k, st_[k]);
+    S_.st[13] = STAT_CLOCK() - t_start;
+    for (int k = 0; k < 16; k++) atomicAdd(A.stats + k, S_.st[k]);
   }
 #endif
 }
 
 // Split rows: the staging row (self term applied on the fly) compacted in column order into an
 // exact-size region; the uint32 overflow check compares the count sum with the closed-form row sum.
-__global__ __launch_bounds__(kSpThreads) void k_sp_split_finalize(const int32_t *__restrict__ split_row,
-                                                                   const uint32_t *__restrict__ staging, int32_t M,
-                                                                   const int64_t *__restrict__ row_ptr,
-                                                                   const int64_t *__restrict__ rowsum,
-                                                                   int32_t *__restrict__ col_out,
-                                                                   uint32_t *__restrict__ cnt_out,
-                                                                   unsigned long long *__restrict__ bump, int64_t cap,
-                                                                   int64_t *__restrict__ row_base,
-                                                                   int32_t *__restrict__ row_nnz,
-                                                                   PlanTotals *__restrict__ tot) {
-  __shared__ uint32_t s_w[kSpWaves];
-  __shared__ uint64_t s_red[kSpWaves];
+// One 1,024-thread block per row; staging rows have a 16-B aligned stride, so every lane reads
+// kFinU x 4 counters (16-B loads) per step and the waves own 4,096-column-aligned ranges.
+constexpr int kFinThreads = 1024, kFinWaves = kFinThreads / 64, kFinU = 4;
+__global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t *__restrict__ split_row,
+                                                                    const uint32_t *__restrict__ staging, int64_t stride,
+                                                                    int32_t M, const int64_t *__restrict__ row_ptr,
+                                                                    const int64_t *__restrict__ rowsum,
+                                                                    int32_t *__restrict__ col_out,
+                                                                    uint32_t *__restrict__ cnt_out,
+                                                                    unsigned long long *__restrict__ bump, int64_t cap,
+                                                                    int64_t *__restrict__ row_base,
+                                                                    int32_t *__restrict__ row_nnz,
+                                                                    PlanTotals *__restrict__ tot) {
+  __shared__ uint32_t s_w[kFinWaves];
+  __shared__ uint64_t s_red[kFinWaves];
   __shared__ int64_t s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t s = blockIdx.x;
   const int32_t a = split_row[s];
   const uint32_t self = uint32_t(row_ptr[a + 1] - row_ptr[a]);
-  const uint32_t *row = staging + int64_t(s) * M;
-  const int32_t per = ((M + kSpWaves - 1) / kSpWaves + 63) & ~63;
+  const uint32_t *row = staging + int64_t(s) * stride;
+  constexpr int32_t kStep = 64 * 4 * kFinU;  // columns per wave step
+  const int32_t per = ((M + kFinWaves - 1) / kFinWaves + kStep - 1) / kStep * kStep;
   const int32_t lo = min(M, wave * per), hi = min(M, lo + per);
-  auto val = [&](int32_t b) -> uint32_t {
-    if (b >= hi) return 0u;
-    const uint32_t v = row[b];
-    return b == a ? v - self : v;
+  auto load = [&](int32_t b, uint32_t v[4]) {
+    if (b + 3 < hi) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(row + b);
+      v[0] = q.x;
+      v[1] = q.y;
+      v[2] = q.z;
+      v[3] = q.w;
+    } else {
+      for (int k = 0; k < 4; k++) v[k] = b + k < hi ? row[b + k] : 0u;
+    }
+    for (int k = 0; k < 4; k++)
+      if (b + k == a) v[k] -= self;
   };
   uint32_t cnt = 0;
   uint64_t sum = 0;
-  for (int32_t b = lo + lane; b < hi; b += 64) {
-    const uint32_t v = val(b);
-    cnt += v != 0u;
-    sum += v;
+  for (int32_t b0 = lo; b0 < hi; b0 += kStep) {
+    uint32_t v[kFinU][4];
+#pragma unroll
+    for (int u = 0; u < kFinU; u++) load(b0 + (u * 64 + lane) * 4, v[u]);
+#pragma unroll
+    for (int u = 0; u < kFinU; u++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        cnt += v[u][k] != 0u;
+        sum += v[u][k];
+      }
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (lane == 0) s_w[wave] = cnt;
-  const uint64_t total_sum = block_sum_u64(sum, s_red);
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) s_red[wave] = sum;
+  __syncthreads();
   uint32_t off = 0, tot_n = 0;
-  for (int w = 0; w < kSpWaves; w++) {
+  uint64_t total_sum = 0;
+  for (int w = 0; w < kFinWaves; w++) {
     off += w < wave ? s_w[w] : 0u;
     tot_n += s_w[w];
+    total_sum += s_red[w];
   }
   if (tid == 0) {
     int64_t b = int64_t(atomicAdd(bump, (unsigned long long)tot_n));
@@ -1257,16 +1247,26 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split_finalize(const int32_t 
   const int64_t base = s_base;
   if (base < 0) return;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int32_t b0 = lo; b0 < hi; b0 += 64) {
-    const int32_t b = b0 + lane;
-    const uint32_t v = val(b);
-    const uint64_t m = __ballot(v != 0u);
-    if (v) {
-      const int64_t pos = base + off + uint32_t(__popcll(m & lt_mask));
-      col_out[pos] = b;
-      cnt_out[pos] = v;
+  for (int32_t b0 = lo; b0 < hi; b0 += kStep) {
+    uint32_t v[kFinU][4];
+#pragma unroll
+    for (int u = 0; u < kFinU; u++) load(b0 + (u * 64 + lane) * 4, v[u]);
+#pragma unroll
+    for (int u = 0; u < kFinU; u++) {
+      const int32_t b = b0 + (u * 64 + lane) * 4;
+      const uint32_t c = (v[u][0] != 0u) + (v[u][1] != 0u) + (v[u][2] != 0u) + (v[u][3] != 0u);
+      const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
+      int64_t pos = base + off + uint32_t(__popcll(m0 & lt_mask)) + 2u * uint32_t(__popcll(m1 & lt_mask)) +
+                    4u * uint32_t(__popcll(m2 & lt_mask));
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (v[u][k]) {
+          col_out[pos] = b + k;
+          cnt_out[pos] = v[u][k];
+          pos++;
+        }
+      off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2));
     }
-    off += uint32_t(__popcll(m));
   }
 }
 
@@ -1471,8 +1471,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipGetLastError());
   }
   SPT("queue");
+  const int64_t sstride = (int64_t(M) + 3) & ~int64_t(3);  // 16-B aligned staging rows
   if (n_split > 0) {
-    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
+    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(sstride);
     COOC_TRY(staging_.reserve(need));
   }
   // gather scratch: a bucket region per workgroup for the largest expected tail (+25%); a work item
@@ -1490,16 +1491,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
     if (need > sp_scr_.cap && (need > (f0 + sp_scr_.cap) / 4 || !sp_scr_.reserve(need).ok())) scr_cap = 0;
   }
-  const int64_t n_gather = T < 64 ? h_tot_->n_gather_rows + h_tot_->n_split_work : 0;  // bucket-start slots
-  if (scr_cap > 0 && n_gather > 0) {
-    const size_t nb = sizeof(uint32_t) * size_t(n_gather) * size_t(T + 1);
-    COOC_TRY(sp_bst_.reserve(nb));
-    COOC_HIP_TRY(hipMemsetAsync(sp_bst_.p, 0, nb, s));
-    k_sp_tail_count<<<dim3(1024, 8), 256, 0, s>>>(sp_queue_.as<SpWork>(), n_work, vals, sp_tb_.as<int32_t>(), T,
-                                                  sp_bst_.as<uint32_t>());
-    k_sp_tail_scan<<<unsigned(std::min<int64_t>(4096, (n_gather + 3) / 4)), 256, 0, s>>>(tot, T, sp_bst_.as<uint32_t>());
-    COOC_HIP_TRY(hipGetLastError());
-  }
+  const int64_t n_gather = T < 64 ? h_tot_->n_gather_rows + h_tot_->n_split_work : 0;  // gather items (bound)
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -1519,7 +1511,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.vals = vals;
   proto.tb = sp_tb_.as<int32_t>();
   proto.tarena = sp_arena_.as<uint4>();
-  proto.bst = sp_bst_.as<uint32_t>();
+  proto.epre = epre;
+  proto.gmass = gmass;
   proto.split_slot = split_slot_.as<int32_t>();
   proto.bump = bump_.as<unsigned long long>();
   proto.slab = slab;
@@ -1536,10 +1529,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
     COOC_TRY(cnt_.reserve(sizeof(uint32_t) * size_t(cap + 1)));
-    if (n_split > 0) COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, sizeof(uint32_t) * size_t(n_split) * size_t(M), s));
+    if (n_split > 0)
+      COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, sizeof(uint32_t) * size_t(n_split) * size_t(sstride), s));
     k_sp_reset_run<<<1, 1, 0, s>>>(tot, qctr, bump_.as<unsigned long long>());
     SpArgs A = proto;
     A.staging = staging_.as<uint32_t>();
+    A.sstride = sstride;
     A.col_out = col_.as<int32_t>();
     A.cnt_out = cnt_.as<uint32_t>();
     A.cap = cap;
@@ -1588,8 +1583,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
   SPT("main");
     if (n_split > 0) {
-      k_sp_split_finalize<<<unsigned(n_split), kSpThreads, 0, s>>>(
-          split_row_.as<int32_t>(), staging_.as<uint32_t>(), M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
+      k_sp_split_finalize<<<unsigned(n_split), kFinThreads, 0, s>>>(
+          split_row_.as<int32_t>(), staging_.as<uint32_t>(), sstride, M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
           cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
           tot);
       COOC_HIP_TRY(hipGetLastError());
