@@ -108,7 +108,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["c3", "c2"], default="c3")
+    ap.add_argument("--config", choices=["c3", "c5", "c2"], default="c3")
+    ap.add_argument("--topk", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -128,7 +129,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.config == "c3":
+    large = args.config in ("c3", "c5")
+    if large:
         U8 = datagen.C3_USERS // 8
         u0, u1 = rank * U8, (rank + 1) * U8
         up, it = datagen.c3_users(u0, u1, device=dev)
@@ -140,6 +142,9 @@ def main():
                     f"datagen.c3_users seed {datagen.C3_SEED}: users [r*1.25e6, (r+1)*1.25e6) on rank r "
                     f"(1/8 of 1e7 users per GPU; the whole 1e9-interaction log at 8 GPUs), 1e6 items, Zipf(1.0) "
                     "with replacement, lognormal lengths of mean 100, one window")
+        if args.config == "c5":
+            workload = (f"C5 (BASELINE configs[4]): co-occurrence counts + LLR scoring of every entry + per-item "
+                        f"top-{args.topk} (ItemRowRescorer...java:195-241) on " + workload[:1].lower() + workload[1:])
     else:
         d = datagen.config_c2(seed=2 + rank)
         up = torch.from_numpy(d["user_ptr"]).to(dev)
@@ -156,12 +161,32 @@ def main():
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
     core.set_kernel_timing(True)
 
-    def step():
+    topk_ms = []
+    if args.config == "c5":
+        tk_sizes = torch.empty(M, dtype=torch.int32, device=dev)
+        tk_vals = torch.empty((M, args.topk), dtype=torch.int32, device=dev)
+        tk_scores = torch.empty((M, args.topk), dtype=torch.float64, device=dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def count():
         if world == 1:
             return core.count_device(up, it)  # on torch's current stream; returns after it drained
-        if args.config == "c3":
+        if large:
             return sharding.count_owned(core, up, it)
         return sharding.count_records(core, up, it)
+
+    def step():
+        r = count()
+        if args.config == "c5":  # LLR + top-k of every (owned) row, resident on the device
+            ev0.record()
+            if world == 1:
+                core.topk_batch_device(args.topk, tk_sizes, tk_vals, tk_scores)
+            else:
+                sharding.topk_owned(core, args.topk)
+            ev1.record()
+            ev1.synchronize()
+            topk_ms.append(ev0.elapsed_time(ev1))
+        return r
 
     for _ in range(args.warmup):
         step()
@@ -182,7 +207,7 @@ def main():
     if world == 1:
         assert res.observed == P_local, "pair count mismatch"
         D, P_counted, N_seen, U_seen = int(res.nnz), int(res.observed), N, U
-    elif args.config == "c3":
+    elif large:
         D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.local_observed), res.n_interactions_all, res.n_users_all
     else:
         D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.owned.observed), N, U
@@ -193,7 +218,7 @@ def main():
         s = stats[1:].clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         elapsed, p_total, d_total = float(t.item()), float(s[0].item()), float(s[1].item())
-        if args.config == "c3":
+        if large:
             assert int(round(p_total)) == res.observed, "global pair count mismatch"
     else:
         p_total, d_total = float(P_local), float(D)
@@ -224,7 +249,7 @@ def main():
             "output": "padded CSR (row_base, row_nnz, col int32, cnt uint32) in HBM, exact counts",
             "parallelism": f"users sharded over {world} GPU(s)" + (
                 "; rows owned by frequency-snake order, histories all-gathered over RCCL" if world > 1 and
-                args.config == "c3" else "; rows owned by a mod N, records exchange over RCCL" if world > 1 else ""),
+                large else "; rows owned by a mod N, records exchange over RCCL" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -252,8 +277,12 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if args.config == "c5":
+        out["config"]["topk"] = args.topk
+        out["config"]["output"] += f"; top-{args.topk} heaps (sizes, values, scores) per row in HBM"
+        out["topk_ms"] = float(np.median(topk_ms))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if args.config == "c3":
+        if large:
             bu, bi = datagen.c3_users(0, 200_000)
             out["cpu_baseline"] = cpu_baseline(bu, bi, M, "the same C3 log")
         else:

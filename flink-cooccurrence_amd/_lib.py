@@ -87,6 +87,7 @@ _SIGS = {
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
     "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
     "cooc_copy_topk_batch": (ctypes.c_int, [vp, i32p, i32p, f64p]),
+    "cooc_topk_batch_device": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "cooc_llr": (ctypes.c_int, [vp, ctypes.c_int64, i64p, f64p]),
     "cooc_topk_items": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p, i32p, i32p, f64p]),
     "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),

@@ -183,6 +183,17 @@ class CooccurrenceCore:
         check(L.cooc_copy_topk_batch(self._h, _p(sizes, i32p), _p(vals, i32p), _p(scores, f64p)), self._h)
         return sizes, vals, scores
 
+    def topk_batch_device(self, topk: int, sizes, values, scores, rowsum_global=None, exact_scores: bool = False,
+                          stream=None) -> None:
+        """LLR top-k of every row of the last batch into device tensors (sizes int32 [M], values int32
+        [M, k], scores float64 [M, k]) on torch's current stream.  rowsum_global (int64 device [M]):
+        the all-reduced row sums of a multi-GPU run (rows not owned here come out with size 0)."""
+        check(_lib.load().cooc_topk_batch_device(
+            self._h, topk, _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0,
+            None if rowsum_global is None else ctypes.c_void_p(rowsum_global.data_ptr()),
+            ctypes.c_void_p(sizes.data_ptr()), ctypes.c_void_p(values.data_ptr()), ctypes.c_void_p(scores.data_ptr()),
+            _stream_arg(stream, sizes)), self._h)
+
     def llr(self, k4) -> np.ndarray:
         """LogLikelihood.logLikelihoodRatio of each (k11, k12, k21, k22) row, on the device."""
         k = np.ascontiguousarray(k4, np.int64).reshape(-1, 4)

@@ -151,6 +151,17 @@ int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream
   });
 }
 
+int cooc_topk_batch_device(cooc_ctx *ctx, int32_t topk, int32_t flags, const int64_t *d_rowsum_global,
+                           int32_t *d_sizes, int32_t *d_values, double *d_scores, void *hip_stream) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    if (!d_sizes || !d_values || !d_scores) return fail(ctx, COOC_ERR_ARG, "bad topk output buffers");
+    Status s = ctx->topk_batch_device(topk, flags, d_rowsum_global, d_sizes, d_values, d_scores,
+                                      static_cast<hipStream_t>(hip_stream));
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
 int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;

@@ -219,16 +219,26 @@ Status cooc_ctx::topk_batch(int32_t topk, int32_t flags, hipStream_t s) {
   COOC_TRY(b_tk_size.reserve(sizeof(int32_t) * M));
   COOC_TRY(b_tk_val.reserve(sizeof(int32_t) * size_t(M) * topk));
   COOC_TRY(b_tk_score.reserve(sizeof(double) * size_t(M) * topk));
-  COOC_TRY(b_obs3.reserve(sizeof(int64_t) * 4));
-  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
-  const cooc::CountResult &r = batch_result;
-  COOC_TRY(cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense, r.rowsum,
-                                      (flags & COOC_FLAG_EXACT_SCORES) != 0, topk, b_obs3.as<int64_t>(),
-                                      b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(), b_tk_score.as<double>()));
+  COOC_TRY(topk_batch_device(topk, flags, nullptr, b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(),
+                             b_tk_score.as<double>(), s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   batch_topk = topk;
   batch_topk_flags = flags & COOC_FLAG_EXACT_SCORES;
   return Status::Ok();
+}
+
+Status cooc_ctx::topk_batch_device(int32_t topk, int32_t flags, const int64_t *d_rowsum_global, int32_t *d_sizes,
+                                   int32_t *d_values, double *d_scores, hipStream_t s) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  if (topk <= 0) return Status{COOC_ERR_ARG, std::to_string(topk) + " is <= 0"};  // ItemRowRescorer...java:52-54
+  COOC_HIP_TRY(hipSetDevice(device));
+  const int32_t M = cfg.n_items;
+  COOC_TRY(b_obs3.reserve(sizeof(int64_t) * 4));
+  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  const cooc::CountResult &r = batch_result;
+  return cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense,
+                                    d_rowsum_global ? d_rowsum_global : r.rowsum, (flags & COOC_FLAG_EXACT_SCORES) != 0,
+                                    topk, b_obs3.as<int64_t>(), d_sizes, d_values, d_scores);
 }
 
 Status cooc_ctx::llr(int64_t n, const int64_t *k, double *out) {

@@ -112,6 +112,10 @@ struct cooc_ctx {
   cooc::Status copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                           int32_t *rowsum32);
   cooc::Status topk_batch(int32_t topk, int32_t flags, hipStream_t s);
+  // top-k into caller device buffers; d_rowsum_global (may be NULL) replaces the batch's row sums
+  // (multi-GPU: the all-reduced row sums, so that k21 and the observed total are the whole log's)
+  cooc::Status topk_batch_device(int32_t topk, int32_t flags, const int64_t *d_rowsum_global, int32_t *d_sizes,
+                                 int32_t *d_values, double *d_scores, hipStream_t s);
   cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
   cooc::Status llr(int64_t n, const int64_t *k, double *out);
   cooc::Status topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,

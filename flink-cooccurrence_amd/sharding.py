@@ -213,3 +213,28 @@ def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     dist.all_reduce(obs, group=group)
     return OwnedResult(rank, world, res, owner, int(obs.item()), int(res.observed), int(lens_cat.numel()), n_all,
                        4 * (n_all - n) + 8 * (int(lens_cat.numel()) - n_users))
+
+
+@dataclass
+class TopkResult:
+    sizes: torch.Tensor     # int32 [n_items]: heap sizes (0 for rows owned elsewhere)
+    values: torch.Tensor    # int32 [n_items, k]: IntDoublePriorityQueue heap positions 1..size
+    scores: torch.Tensor    # float64 [n_items, k]
+    rowsum: torch.Tensor    # int64 [n_items]: the all-reduced row sums the scores used
+
+
+def topk_owned(core, topk: int, group=None, exact_scores: bool = False, stream=None) -> TopkResult:
+    """C5 after count_owned: the rows' LLR top-k on their owner (ItemRowRescorer...java:195-241).
+    The owned results' row sums are all-reduced first -- the reference broadcasts its row-sum stream to
+    every rescorer (FlinkCooccurrences.java:163) -- so that k21 = rowSum(b) - k11 and the observed total
+    are the whole log's; each rank then scores only the rows it owns."""
+    M = core.n_items
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rowsum = torch.empty(M, dtype=torch.int64, device=dev)
+    core.copy_rowsum_device(rowsum, stream)
+    dist.all_reduce(rowsum, group=group)
+    sizes = torch.empty(M, dtype=torch.int32, device=dev)
+    values = torch.empty((M, topk), dtype=torch.int32, device=dev)
+    scores = torch.empty((M, topk), dtype=torch.float64, device=dev)
+    core.topk_batch_device(topk, sizes, values, scores, rowsum_global=rowsum, exact_scores=exact_scores, stream=stream)
+    return TopkResult(sizes, values, scores, rowsum)

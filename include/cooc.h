@@ -172,6 +172,15 @@ COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uin
  * (heap positions 1..size, least score first; rows without entries have size 0). */
 COOC_API int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream);
 COOC_API int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores);
+/* The same top-k into caller DEVICE buffers on hip_stream (ordered after the count on the caller's
+ * stream; the C5 config keeps its output resident): d_sizes int32[n_items], d_values
+ * int32[n_items*topk], d_scores double[n_items*topk].  d_rowsum_global (device int64[n_items], may be
+ * NULL) replaces the result's own row sums: multi-GPU owners pass the all-reduced row sums (the
+ * broadcast row-sum stream, FlinkCooccurrences.java:163), so that k21 = rowSum(b) - k11 and the
+ * observed total (ItemRowRescorer...java:154,203-240) are the whole log's; rows the context does not
+ * own have no entries and get size 0. */
+COOC_API int cooc_topk_batch_device(cooc_ctx *ctx, int32_t topk, int32_t flags, const int64_t *d_rowsum_global,
+                                    int32_t *d_sizes, int32_t *d_values, double *d_scores, void *hip_stream);
 /* LogLikelihood.logLikelihoodRatio (LogLikelihood.java:41-57) evaluated by the device function the
  * rescoring kernels use: k = host int64[n][4] of (k11, k12, k21, k22), out = host double[n].  For
  * known-answer tests of the device scores (LogLikelihoodTest.java:14-16). */

@@ -123,3 +123,30 @@ def assert_topk_equal(got, want, rtol=1e-6):
             kth = w_sorted[0]
             margin = max(rtol * abs(kth), 1e-9)
             assert set(gv[gs > kth + margin].tolist()) == set(wv[ws > kth + margin].tolist())
+
+
+def oracle_row_topk(oracle, cols, cnt16, rs32, a: int, k: int, observed: int):
+    """The rescorer's heap for row a (ItemRowRescorer...java:195-223) fed in ascending column order
+    with the reference's views: int16 counts, int32 row sums, observed = sum of the int32 row sums."""
+    q = oracle.PriorityQueue(k)
+    for b, c16 in zip(np.asarray(cols).tolist(), np.asarray(cnt16).tolist()):
+        sc = oracle.score_item(int(c16), int(rs32[a]), int(rs32[b]), observed)
+        if q.size() < k:
+            q.add(b, sc)
+        elif sc > q.least_score():
+            q.update(b, sc)
+    return q.entries()
+
+
+def assert_row_topk(size, vals, scores, want, rtol=1e-6, where=""):
+    """One row's heap against the oracle's: scores within rtol (NaN where NaN), and the identical heap
+    layout when every score agrees bit for bit."""
+    assert int(size) == len(want), f"{where}: heap size {size} != {len(want)}"
+    wv = np.array([v for v, _ in want], np.int32)
+    ws = np.array([x for _, x in want], np.float64)
+    gs = np.asarray(scores[: int(size)], np.float64)
+    assert np.array_equal(np.isnan(gs), np.isnan(ws)), f"{where}: NaN scores differ"
+    fin = ~np.isnan(ws)
+    assert np.allclose(gs[fin], ws[fin], rtol=rtol, atol=1e-9), f"{where}: scores differ"
+    if np.array_equal(gs[fin], ws[fin]):
+        assert np.array_equal(np.asarray(vals[: int(size)]), wv), f"{where}: heap layout differs"

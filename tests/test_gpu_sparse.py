@@ -204,3 +204,73 @@ def test_owned_parts_union_is_whole(pkg, torch_cuda):
                     gc, gn = r.row(a)
                     assert np.array_equal(gc, wc) and np.array_equal(gn, wn)
     assert nnz_total == whole.nnz
+
+
+def test_c5_topk_c3_shape_vs_oracle(pkg, oracle, torch_cuda):
+    """C5 (LLR + top-50) on the large-universe path: the first 1,500 users of the C3 log, sampled rows'
+    heaps against the oracle's rescorer (ItemRowRescorer...java:195-241), tolerance 1e-6 relative."""
+    from tests._helpers import assert_row_topk, oracle_row_topk
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.c3_users(0, 1500)
+    M, k = datagen.C3_ITEMS, 50
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        got = core.count(up, it)
+        rs32 = got.rowsum32.astype(np.int64)
+        observed = int(rs32.sum())
+        rows = np.flatnonzero(np.diff(got.row_ptr))
+        rng = np.random.default_rng(9)
+        sample = np.unique(np.concatenate([rows[:6], rng.choice(rows, 40, replace=False)]))
+        sizes, vals, scores = core.topk_items(sample, k)
+        empty = np.setdiff1d(np.arange(0, M, 9973), rows)[:5]
+        esz, _, _ = core.topk_items(empty, k)
+    assert np.all(esz == 0)
+    for i, a in enumerate(sample.tolist()):
+        s, e = got.row_ptr[a], got.row_ptr[a + 1]
+        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed)
+        assert_row_topk(sizes[i], vals[i], scores[i], want, where=f"row {a}")
+
+
+def test_c5_topk_owned_parts_vs_whole(pkg, torch_cuda):
+    """Multi-GPU C5 on one GPU: 3 owned parts, each scored with the summed (all-reduced) row sums
+    through cooc_topk_batch_device, equal the unpartitioned top-k on every owned row (bit for bit:
+    same scores, same heap); rows owned elsewhere have size 0."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen, sharding
+
+    up, it = datagen.c3_users(0, 3000)
+    M, k = datagen.C3_ITEMS, 50
+    dev = torch.device("cuda")
+    up_d, it_d = torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev)
+    freq_d = torch.from_numpy(np.bincount(it, minlength=M).astype(np.int64)).to(dev)
+    owner_d = sharding.snake_owner(freq_d, 3)
+    owner = owner_d.cpu().numpy()
+
+    def topk(core, rowsum=None):
+        sz = torch.empty(M, dtype=torch.int32, device=dev)
+        v = torch.empty((M, k), dtype=torch.int32, device=dev)
+        sc = torch.empty((M, k), dtype=torch.float64, device=dev)
+        core.topk_batch_device(k, sz, v, sc, rowsum_global=rowsum)
+        return sz.cpu().numpy(), v.cpu().numpy(), sc.cpu().numpy()
+
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        core.count_device(up_d, it_d)
+        w_sz, w_v, w_sc = topk(core)
+    parts, rowsum = [], torch.zeros(M, dtype=torch.int64, device=dev)
+    for part in range(3):
+        core = pkg.CooccurrenceCore(n_items=M, device=0)
+        core.count_device_owned(up_d, it_d, owner_d, part, freq_d, int(len(it)))
+        rs = torch.empty(M, dtype=torch.int64, device=dev)
+        core.copy_rowsum_device(rs)
+        rowsum += rs
+        parts.append(core)
+    for part, core in enumerate(parts):
+        sz, v, sc = topk(core, rowsum)
+        mine = owner == part
+        assert np.all(sz[~mine] == 0)
+        assert np.array_equal(sz[mine], w_sz[mine])
+        rows = np.flatnonzero(mine & (w_sz > 0))
+        for a in rows[:: max(1, len(rows) // 2000)].tolist():
+            n = int(w_sz[a])
+            assert np.array_equal(v[a, :n], w_v[a, :n]) and np.array_equal(sc[a, :n], w_sc[a, :n], equal_nan=True), f"row {a}"
+        core.close()
