@@ -132,10 +132,12 @@ def main():
     large = args.config in ("c3", "c5")
     if large:
         U8 = datagen.C3_USERS // 8
-        u0, u1 = rank * U8, (rank + 1) * U8
+        # the job's users [0, N U/8): contiguous ranges balanced on sum n_u (n_u - 1)
+        lens_all = datagen.c3_lengths(0, world * U8)
+        u0, u1 = sharding.balanced_user_ranges(np.concatenate([[0], np.cumsum(lens_all)]), world)[rank]
         up, it = datagen.c3_users(u0, u1, device=dev)
         M = datagen.C3_ITEMS
-        P_local = datagen.c3_ordered_pairs(u0, u1)
+        P_local = int(np.sum(lens_all[u0:u1] * (lens_all[u0:u1] - 1)))
         kernel = "k_sp_main"
         pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_sp_main.json"))
         workload = ("C3 Zipf-skewed 1B log (BASELINE configs[2]), shard-invariant generator "

@@ -47,7 +47,7 @@ cooc_ctx::~cooc_ctx() {
   sharder.release();
   counter.release();
   cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
-                          &b_cut_ptr, &b_cut_items, &b_cut_tmp};
+                          &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
   if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);
@@ -238,7 +238,7 @@ Status cooc_ctx::topk_batch_device(int32_t topk, int32_t flags, const int64_t *d
   const cooc::CountResult &r = batch_result;
   return cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense,
                                     d_rowsum_global ? d_rowsum_global : r.rowsum, (flags & COOC_FLAG_EXACT_SCORES) != 0,
-                                    topk, b_obs3.as<int64_t>(), d_sizes, d_values, d_scores);
+                                    topk, b_obs3.as<int64_t>(), b_llr_terms, d_sizes, d_values, d_scores);
 }
 
 Status cooc_ctx::llr(int64_t n, const int64_t *k, double *out) {

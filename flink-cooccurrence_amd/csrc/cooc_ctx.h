@@ -63,7 +63,7 @@ class StreamState {
   DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
   // global state
   bool global_ready_ = false;
-  DevBuf d_global_, d_grs_, d_touched_, d_scan_tmp_, d_scal_, d_topk_val_, d_topk_score_, d_topk_size_;
+  DevBuf d_global_, d_grs_, d_touched_, d_scan_tmp_, d_scal_, d_topk_val_, d_topk_score_, d_topk_size_, d_llr_terms_;
   // last window
   bool have_window_ = false;
   bool empty_window_ = false;  // the last window had no interaction left after user_cut
@@ -135,7 +135,7 @@ struct cooc_ctx {
   cooc::Operator op;
 
   // stateless batch buffers
-  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3;
+  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3, b_llr_terms;
   // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
   cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
   int32_t batch_topk = 0;

@@ -569,7 +569,7 @@ struct SpStatic {
   uint32_t wtot[kSpWaves];
   uint64_t red[kSpWaves];
   int32_t work;
-  uint32_t flag, claims;
+  uint32_t flag;
   int64_t slab_cur, slab_end, row_begin, row_n, pos, copy_from, copy_n;
   int64_t saved_cur, saved_end;  // the workgroup's slab while a big row fills a region of its own
   uint32_t own;
@@ -577,47 +577,48 @@ struct SpStatic {
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
 #ifdef COOC_SP_STATS
-  unsigned long long st[16];
+  unsigned long long st[24];
 #endif
 };
 
-// Insert one partner id into the LDS table (keys store id + 1; 0 = empty).  Linear probing from a
-// multiplicative hash; raises *flag when the probe budget or the fill limit is exceeded.
-__device__ inline void sp_hash_insert(uint32_t *keys, uint32_t *cnts, uint32_t id, uint32_t hshift, uint32_t hmask,
-                                      uint32_t fill_limit, SpStatic &S_) {
-  const uint32_t k = id + 1u;
-  uint32_t h = (id * 0x9E3779B1u) >> hshift;
+// Insert the (up to 4) partner ids of one 16-B group into the LDS table (keys store id + 1; 0 =
+// empty), linear probing from a multiplicative hash.  The ids are probed in lockstep so that their
+// LDS round trips overlap; each probe is one returning compare-and-swap (it claims an empty slot or
+// returns the key that holds it) followed, on a hit, by a non-returning count add.  An id that finds
+// no slot within kMaxProbe probes raises the overflow flag (the chunk is redone with a larger table);
+// the planner sizes tables at <= 1/2 fill, so probe chains stay short.
+__device__ inline void sp_hash_insert4(uint32_t *keys, uint32_t *cnts, const uint4 &v, uint32_t hshift, uint32_t hmask,
+                                       SpStatic &S_) {
+  uint32_t k[4] = {v.x + 1u, v.y + 1u, v.z + 1u, v.w + 1u};  // kSink + 1 == 0: a pad is never inserted
+  uint32_t h[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) h[i] = (k[i] - 1u) * 0x9E3779B1u >> hshift;
   for (int p = 0; p < kMaxProbe; p++) {
-    uint32_t cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == 0u) {
-      cur = atomicCAS(keys + h, 0u, k);
-      if (cur == 0u) {
-        atomicAdd(cnts + h, 1u);
-        if (atomicAdd(&S_.claims, 1u) >= fill_limit) S_.flag = 1u;
-        return;
+    uint32_t cur[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = k[i] ? atomicCAS(keys + h[i], 0u, k[i]) : 0u;
+    bool left = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!k[i]) continue;
+      if (cur[i] == 0u || cur[i] == k[i]) {
+        atomicAdd(cnts + h[i], 1u);
+        k[i] = 0u;
+      } else {
+        h[i] = (h[i] + 1u) & hmask;
+        left = true;
       }
     }
-    if (cur == k) {
-      atomicAdd(cnts + h, 1u);
-      return;
-    }
-    h = (h + 1u) & hmask;
+    if (!left) return;
   }
   S_.flag = 1u;
 }
 
 struct WalkOp {
   int mode;  // 0: dense counters R[id - c0]; 1: hash insert; 2: gather (tile 0 dense, other tiles to buckets)
-  uint32_t c0, hshift, hmask, limit;
+  uint32_t c0, hshift, hmask;
   int64_t sbase;  // gather: the workgroup's scratch
 };
-
-__device__ inline void sp_apply(const SpShared &L, SpStatic &S_, const WalkOp &op, uint32_t id) {
-  if (op.mode == 0)
-    atomicAdd(&L.R[id - op.c0], 1u);
-  else
-    sp_hash_insert(L.R, L.R + kHashMax, id, op.hshift, op.hmask, op.limit, S_);
-}
 
 // One 16-B group of partner ids (one tile's; kSink pads).  Gather mode: a group of tile 0 is counted
 // in the dense tile, any other is appended to its tile's bucket in the workgroup's scratch.
@@ -637,10 +638,14 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
     }
     return;
   }
-  sp_apply(L, S_, op, v.x);
-  if (v.y != kSink) sp_apply(L, S_, op, v.y);
-  if (v.z != kSink) sp_apply(L, S_, op, v.z);
-  if (v.w != kSink) sp_apply(L, S_, op, v.w);
+  if (op.mode == 1) {
+    sp_hash_insert4(L.R, L.R + kHashMax, v, op.hshift, op.hmask, S_);
+    return;
+  }
+  atomicAdd(&L.R[v.x - op.c0], 1u);
+  if (v.y != kSink) atomicAdd(&L.R[v.y - op.c0], 1u);
+  if (v.z != kSink) atomicAdd(&L.R[v.z - op.c0], 1u);
+  if (v.w != kSink) atomicAdd(&L.R[v.w - op.c0], 1u);
 }
 
 // Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
@@ -655,6 +660,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
 __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
                                          int64_t nsrc, int nb, uint32_t len, int64_t start, const WalkOp &op) {
   const int tid = threadIdx.x;
+  const unsigned long long c_b0 = STAT_CLOCK();
   uint32_t total;
   const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
   if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
@@ -672,6 +678,9 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   }
   if (tid == 0) L.vst[nb] = total;
   __syncthreads();
+  const unsigned long long c_b1 = STAT_CLOCK();
+  if (op.mode == 1) STAT_ADD(16, c_b1 - c_b0);
+  if (op.mode == 1) STAT_ADD(18, total);
   const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
   const uint32_t lo = uint32_t(uint64_t(total) * q / nW), hi = uint32_t(uint64_t(total) * (q + 1) / nW);
   uint32_t g = lo + ql;
@@ -721,6 +730,7 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
     }
   }
   __syncthreads();
+  if (op.mode == 1) STAT_ADD(17, STAT_CLOCK() - c_b1);
   return total;
 }
 
@@ -732,6 +742,7 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
     uint32_t len = 0;
     int64_t start = 0;
+    STAT_ADD(19, op.mode == 1 ? 1 : 0);
     if (tid < nb) {  // the segment of tiles [t0, t1) (full: the whole list) in 16-B groups
       const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] : 0u;
       const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
@@ -881,6 +892,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
 __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t H, int32_t c0,
                                        int32_t c1) {
   const int tid = threadIdx.x;
+  const unsigned long long c_h0 = STAT_CLOCK();
   uint32_t *keys = L.R, *cnts = L.R + kHashMax;
   const int per = H / kSpThreads;
   const int32_t nL1 = (c1 - c0 + 1023) >> 10;
@@ -942,7 +954,11 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     cnts[r] = run;
     run += uint32_t(__popc(keys[r]));
   }
+  const unsigned long long c_h1 = STAT_CLOCK();
+  STAT_ADD(20, c_h1 - c_h0);
   const int64_t base = sp_reserve(A, S_, ne);  // (barrier: bases visible)
+  const unsigned long long c_h2 = STAT_CLOCK();
+  STAT_ADD(21, c_h2 - c_h1);
   if (base >= 0) {
 #pragma unroll
     for (int i = 0; i < kHashMax / kSpThreads; i++) {
@@ -956,6 +972,8 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     }
   }
   __syncthreads();
+  STAT_ADD(22, STAT_CLOCK() - c_h2);
+  STAT_ADD(23, ne);
   for (uint32_t r = tid; r < nblk; r += kSpThreads) {
     keys[r] = 0u;
     cnts[r] = 0u;
@@ -985,7 +1003,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   }
   const int64_t n_work = A.tot->n_chunks;
 #ifdef COOC_SP_STATS
-  if (threadIdx.x < 16) S_.st[threadIdx.x] = 0ull;
+  if (threadIdx.x < 24) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -1065,10 +1083,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       const uint32_t lg = dense ? 0u : 31u - uint32_t(__clz(uint32_t(H)));
       op.hshift = 32u - lg;
       op.hmask = uint32_t(H) - 1u;
-      op.limit = uint32_t(H) - uint32_t(H) / 8u;
       if (tid == 0) {
         S_.flag = 0u;
-        S_.claims = 0u;
       }
       __syncthreads();
       const unsigned long long c_walk = STAT_CLOCK();
@@ -1162,7 +1178,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
 #ifdef COOC_SP_STATS
   if (tid == 0) {
     S_.st[13] = STAT_CLOCK() - t_start;
-    for (int k = 0; k < 16; k++) atomicAdd(A.stats + k, S_.st[k]);
+    for (int k = 0; k < 24; k++) atomicAdd(A.stats + k, S_.st[k]);
   }
 #endif
 }
@@ -1550,8 +1566,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
 #ifdef COOC_SP_STATS
     static unsigned long long *d_stats = nullptr;
-    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 16 * 8);
-    hipMemsetAsync(d_stats, 0, 16 * 8, s);
+    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 24 * 8);
+    hipMemsetAsync(d_stats, 0, 24 * 8, s);
     A.stats = d_stats;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
@@ -1597,7 +1613,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipStreamSynchronize(s));
 #ifdef COOC_SP_STATS
     {
-      unsigned long long h[16];
+      unsigned long long h[24];
       hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
       const double g = double(grid);
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
@@ -1606,6 +1622,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
               h[13] / 100.0 / g, h[0] / 100.0 / g, h[1] / 100.0 / g, h[4] / 100.0 / g, h[2] / 100.0 / g, h[3] / 100.0 / g,
               h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0,
               h[15] / 100.0 / g);
+      fprintf(stderr, "[sp stats] hash detail per WG (us): walk scan %.0f walk loop %.0f | groups %.3g batches %llu | "
+              "compact rank %.0f reserve %.0f write %.0f | entries %.3g\n", h[16] / 100.0 / g, h[17] / 100.0 / g,
+              double(h[18]), h[19], h[20] / 100.0 / g, h[21] / 100.0 / g, h[22] / 100.0 / g, double(h[23]));
       fprintf(stderr, "[sp stats] attempt %d: cap %lld slab %lld grid %lld err %lld scr_cap %lld n_gather %lld\n", attempt,
               (long long)cap, (long long)slab, (long long)grid, (long long)err, (long long)A.scr_cap, (long long)n_gather);
     }

@@ -60,7 +60,7 @@ void StreamState::release() {
   DevBuf *all[] = {&arena_,      &d_act_off_,      &d_act_len_,     &d_act_old_,   &d_cbase_,
                    &d_new_items_, &d_new_dst_ptr_, &d_new_dst_,     &d_reloc_,     &d_global_,
                    &d_grs_,       &d_touched_,     &d_scan_tmp_,    &d_scal_,      &d_topk_val_,
-                   &d_topk_score_, &d_topk_size_};
+                   &d_topk_score_, &d_topk_size_, &d_llr_terms_};
   for (DevBuf *b : all) b->release();
   global_ready_ = false;
 }
@@ -271,7 +271,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
     COOC_TRY(d_topk_val_.reserve(sizeof(int32_t) * size_t(M) * topk));
     COOC_TRY(d_topk_score_.reserve(sizeof(double) * size_t(M) * topk));
     COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
-                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_topk_size_.as<int32_t>(),
+                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_, d_topk_size_.as<int32_t>(),
                             d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
   }
   tr.mark("merge_rescore", s);

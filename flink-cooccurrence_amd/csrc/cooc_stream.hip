@@ -119,6 +119,38 @@ __device__ inline double llr(int64_t k11, int64_t k12, int64_t k21, int64_t k22)
   return 2.0 * (row + column - matrix);
 }
 
+// The same function over precomputed x log x terms, in the same operation order (bit-identical when
+// every term is: a term looked up from a table was computed by the same xlogx of the same integer).
+__device__ inline double llr_terms(double all, double x_k11k12, double x_k21k22, double x_k11k21, double x_k12k22,
+                                   double x_k11, double x_k12, double x_k21, double x_k22) {
+#pragma clang fp contract(off)
+  const double row = all - x_k11k12 - x_k21k22;
+  const double column = all - x_k11k21 - x_k12k22;
+  const double matrix = all - x_k11 - x_k12 - x_k21 - x_k22;
+  if (row + column < matrix) return 0.0;
+  return 2.0 * (row + column - matrix);
+}
+
+// Per column b of the rescored rows (the int32 view of its row sum unless exact): rs = rowSum(b) and the
+// terms of an entry with k11 == 1 that depend on b only (ItemRowRescorer...java:230-240): k11 + k21 =
+// rs, k21 = rs - 1, k12 + k22 = observed + 2 - rs.  32 B per column, one line per gathered entry.
+constexpr int kRsR = 8;   // 64-entry steps scored before the heap is fed (per wave)
+struct alignas(32) ColTerms {
+  int64_t rs;
+  double x_rs;   // xlogx(rs)
+  double x_rs1;  // xlogx(rs - 1)
+  double x_or2;  // xlogx(observed + 2 - rs)
+};
+
+__global__ void k_col_terms(int32_t M, const int64_t *__restrict__ grs, const int64_t *__restrict__ obs, int32_t exact,
+                            ColTerms *__restrict__ out) {
+  const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= M) return;
+  const int64_t observed = exact ? obs[1] : obs[0];
+  const int64_t rs = exact ? grs[b] : int64_t(int32_t(uint32_t(uint64_t(grs[b]))));
+  out[b] = ColTerms{rs, xlogx(rs), xlogx(rs - 1), xlogx(observed + 2 - rs)};
+}
+
 // ---- IntDoublePriorityQueue.java:132-205, every lane of the wave runs it on the same LDS heap ----
 __device__ inline void heap_add(int32_t *hv, double *hs, int32_t &size, int32_t value, double score) {
   size++;
@@ -174,55 +206,98 @@ struct CsrRows {
   }
 };
 
-// One wave per rescored row; the wave scores 64 consecutive entries at a time (ascending column =
-// the iteration order contract) and feeds the lanes that can enter the heap to it in lane order,
-// which is exactly the sequential loop of ItemRowRescorer...java:199-223.
+// One wave per rescored row, rows iterated in ascending column order (the tie contract).  The wave
+// scores kRsR steps of 64 entries, then feeds the lanes that can enter the heap to it step by step in
+// lane order, which is exactly the sequential loop of ItemRowRescorer...java:199-223.  Scoring is
+// split by count so that the wave's lanes do not diverge over the expensive case: an entry with
+// k11 == 1 (most of a sparse row) needs one log (every other term comes from the per-column table
+// and the row's constants); the others (hot pairs, wrapped or zero int16 views) are queued in LDS and
+// scored 64 at a time with the full formula (7 logs).  Both are LogLikelihood.java:41-57 in Java's operation order, bit for bit.
 // rows == nullptr: rescored row t is item t.  obs[0] = the rescorer's observed (sum of int
 // deltas), obs[1] = the exact pair count.
 template <class Rows>
 __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__restrict__ n_rows_p, Rows src,
-                          const int64_t *__restrict__ grs, const int64_t *__restrict__ obs, int32_t exact,
+                          const int64_t *__restrict__ grs, const ColTerms *__restrict__ cterm,
+                          const int64_t *__restrict__ obs, int32_t exact,
                           int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
                           double *__restrict__ out_score) {
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + int64_t(waves) * (topk + 1)) + int64_t(wave) * (topk + 1);
+  double *ring = smem + int64_t(waves) * (topk + 1) + (int64_t(waves) * (topk + 1) + 1) / 2;
+  double *rscore = ring + int64_t(wave) * (kRsR * 64) * 2;
+  int32_t *rcol = reinterpret_cast<int32_t *>(rscore + kRsR * 64);
+  int32_t *rq = rcol + kRsR * 64;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const int64_t n_rows = n_rows_p[0];
   const int64_t observed = exact ? obs[1] : obs[0];
   for (int64_t t = int64_t(blockIdx.x) * waves + wave; t < n_rows; t += int64_t(gridDim.x) * waves) {
     const int32_t a = rows ? rows[t] : int32_t(t);
     const int64_t rs_a = exact ? grs[a] : int64_t(int32_t(uint32_t(uint64_t(grs[a]))));
     const int64_t n = src.size(a);
+    // row terms: k11k12 = k11 + k12 = rs_a; with k11 == 1 also k11k12 + k21k22 = observed + 2,
+    // k21k22 = observed + 2 - rs_a, k12 = rs_a - 1
+    const double x_a = xlogx(rs_a), x_all1 = xlogx(observed + 2), x_r1 = xlogx(observed + 2 - rs_a),
+                 x_a1 = xlogx(rs_a - 1);
     int32_t size = 0;
     double least = 0.0;
-    for (int64_t i0 = 0; i0 < n; i0 += 64) {
-      int32_t c = 0;
-      uint32_t v = 0u;
-      if (i0 + lane < n) src.get(a, i0 + lane, c, v);
-      double score = 0.0;
-      if (v != 0u) {
-        // ItemRowRescorer...java:203-205,230-240
+    for (int64_t i0 = 0; i0 < n; i0 += kRsR * 64) {
+      uint32_t npend = 0;
+#pragma unroll 2
+      for (int j = 0; j < kRsR; j++) {
+        int32_t c = 0;
+        uint32_t v = 0u;
+        if (i0 + j * 64 + lane < n) src.get(a, i0 + j * 64 + lane, c, v);
         const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
-        const int64_t rs_b = exact ? grs[c] : int64_t(int32_t(uint32_t(uint64_t(grs[c]))));
-        const int64_t k12 = rs_a - k11;
-        const int64_t k21 = rs_b - k11;
-        const int64_t k22 = observed + k11 - k12 - k21;
-        score = llr(k11, k12, k21, k22);
-      }
-      uint64_t m = __ballot(v != 0u && (size < topk || score > least));
-      while (m) {
-        const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
-        m &= m - 1;
-        const double sc = __shfl(score, l, 64);
-        const int32_t cl = __shfl(c, l, 64);
-        if (size < topk) {
-          heap_add(hv, hs, size, cl, sc);
-        } else if (sc > hs[1]) {
-          heap_update(hv, hs, size, cl, sc);
+        const bool fast = v != 0u && k11 == 1;
+        double score = 0.0;
+        if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+          const ColTerms t = cterm[c];
+          const int64_t k22 = observed + k11 - (rs_a - k11) - (t.rs - k11);
+          score = llr_terms(x_all1, x_a, x_r1, t.x_rs, t.x_or2, 0.0, x_a1, t.x_rs1, xlogx(k22));
         }
-        least = hs[1];
+        const bool slow = v != 0u && !fast;
+        const uint64_t sm = __ballot(slow);
+        if (slow) rq[npend + uint32_t(__popcll(sm & lt))] = j * 64 + lane;
+        npend += uint32_t(__popcll(sm));
+        rscore[j * 64 + lane] = slow ? __longlong_as_double(k11) : score;  // slow: k11 parked until scored
+        rcol[j * 64 + lane] = v != 0u ? c : -1;
       }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t p = lane; p < npend; p += 64) {  // LogLikelihood.java:41-57, k11k12 and k11 + k21 from tables
+        const int32_t idx = rq[p];
+        const int32_t c = rcol[idx];
+        const int64_t k11 = __double_as_longlong(rscore[idx]);
+        const ColTerms h = cterm[c];
+        const int64_t k12 = rs_a - k11;
+        const int64_t k21 = h.rs - k11;
+        const int64_t k22 = observed + k11 - k12 - k21;
+        rscore[idx] = llr_terms(xlogx(k11 + k12 + (k21 + k22)), x_a, xlogx(k21 + k22), h.x_rs, xlogx(k12 + k22),
+                                xlogx(k11), xlogx(k12), xlogx(k21), xlogx(k22));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < kRsR && i0 + j * 64 < n; j++) {
+        const int32_t c = rcol[j * 64 + lane];
+        const double score = rscore[j * 64 + lane];
+        uint64_t m = __ballot(c >= 0 && (size < topk || score > least));
+        while (m) {
+          const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+          m &= m - 1;
+          const double sc = __shfl(score, l, 64);
+          const int32_t cl = __shfl(c, l, 64);
+          if (size < topk) {
+            heap_add(hv, hs, size, cl, sc);
+          } else if (sc > hs[1]) {
+            heap_update(hv, hs, size, cl, sc);
+          }
+          least = hs[1];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
     out_size[t] = size;
     for (int32_t i = lane; i < size; i += 64) {
@@ -233,33 +308,31 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
 }
 
 // The rescorer's observed total after one window from an empty state: sum of the int views of the
-// row-sum updates (ItemRowRescorer...java:154), and the exact total.
+// row-sum updates (ItemRowRescorer...java:154), and the exact total (out3 zeroed by the caller).
 __global__ void k_observed(const int64_t *__restrict__ rowsum, int32_t M, int64_t *__restrict__ out3) {
-  __shared__ int64_t sr[256], se[256];
+  __shared__ int64_t sr[4], se[4];
   int64_t r = 0, e = 0;
-  for (int32_t a = threadIdx.x; a < M; a += 256) {
+  for (int32_t a = blockIdx.x * 256 + threadIdx.x; a < M; a += gridDim.x * 256) {
     r += int64_t(int32_t(uint32_t(uint64_t(rowsum[a]))));
     e += rowsum[a];
   }
-  sr[threadIdx.x] = r;
-  se[threadIdx.x] = e;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      sr[threadIdx.x] += sr[threadIdx.x + o];
-      se[threadIdx.x] += se[threadIdx.x + o];
-    }
-    __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    r += __shfl_xor(r, o, 64);
+    e += __shfl_xor(e, o, 64);
   }
+  if ((threadIdx.x & 63) == 0) {
+    sr[threadIdx.x >> 6] = r;
+    se[threadIdx.x >> 6] = e;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    out3[0] = sr[0];
-    out3[1] = se[0];
-    out3[2] = M;
+    atomicAdd(reinterpret_cast<unsigned long long *>(out3), (unsigned long long)(sr[0] + sr[1] + sr[2] + sr[3]));
+    atomicAdd(reinterpret_cast<unsigned long long *>(out3 + 1), (unsigned long long)(se[0] + se[1] + se[2] + se[3]));
+    if (blockIdx.x == 0) out3[2] = M;
   }
 }
 
 }  // namespace
-
 namespace {
 __global__ void k_llr(int64_t n, const int64_t *__restrict__ k, double *__restrict__ out) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -339,13 +412,17 @@ Status launch_touched(hipStream_t s, int32_t M, const int32_t *row_nnz, int32_t 
 int rescore_waves_per_block(int32_t topk) { return topk <= 1024 ? 4 : 1; }
 
 size_t rescore_lds_bytes(int32_t topk) {
-  return size_t(rescore_waves_per_block(topk)) * size_t(topk + 1) * (sizeof(double) + sizeof(int32_t));
+  const size_t w = size_t(rescore_waves_per_block(topk));
+  const size_t heaps = sizeof(double) * (w * size_t(topk + 1) + (w * size_t(topk + 1) + 1) / 2);
+  return heaps + w * kRsR * 64 * (sizeof(double) * 2);  // + per-wave score / column / queue rings
 }
 
 template <class Rows>
 Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_rows_dev, int64_t max_rows, Rows src,
-                           const int64_t *grs, const int64_t *obs, bool exact, int32_t topk, int32_t *out_size,
-                           int32_t *out_val, double *out_score) {
+                           int32_t M, const int64_t *grs, const int64_t *obs, bool exact, int32_t topk,
+                           DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score) {
+  COOC_TRY(terms.reserve(sizeof(ColTerms) * size_t(std::max(M, 1))));
+  k_col_terms<<<blocks_for(M, 256), 256, 0, s>>>(M, grs, obs, exact ? 1 : 0, terms.as<ColTerms>());
   const int waves = rescore_waves_per_block(topk);
   const size_t lds = rescore_lds_bytes(topk);
   if (lds > 160 * 1024 - 256) return Status{1, "topk too large for the LDS heaps"};
@@ -357,32 +434,33 @@ Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   const int64_t want = (max_rows + waves - 1) / waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
-  k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, obs, exact ? 1 : 0, topk, out_size,
-                                                 out_val, out_score);
+  k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), obs, exact ? 1 : 0, topk,
+                                                 out_size, out_val, out_score);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }
 
 Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
-                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
+                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, DevBuf &terms, int32_t *out_size,
                       int32_t *out_val, double *out_score) {
   // scal: [0] touched rows, [2] rescorer observed, [3] exact observed
-  return launch_rescore_rows(s, touched, scal, max_rows, DenseRows{G, M}, grs, scal + 2, exact, topk, out_size,
-                             out_val, out_score);
+  return launch_rescore_rows(s, touched, scal, max_rows, DenseRows{G, M}, M, grs, scal + 2, exact, topk, terms,
+                             out_size, out_val, out_score);
 }
 
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                             const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
-                            bool exact, int32_t topk, int64_t *obs3, int32_t *out_size, int32_t *out_val,
-                            double *out_score) {
-  k_observed<<<1, 256, 0, s>>>(rowsum, M, obs3);
+                            bool exact, int32_t topk, int64_t *obs3, DevBuf &terms, int32_t *out_size,
+                            int32_t *out_val, double *out_score) {
+  COOC_HIP_TRY(hipMemsetAsync(obs3, 0, sizeof(int64_t) * 2, s));
+  k_observed<<<std::min<unsigned>(blocks_for(M, 256), 1024), 256, 0, s>>>(rowsum, M, obs3);
   COOC_HIP_TRY(hipGetLastError());
   // obs3: [0] rescorer observed, [1] exact, [2] n_rows (= M)
   if (dense)
-    return launch_rescore_rows(s, nullptr, obs3 + 2, M, DenseRows{dense, M}, rowsum, obs3, exact, topk, out_size,
-                               out_val, out_score);
-  return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, rowsum, obs3, exact,
-                             topk, out_size, out_val, out_score);
+    return launch_rescore_rows(s, nullptr, obs3 + 2, M, DenseRows{dense, M}, M, rowsum, obs3, exact, topk, terms,
+                               out_size, out_val, out_score);
+  return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, M, rowsum, obs3, exact,
+                             topk, terms, out_size, out_val, out_score);
 }
 
 }  // namespace cooc

@@ -23,14 +23,15 @@ Status launch_touched(hipStream_t s, int32_t M, const int32_t *row_nnz, int32_t 
                       DevBuf &tmp);
 size_t rescore_lds_bytes(int32_t topk);
 Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const uint32_t *G,
-                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, int32_t *out_size,
+                      const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, DevBuf &terms, int32_t *out_size,
                       int32_t *out_val, double *out_score);
 
 // LLR top-k of every row of a batch result (padded CSR) -- the C5 stage over one window.
-// obs3 (device int64[3]) receives the rescorer's observed, the exact observed and n_items.
+// obs3 (device int64[3]) receives the rescorer's observed, the exact observed and n_items; terms is
+// scratch for the per-column LLR terms (32 B per item).
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                             const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
                             bool exact, int32_t topk,
-                            int64_t *obs3, int32_t *out_size, int32_t *out_val, double *out_score);
+                            int64_t *obs3, DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score);
 
 }  // namespace cooc

@@ -35,6 +35,34 @@ import torch
 import torch.distributed as dist
 
 
+def balanced_user_ranges(user_ptr, world: int) -> list:
+    """Contiguous user ranges [u0, u1) of about equal pair work sum n_u (n_u - 1), one per rank: the
+    keyBy(user) of FlinkCooccurrences.java:70 balanced on sum n_u^2, since hashing users
+    to ranks is unbalanced under skew.  user_ptr: int64 numpy array or tensor [U+1]; deterministic, so
+    every rank computes the same split from the same offsets."""
+    import numpy as np
+
+    up = user_ptr.cpu().numpy() if isinstance(user_ptr, torch.Tensor) else np.asarray(user_ptr, np.int64)
+    n = np.diff(up).astype(np.int64)
+    cum = np.cumsum(n * (n - 1))
+    total = int(cum[-1]) if len(cum) else 0
+    cuts = [0]
+    for r in range(1, world):
+        # first user whose prefix reaches r/world of the work (ties: ranges stay non-decreasing)
+        cuts.append(max(cuts[-1], int(np.searchsorted(cum, total * r / world, side="left")) + 1 if total else 0))
+    cuts.append(len(n))
+    cuts = [min(c, len(n)) for c in cuts]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def shard_users(user_ptr, items, world: int, rank: int):
+    """This rank's users of a whole log (CSR) under balanced_user_ranges: (user_ptr, items, u0) with
+    user_ptr rebased to 0."""
+    u0, u1 = balanced_user_ranges(user_ptr, world)[rank]
+    s, e = int(user_ptr[u0]), int(user_ptr[u1])
+    return user_ptr[u0:u1 + 1] - s, items[s:e], u0
+
+
 def rows_owned(n_items: int, n_parts: int, part: int) -> int:
     return (n_items - part + n_parts - 1) // n_parts if part < n_items else 0
 

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""One-GPU estimate of a rank's compute in the N-GPU C3 run (bench.py --gpus N: sharding.count_owned).
+
+At N GPUs every rank all-gathers the whole log's histories and counts the rows it owns over all of
+them (cooc_count_device_owned).  Here the whole shard-invariant C3 log of N x 1.25e6 users is built on
+one GPU (the state after the all-gather), the owner map is the same snake_owner of the global item
+frequencies, and rank `part`'s counting step is timed (HIP events on its stream).  The exchange itself
+(RCCL all-gather over xGMI) is not measured here.  Prints one JSON line."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--parts", default="0", help="comma-separated ranks to time")
+    ap.add_argument("--steps", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+
+    import __graft_entry__
+
+    pkg = __graft_entry__.load_package()
+    from flink_cooccurrence_amd import datagen, sharding
+
+    dev = torch.device("cuda", 0)
+    U8 = datagen.C3_USERS // 8
+    ups, its = [], []
+    base = 0
+    for r in range(args.world):
+        up, it = datagen.c3_users(r * U8, (r + 1) * U8, device=dev)
+        ups.append(up[:-1] + base)
+        its.append(it)
+        base += int(up[-1].item())
+        del up
+    up = torch.cat(ups + [torch.tensor([base], dtype=torch.int64, device=dev)])
+    it = torch.cat(its)
+    del ups, its
+    M = datagen.C3_ITEMS
+    N = int(it.numel())
+    freq = torch.bincount(it.to(torch.int64), minlength=M)[:M].to(torch.int64)
+    owner = sharding.snake_owner(freq, args.world)
+    core = pkg.CooccurrenceCore(n_items=M, device=0)
+    core.set_kernel_timing(True)
+    out = {"config": f"C3 rank compute at N={args.world}: all {args.world * U8} users ({N} interactions) after the "
+                     f"all-gather, rows owned by snake_owner(freq, {args.world})", "parts": {}}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    P_all = 0
+    for part in [int(x) for x in args.parts.split(",")]:
+        ms, kms = [], []
+        for s in range(args.steps + 1):
+            ev0.record()
+            res = core.count_device_owned(up, it, owner, part, freq, N)
+            ev1.record()
+            ev1.synchronize()
+            if s:
+                ms.append(ev0.elapsed_time(ev1))
+                kms.append(core.last_kernel_ms())
+        P_all += int(res.observed)
+        out["parts"][part] = {"ms": float(np.median(ms)), "k_sp_main_ms": float(np.median(kms)),
+                              "ordered_pairs": int(res.observed), "nnz": int(res.nnz),
+                              "pairs_per_s": int(res.observed) / (float(np.median(ms)) * 1e-3)}
+    out["interactions"] = N
+    print(json.dumps(out), flush=True)
+    core.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -248,3 +248,24 @@ def test_count_sharded_gloo(oracle, pkg, world, mode):
             assert a not in seen
             seen.add(a)
     assert seen == set(range(M))
+
+
+def test_balanced_user_ranges(pkg):
+    """Contiguous user ranges balanced on sum n_u (n_u - 1): they tile the users, and on a
+    skewed log every rank's pair work is within one user's work of the mean."""
+    from flink_cooccurrence_amd import datagen, sharding
+
+    up, it = datagen.c3_users(0, 20_000)
+    n = np.diff(up)
+    w = n * (n - 1)
+    for world in (1, 2, 3, 8):
+        rng = sharding.balanced_user_ranges(up, world)
+        assert rng[0][0] == 0 and rng[-1][1] == len(n)
+        assert all(rng[r][1] == rng[r + 1][0] for r in range(world - 1))
+        work = np.array([w[a:b].sum() for a, b in rng])
+        assert work.sum() == w.sum()
+        assert np.all(np.abs(work - w.sum() / world) <= w.max() + 1)
+        sup, sit, u0 = sharding.shard_users(up, it, world, world - 1)
+        assert u0 == rng[-1][0] and sup[0] == 0 and len(sit) == sup[-1] == up[rng[-1][1]] - up[rng[-1][0]]
+    t = torch.from_numpy(up)
+    assert sharding.balanced_user_ranges(t, 4) == sharding.balanced_user_ranges(up, 4)
