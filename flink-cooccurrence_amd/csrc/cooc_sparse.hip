@@ -118,6 +118,7 @@ struct SpArgs {
   int32_t M, T;
   unsigned long long *prog;   // COOC_SP_TRACE: per-workgroup progress in pinned host memory
   unsigned long long *stats;  // COOC_SP_STATS: per-phase clocks and counts
+  int32_t exp;                // COOC_SP_STATS only: experiment selector (COOC_SP_EXP; results invalid when set)
   int64_t n_contrib, n_users, n_groups;
   uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
   int64_t scr_cap;          // 0: gather mode off
@@ -625,6 +626,12 @@ struct WalkOp {
 __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStatic &S_, const WalkOp &op,
                                       const uint4 &v) {
   if (v.x == kSink) return;  // (the first id of a group is never a pad)
+#ifdef COOC_SP_STATS
+  if (A.exp == 1 && op.mode == 1) {  // timing experiment: hash chunks load their groups but insert nothing
+    if (v.y == 0xFFFFFFFEu) S_.flag = 1u;
+    return;
+  }
+#endif
   if (op.mode == 2) {
     const uint32_t t = v.x >> kTShift;
     if (t == 0) {
@@ -1569,6 +1576,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 24 * 8);
     hipMemsetAsync(d_stats, 0, 24 * 8, s);
     A.stats = d_stats;
+    A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
     if (n_work > 0) {

@@ -274,3 +274,26 @@ def test_c5_topk_owned_parts_vs_whole(pkg, torch_cuda):
             n = int(w_sz[a])
             assert np.array_equal(v[a, :n], w_v[a, :n]) and np.array_equal(sc[a, :n], w_sc[a, :n], equal_nan=True), f"row {a}"
         core.close()
+
+
+def test_underestimated_row_table_overflow_retries(pkg, torch_cuda):
+    """A row whose partners are far more diverse than the global item frequencies predict: the planner
+    sizes its hash chunk from the estimate, the LDS table overflows, and the chunk is redone with a 4x
+    table (then as dense tiles).  Rows must still be exact."""
+    torch = torch_cuda
+    rng = np.random.default_rng(21)
+    M = 300_000
+    lists = [rng.integers(8192, 8202, 10) for _ in range(10_000)]          # global mass on 10 columns
+    for _ in range(3):                                                      # row 5: ~7,500 distinct partners
+        lists.append(np.concatenate([[5], rng.choice(np.arange(20_000, M), 2500, replace=False), [7, 7]]))
+    up = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+    it = np.concatenate(lists).astype(np.int32)
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        torch.cuda.current_stream().synchronize()
+        lens = np.diff(up)
+        assert res.observed == int(np.sum(lens * (lens - 1)))
+        rows = _Rows(res, M)
+        assert int(rows.rowsum.sum()) == res.observed
+        _check_rows(rows, _Brute(up, it, M), [5, 7, 8192, 8195, 8201] + list(np.unique(it[it >= 20_000])[:20]))
