@@ -184,7 +184,7 @@ def main():
             if world == 1:
                 core.topk_batch_device(args.topk, tk_sizes, tk_vals, tk_scores)
             else:
-                sharding.topk_owned(core, args.topk)
+                sharding.topk_owned(core, r, args.topk)
             ev1.record()
             ev1.synchronize()
             topk_ms.append(ev0.elapsed_time(ev1))

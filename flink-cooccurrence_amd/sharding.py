@@ -251,13 +251,14 @@ class TopkResult:
     rowsum: torch.Tensor    # int64 [n_items]: the all-reduced row sums the scores used
 
 
-def topk_owned(core, topk: int, group=None, exact_scores: bool = False, stream=None) -> TopkResult:
+def topk_owned(core, owned: OwnedResult, topk: int, group=None, exact_scores: bool = False,
+               stream=None) -> TopkResult:
     """C5 after count_owned: the rows' LLR top-k on their owner (ItemRowRescorer...java:195-241).
     The owned results' row sums are all-reduced first -- the reference broadcasts its row-sum stream to
     every rescorer (FlinkCooccurrences.java:163) -- so that k21 = rowSum(b) - k11 and the observed total
     are the whole log's; each rank then scores only the rows it owns."""
     M = core.n_items
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = owned.owner.device
     rowsum = torch.empty(M, dtype=torch.int64, device=dev)
     core.copy_rowsum_device(rowsum, stream)
     dist.all_reduce(rowsum, group=group)

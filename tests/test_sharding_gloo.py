@@ -158,7 +158,27 @@ class FakeOwnedCore:
                 r.rows[a] = v
         r.observed = int(sum(rowsums[a] for a in r.rows))
         r.nnz = int(sum(np.count_nonzero(v) for v in r.rows.values()))
+        self.rows = r.rows
+        self.rowsum = np.where(own == part, rowsums, 0).astype(np.int64)
         return r
+
+    def copy_rowsum_device(self, out, stream=None):
+        out.copy_(torch.from_numpy(self.rowsum))
+
+    def topk_batch_device(self, topk, sizes, values, scores, rowsum_global=None, exact_scores=False, stream=None):
+        """cooc_topk_batch_device over the owned rows, scored with the given (all-reduced) row sums."""
+        from oracle import oracle
+        from tests._helpers import oracle_row_topk
+
+        rs32 = rowsum_global.numpy().astype(np.int32).astype(np.int64)
+        sizes.zero_()
+        for a, v in self.rows.items():
+            nz = np.flatnonzero(v)
+            heap = oracle_row_topk(oracle, nz, v[nz].astype(np.int16), rs32, a, topk, int(rs32.sum()))
+            sizes[a] = len(heap)
+            for i, (b, sc) in enumerate(heap):
+                values[a, i] = b
+                scores[a, i] = sc
 
 
 def _worker(rank, world, port, up_all, it_all, M, out_q, mode="partials"):
@@ -178,18 +198,24 @@ def _worker(rank, world, port, up_all, it_all, M, out_q, mode="partials"):
     lo, hi = rank * U // world, (rank + 1) * U // world
     up = up_all[lo:hi + 1] - up_all[lo]
     it = it_all[up_all[lo]:up_all[hi]]
-    if mode == "owned":
-        res = sharding.count_owned(FakeOwnedCore(M), torch.from_numpy(up), torch.from_numpy(it))
+    if mode in ("owned", "owned_topk"):
+        core = FakeOwnedCore(M)
+        res = sharding.count_owned(core, torch.from_numpy(up), torch.from_numpy(it))
         rows, rs = res.owned.rows, None
         owner = res.owner.numpy()
         assert all(owner[a] == rank for a in rows)
+        if mode == "owned_topk":  # C5: heaps of the owned rows against the all-reduced row sums
+            tk = sharding.topk_owned(core, res, 5)
+            rs = tk.rowsum.numpy().tolist()
+            rows = {a: (int(tk.sizes[a]), tk.values[a].tolist(), tk.scores[a].tolist()) for a in rows}
+            assert all(int(tk.sizes[a]) == 0 for a in range(M) if owner[a] != rank)
     elif mode == "records":
         res = sharding.count_records(FakeRecordsCore(M), torch.from_numpy(up), torch.from_numpy(it))
         rows, rs = res.owned, None
     else:
         res = sharding.count_sharded(FakeCore(M), torch.from_numpy(up), torch.from_numpy(it))
         rows, rs = res.merged, res.rowsum.numpy().tolist()
-    out_q.put((rank, {a: v.tolist() for a, v in rows.items()}, rs, res.observed))
+    out_q.put((rank, {a: (v.tolist() if hasattr(v, "tolist") else v) for a, v in rows.items()}, rs, res.observed))
     dist.destroy_process_group()
 
 
@@ -215,7 +241,7 @@ def test_snake_owner_balances_zipf(pkg):
 
 
 @pytest.mark.parametrize("world,mode", [(2, "partials"), (3, "partials"), (2, "records"), (3, "records"), (2, "owned"),
-                                        (3, "owned")])
+                                        (3, "owned"), (2, "owned_topk"), (3, "owned_topk")])
 def test_count_sharded_gloo(oracle, pkg, world, mode):
     rng = np.random.default_rng(3)
     U, M = 90, 23
@@ -237,13 +263,22 @@ def test_count_sharded_gloo(oracle, pkg, world, mode):
     for a in range(M):
         C[a, cols[rp[a]:rp[a + 1]]] = data[rp[a]:rp[a + 1]]
     seen = set()
+    rs32 = rowsums.astype(np.int32).astype(np.int64)
     for rank, rows, rs, obs in outs:
         assert obs == observed
         if rs is not None:
             assert np.array_equal(np.array(rs), rowsums)
         for a, v in rows.items():
-            if mode != "owned":
+            if mode not in ("owned", "owned_topk"):
                 assert a % world == rank
+            if mode == "owned_topk":  # the whole log's heap of row a
+                from tests._helpers import assert_row_topk, oracle_row_topk
+
+                nz = np.flatnonzero(C[a])
+                want = oracle_row_topk(oracle, nz, C[a][nz].astype(np.int16), rs32, a, 5, int(rs32.sum()))
+                assert_row_topk(v[0], v[1], v[2], want, where=f"row {a}")
+                seen.add(a)
+                continue
             assert np.array_equal(np.array(v), C[a])
             assert a not in seen
             seen.add(a)
