@@ -578,7 +578,7 @@ struct SpStatic {
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
 #ifdef COOC_SP_STATS
-  unsigned long long st[24];
+  unsigned long long st[28];
 #endif
 };
 
@@ -594,7 +594,13 @@ __device__ inline void sp_hash_insert4(uint32_t *keys, uint32_t *cnts, const uin
   uint32_t h[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) h[i] = (k[i] - 1u) * 0x9E3779B1u >> hshift;
+#ifdef COOC_SP_STATS
+  if (threadIdx.x == 0) S_.st[24] += (k[0] != 0u) + (k[1] != 0u) + (k[2] != 0u) + (k[3] != 0u);
+#endif
   for (int p = 0; p < kMaxProbe; p++) {
+#ifdef COOC_SP_STATS
+    if (threadIdx.x == 0) S_.st[25] += 1;
+#endif
     uint32_t cur[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) cur[i] = k[i] ? atomicCAS(keys + h[i], 0u, k[i]) : 0u;
@@ -1010,7 +1016,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   }
   const int64_t n_work = A.tot->n_chunks;
 #ifdef COOC_SP_STATS
-  if (threadIdx.x < 24) S_.st[threadIdx.x] = 0ull;
+  if (threadIdx.x < 28) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -1185,7 +1191,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
 #ifdef COOC_SP_STATS
   if (tid == 0) {
     S_.st[13] = STAT_CLOCK() - t_start;
-    for (int k = 0; k < 24; k++) atomicAdd(A.stats + k, S_.st[k]);
+    for (int k = 0; k < 28; k++) atomicAdd(A.stats + k, S_.st[k]);
   }
 #endif
 }
@@ -1573,8 +1579,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
 #ifdef COOC_SP_STATS
     static unsigned long long *d_stats = nullptr;
-    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 24 * 8);
-    hipMemsetAsync(d_stats, 0, 24 * 8, s);
+    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 28 * 8);
+    hipMemsetAsync(d_stats, 0, 28 * 8, s);
     A.stats = d_stats;
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
@@ -1621,7 +1627,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipStreamSynchronize(s));
 #ifdef COOC_SP_STATS
     {
-      unsigned long long h[24];
+      unsigned long long h[28];
       hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
       const double g = double(grid);
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
@@ -1633,6 +1639,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       fprintf(stderr, "[sp stats] hash detail per WG (us): walk scan %.0f walk loop %.0f | groups %.3g batches %llu | "
               "compact rank %.0f reserve %.0f write %.0f | entries %.3g\n", h[16] / 100.0 / g, h[17] / 100.0 / g,
               double(h[18]), h[19], h[20] / 100.0 / g, h[21] / 100.0 / g, h[22] / 100.0 / g, double(h[23]));
+      fprintf(stderr, "[sp stats] thread-0 sample: ids inserted %llu, probe rounds %llu (%.2f per group call)\n", h[24], h[25],
+              h[24] ? double(h[25]) / double(h[24]) * 4.0 : 0.0);
       fprintf(stderr, "[sp stats] attempt %d: cap %lld slab %lld grid %lld err %lld scr_cap %lld n_gather %lld\n", attempt,
               (long long)cap, (long long)slab, (long long)grid, (long long)err, (long long)A.scr_cap, (long long)n_gather);
     }
