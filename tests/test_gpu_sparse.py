@@ -297,3 +297,23 @@ def test_underestimated_row_table_overflow_retries(pkg, torch_cuda):
         rows = _Rows(res, M)
         assert int(rows.rowsum.sum()) == res.observed
         _check_rows(rows, _Brute(up, it, M), [5, 7, 8192, 8195, 8201] + list(np.unique(it[it >= 20_000])[:20]))
+
+
+@pytest.mark.parametrize("lens", [[], [0, 0, 0], [1, 0, 1, 1], [0, 2, 0, 3, 1, 0]])
+def test_large_universe_empty_and_ragged(pkg, oracle, torch_cuda, lens):
+    """Edge cases on the large-universe path (n_items = 100,000): no users, only empty users, users with
+    single items (no pairs), ragged lists with repeats; against the closed form."""
+    torch = torch_cuda
+    M = 100_000
+    rng = np.random.default_rng(len(lens))
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    it = rng.choice([0, 1, 7, 40_000, M - 1], int(up[-1])).astype(np.int32)
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        torch.cuda.current_stream().synchronize()
+        got = core.copy_batch(res.nnz, res.observed)
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert got.observed == observed and res.nnz == len(cols)
+    assert np.array_equal(got.row_ptr, rp) and np.array_equal(got.cols, cols)
+    assert np.array_equal(got.cnt.astype(np.int64), data) and np.array_equal(got.rowsum, rowsums)
