@@ -249,18 +249,25 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      int32_t run = 0;
-      for (int32_t t = 0; t <= T; t++) {
-        const int32_t x = c[t];
-        c[t] = run;
-        run += (x + 3) & ~3;
+    if (T < 64) {  // exclusive prefix of the padded tile counts: one wave scan (lane t = tile t)
+      const uint32_t x = lane <= T ? uint32_t((c[lane] + 3) & ~3) : 0u;
+      const uint32_t inc = wave_incl_scan(x);
+      if (lane <= T) tb[j * (T + 1) + lane] = int32_t(inc - x);
+      if (lane == T) plen[j] = int64_t(inc);  // (tile T is empty: inc = the padded length)
+    } else {
+      if (lane == 0) {
+        int32_t run = 0;
+        for (int32_t t = 0; t <= T; t++) {
+          const int32_t x = c[t];
+          c[t] = run;
+          run += (x + 3) & ~3;
+        }
+        plen[j] = run;
       }
-      plen[j] = run;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
