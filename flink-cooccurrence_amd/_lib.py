@@ -81,6 +81,7 @@ _SIGS = {
     "cooc_last_error": (ctypes.c_char_p, [vp]),
     "cooc_count_device": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
                                          ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_item_counts": (ctypes.c_int, [vp, vp, ctypes.c_int64, vp, vp]),
     "cooc_count_device_owned": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.c_int32, vp,
                                                ctypes.c_int64, vp, ctypes.POINTER(CoocDeviceResult)]),
     "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),

@@ -138,6 +138,17 @@ class CooccurrenceCore:
                                             _stream_arg(stream, items), ctypes.byref(res)), self._h)
         return res
 
+    def item_counts(self, items, out=None, stream=None):
+        """Item frequencies of a device int32 tensor -> int64 device tensor [n_items] (cooc_item_counts)."""
+        import torch
+
+        if out is None:
+            out = torch.empty(self.n_items, dtype=torch.int64, device=items.device)
+        check(_lib.load().cooc_item_counts(self._h, ctypes.c_void_p(items.data_ptr()) if items.numel() else None,
+                                           int(items.numel()), ctypes.c_void_p(out.data_ptr()),
+                                           _stream_arg(stream, out)), self._h)
+        return out
+
     def count_device_owned(self, user_ptr, items, owner, part: int, item_counts, n_total: int,
                            stream=None) -> CoocDeviceResult:
         """Rows a with owner[a] == part over every user given (multi-GPU, n_items >= 40,320).

@@ -124,6 +124,17 @@ int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_use
   });
 }
 
+int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactions, int64_t *d_counts, void *hip_stream) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !d_counts || n_interactions < 0 || (n_interactions > 0 && !d_items))
+      return fail(ctx, COOC_ERR_ARG, "bad item_counts arguments");
+    (void)hipSetDevice(ctx->device);
+    Status s = cooc::launch_item_counts(static_cast<hipStream_t>(hip_stream), d_items, n_interactions, ctx->cfg.n_items,
+                                        d_counts);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
 int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
                     cooc_window_info *info) {
   return guarded(ctx, [&]() -> int {

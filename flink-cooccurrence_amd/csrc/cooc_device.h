@@ -225,4 +225,8 @@ class Counter {
 Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr, int64_t *off, int32_t *len,
                          int32_t *old);
 
+// Item frequencies of a device item array into counts int64[M] (zeroed first); ids outside [0, M) are
+// not counted.
+Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_t M, int64_t *counts);
+
 }  // namespace cooc

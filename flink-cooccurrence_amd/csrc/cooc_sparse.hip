@@ -1337,6 +1337,43 @@ int bits_for(int64_t v) {
 
 }  // namespace
 
+namespace {
+// Item frequencies of a log (the multi-GPU owner map and the planner's column estimate): ids below
+// kHistLds are counted in LDS (Zipf ranks: the hot ids; no contended global atomics), the rest with
+// global 64-bit atomics (each such bin is cold); the LDS bins are flushed once per workgroup.
+constexpr int kHistLds = 16384;
+__global__ __launch_bounds__(1024) void k_item_counts(const int32_t *__restrict__ items, int64_t n, int32_t M,
+                                                      unsigned long long *__restrict__ counts) {
+  __shared__ uint32_t h[kHistLds];
+  for (int i = threadIdx.x; i < kHistLds; i += 1024) h[i] = 0u;
+  __syncthreads();
+  const uint32_t hot = uint32_t(min(M, kHistLds));
+  const int64_t stride = int64_t(gridDim.x) * 1024;
+  for (int64_t i = int64_t(blockIdx.x) * 1024 + threadIdx.x; i < n; i += stride) {
+    const uint32_t it = uint32_t(items[i]);
+    if (it < hot) atomicAdd(&h[it], 1u);
+    else if (it < uint32_t(M)) atomicAdd(counts + it, 1ull);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < hot; b += 1024)
+    if (h[b]) atomicAdd(counts + b, (unsigned long long)h[b]);
+}
+}  // namespace
+
+Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_t M, int64_t *counts) {
+  COOC_HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int64_t) * size_t(M), s));
+  if (n > 0) {
+    int dev = 0, n_cu = 256;
+    COOC_HIP_TRY(hipGetDevice(&dev));
+    COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t want = (n + 1023) / 1024;
+    k_item_counts<<<unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 2))), 1024, 0, s>>>(
+        items, n, M, reinterpret_cast<unsigned long long *>(counts));
+    COOC_HIP_TRY(hipGetLastError());
+  }
+  return Status::Ok();
+}
+
 Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
                            CountResult *out, KernelTimer *timer, const int32_t *owner, int32_t part,
                            const int64_t *freq, int64_t n_freq) {

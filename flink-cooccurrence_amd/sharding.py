@@ -213,7 +213,7 @@ def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     M = core.n_items
     n_users, n = int(user_ptr.numel()) - 1, int(items.numel())
     # global item frequencies (the planner's column estimate) and the row owner map
-    counts = torch.bincount(items.to(torch.int64), minlength=M)[:M].to(torch.int64)
+    counts = core.item_counts(items, stream=stream)  # (torch.bincount: global atomics on Zipf-hot bins)
     dist.all_reduce(counts, group=group)
     owner = snake_owner(counts, world)
     # all-gather the histories: lengths and items, padded to the largest rank's share

@@ -156,6 +156,12 @@ COOC_API int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64
                                      int64_t n_interactions, const int32_t *d_owner, int32_t part,
                                      const int64_t *d_item_counts, int64_t n_total, void *hip_stream,
                                      cooc_device_result *out);
+/* Item frequencies of a device item array (d_items int32[n_interactions]) into d_counts int64[n_items]
+ * (device, overwritten) on hip_stream: the local part of the global frequencies that
+ * cooc_count_device_owned's caller all-reduces (owner map, planner estimate).  Ids outside
+ * [0, n_items) are not counted. */
+COOC_API int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactions, int64_t *d_counts,
+                              void *hip_stream);
 /* Same from host buffers; afterwards cooc_copy_batch copies the packed CSR out. */
 COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
                     cooc_window_info *info);

@@ -45,13 +45,20 @@ def main():
     del ups, its
     M = datagen.C3_ITEMS
     N = int(it.numel())
-    freq = torch.bincount(it.to(torch.int64), minlength=M)[:M].to(torch.int64)
-    owner = sharding.snake_owner(freq, args.world)
     core = pkg.CooccurrenceCore(n_items=M, device=0)
     core.set_kernel_timing(True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the rank's own share of the frequencies (cooc_item_counts on 1/world of the log), timed
+    core.item_counts(it[: N // args.world])
+    ev0.record()
+    core.item_counts(it[: N // args.world])
+    ev1.record()
+    ev1.synchronize()
+    freq_ms = ev0.elapsed_time(ev1)
+    freq = core.item_counts(it)
+    owner = sharding.snake_owner(freq, args.world)
     out = {"config": f"C3 rank compute at N={args.world}: all {args.world * U8} users ({N} interactions) after the "
                      f"all-gather, rows owned by snake_owner(freq, {args.world})", "parts": {}}
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     P_all = 0
     for part in [int(x) for x in args.parts.split(",")]:
         ms, kms = [], []
@@ -68,6 +75,7 @@ def main():
                               "ordered_pairs": int(res.observed), "nnz": int(res.nnz),
                               "pairs_per_s": int(res.observed) / (float(np.median(ms)) * 1e-3)}
     out["interactions"] = N
+    out["item_counts_ms_per_rank_share"] = freq_ms
     print(json.dumps(out), flush=True)
     core.close()
 

@@ -317,3 +317,20 @@ def test_large_universe_empty_and_ragged(pkg, oracle, torch_cuda, lens):
     assert got.observed == observed and res.nnz == len(cols)
     assert np.array_equal(got.row_ptr, rp) and np.array_equal(got.cols, cols)
     assert np.array_equal(got.cnt.astype(np.int64), data) and np.array_equal(got.rowsum, rowsums)
+
+
+def test_item_counts_vs_bincount(pkg, torch_cuda):
+    """cooc_item_counts (the multi-GPU owner map's frequencies): equal to numpy's bincount on a C3-shaped
+    log, LDS-counted hot ids and globally counted tail ids alike; ids outside [0, n_items) not counted."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.c3_users(0, 20_000)
+    M = datagen.C3_ITEMS
+    it_bad = np.concatenate([it, np.array([-1, M, M + 5], np.int32)])
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        got = core.item_counts(torch.from_numpy(it_bad).to(dev)).cpu().numpy()
+        empty = core.item_counts(torch.zeros(0, dtype=torch.int32, device=dev)).cpu().numpy()
+    assert np.array_equal(got, np.bincount(it, minlength=M))
+    assert not empty.any()

@@ -136,6 +136,9 @@ class FakeOwnedCore:
     def __init__(self, n_items):
         self.n_items = n_items
 
+    def item_counts(self, items, out=None, stream=None):
+        return torch.from_numpy(np.bincount(items.numpy(), minlength=self.n_items).astype(np.int64))
+
     def count_device_owned(self, user_ptr, items, owner, part, item_counts, n_total, stream=None):
         from oracle import oracle
 
