@@ -1465,8 +1465,9 @@ Status Counter::init(int32_t n_items) {
   int dev = 0;
   COOC_HIP_TRY(hipGetDevice(&dev));
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu_, hipDeviceAttributeMultiprocessorCount, dev));
-  if (n_items >= kBatchMaxItems) return Status::Ok();  // run_sparse (cooc_sparse.hip) sets its own attributes
-  // general planner (streaming windows): one LDS row over all items plus the descriptor batch
+  // run_sparse (cooc_sparse.hip) sets its own attributes; the general planner (streaming windows) keeps
+  // one LDS row over all items plus the descriptor batch, up to kMaxGeneralItems
+  if (n_items > kMaxGeneralItems) return Status::Ok();
   const size_t lds = size_t(n_items) * 4;
   db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
   if (db_ < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
@@ -1564,7 +1565,7 @@ Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, Kern
   dense_mode_ = false;
   last_rows_ = M;
   const int64_t n = au.n_contrib;
-  if (M > kMaxGeneralItems)
+  if (M > kMaxGeneralItems || db_ < 32)
     return Status{1, "n_items > " + std::to_string(kMaxGeneralItems) +
                          " is supported for one-window batches (cooc_count_device), not for streaming windows"};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};

@@ -63,6 +63,8 @@ class StreamState {
   DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
   // global state
   bool global_ready_ = false;
+  bool sparse_global_ = false;  // n_items >= 40,320: sorted row slabs (gs_) instead of the dense matrix
+  GlobalSparse gs_;
   DevBuf d_global_, d_grs_, d_touched_, d_scan_tmp_, d_scal_, d_topk_val_, d_topk_score_, d_topk_size_, d_llr_terms_;
   // last window
   bool have_window_ = false;

@@ -229,4 +229,17 @@ Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr
 // not counted.
 Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_t M, int64_t *counts);
 
+// Sparse global rows of the streaming state (n_items >= 40,320; the rescorer's itemRows,
+// ItemRowRescorer...java:35,171-177): row a = len[a] (column, count) entries in ascending column order
+// at base[a] of the arena (col, cnt); kernels in cooc_stream.hip.
+struct GlobalSparse {
+  DevBuf base, len, col, cnt, flag, newpre, nbase, bump_dev;
+  int64_t cap = 0, bump = 0, live = 0;
+  void release() {
+    DevBuf *all[] = {&base, &len, &col, &cnt, &flag, &newpre, &nbase, &bump_dev};
+    for (DevBuf *b : all) b->release();
+    cap = bump = live = 0;
+  }
+};
+
 }  // namespace cooc

@@ -62,7 +62,9 @@ void StreamState::release() {
                    &d_grs_,       &d_touched_,     &d_scan_tmp_,    &d_scal_,      &d_topk_val_,
                    &d_topk_score_, &d_topk_size_, &d_llr_terms_};
   for (DevBuf *b : all) b->release();
+  gs_.release();
   global_ready_ = false;
+  sparse_global_ = false;
 }
 
 // Keyed user state lookup (userHistoryState, NonSampled...java:129-132): a dense table for
@@ -154,6 +156,20 @@ Status StreamState::grow_arena(cooc_ctx &ctx, int64_t need) {
 Status StreamState::ensure_global(cooc_ctx &ctx) {
   if (global_ready_) return Status::Ok();
   const int64_t M = ctx.cfg.n_items;
+  if (!ctx.counter.batch_ok()) {  // large universe: sorted row slabs, grown per window
+    sparse_global_ = true;
+    COOC_TRY(gs_.base.reserve(sizeof(int64_t) * size_t(M)));
+    COOC_TRY(gs_.len.reserve(sizeof(int32_t) * size_t(M)));
+    COOC_TRY(d_grs_.reserve(sizeof(int64_t) * M));
+    COOC_TRY(d_scal_.reserve(sizeof(int64_t) * 8));
+    COOC_HIP_TRY(hipMemsetAsync(gs_.base.p, 0, sizeof(int64_t) * size_t(M), ctx.stream));
+    COOC_HIP_TRY(hipMemsetAsync(gs_.len.p, 0, sizeof(int32_t) * size_t(M), ctx.stream));
+    COOC_HIP_TRY(hipMemsetAsync(d_grs_.p, 0, sizeof(int64_t) * M, ctx.stream));
+    COOC_HIP_TRY(hipMemsetAsync(d_scal_.p, 0, sizeof(int64_t) * 8, ctx.stream));
+    gs_.cap = gs_.bump = gs_.live = 0;
+    global_ready_ = true;
+    return Status::Ok();
+  }
   const size_t g_bytes = sizeof(uint32_t) * size_t(M) * size_t(M);
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -261,8 +277,19 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
   COOC_TRY(ensure_global(ctx));
   int64_t *scal = d_scal_.as<int64_t>();
-  COOC_TRY(launch_merge_global(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, d_global_.as<uint32_t>(),
-                               d_grs_.as<int64_t>(), scal, observed_window));
+  COOC_TRY(launch_merge_global(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum,
+                               sparse_global_ ? nullptr : d_global_.as<uint32_t>(), d_grs_.as<int64_t>(), scal,
+                               observed_window));
+  if (sparse_global_) {  // the window's delta rows (packed) merged into the row slabs
+    int64_t *drp;
+    int32_t *dcol;
+    uint32_t *dcnt;
+    COOC_TRY(ctx.counter.pack(s, &drp, &dcol, &dcnt));
+    PlanTotals pt;
+    COOC_TRY(ctx.counter.read_totals(&pt));
+    int64_t new_cols = 0;
+    COOC_TRY(launch_gs_merge(s, M, drp, dcol, dcnt, pt.nnz_total, gs_, d_scan_tmp_, &new_cols));
+  }
   COOC_TRY(d_touched_.reserve(sizeof(int32_t) * M));
   COOC_TRY(launch_touched(s, M, r.row_nnz, d_touched_.as<int32_t>(), scal, d_scan_tmp_));
   const int32_t topk = ctx.cfg.topk;
@@ -270,9 +297,14 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
     COOC_TRY(d_topk_size_.reserve(sizeof(int32_t) * M));
     COOC_TRY(d_topk_val_.reserve(sizeof(int32_t) * size_t(M) * topk));
     COOC_TRY(d_topk_score_.reserve(sizeof(double) * size_t(M) * topk));
-    COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
-                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_, d_topk_size_.as<int32_t>(),
-                            d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+    if (sparse_global_)
+      COOC_TRY(launch_rescore_sparse(s, d_touched_.as<int32_t>(), scal, M, gs_, d_grs_.as<int64_t>(),
+                                     (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
+                                     d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+    else
+      COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
+                              (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
+                              d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
   }
   tr.mark("merge_rescore", s);
   int64_t h_scal[8];
@@ -400,6 +432,12 @@ Status StreamState::global_row_nnz(cooc_ctx &ctx, int32_t item, int64_t *nnz) {
   *nnz = 0;
   if (!global_ready_) return Status::Ok();
   COOC_HIP_TRY(hipSetDevice(ctx.device));
+  if (sparse_global_) {
+    int32_t n = 0;
+    COOC_HIP_TRY(hipMemcpy(&n, gs_.len.as<int32_t>() + item, sizeof(int32_t), hipMemcpyDeviceToHost));
+    *nnz = n;
+    return Status::Ok();
+  }
   std::vector<uint32_t> row(M);
   COOC_HIP_TRY(hipMemcpy(row.data(), d_global_.as<uint32_t>() + int64_t(item) * M, sizeof(uint32_t) * M,
                          hipMemcpyDeviceToHost));
@@ -412,6 +450,20 @@ Status StreamState::global_row(cooc_ctx &ctx, int32_t item, int32_t *cols, uint3
   if (item < 0 || item >= M) return Status{COOC_ERR_ARG, "item outside [0, n_items)"};
   if (!global_ready_) return Status::Ok();
   COOC_HIP_TRY(hipSetDevice(ctx.device));
+  if (sparse_global_) {
+    int32_t n = 0;
+    int64_t b = 0;
+    COOC_HIP_TRY(hipMemcpy(&n, gs_.len.as<int32_t>() + item, sizeof(int32_t), hipMemcpyDeviceToHost));
+    COOC_HIP_TRY(hipMemcpy(&b, gs_.base.as<int64_t>() + item, sizeof(int64_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> c(n);
+    if (n && cols) COOC_HIP_TRY(hipMemcpy(cols, gs_.col.as<int32_t>() + b, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    if (n) COOC_HIP_TRY(hipMemcpy(c.data(), gs_.cnt.as<uint32_t>() + b, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    for (int32_t i = 0; i < n; i++) {
+      if (cnt) cnt[i] = c[i];
+      if (cnt16) cnt16[i] = int16_t(uint16_t(c[i]));
+    }
+    return Status::Ok();
+  }
   std::vector<uint32_t> row(M);
   COOC_HIP_TRY(hipMemcpy(row.data(), d_global_.as<uint32_t>() + int64_t(item) * M, sizeof(uint32_t) * M,
                          hipMemcpyDeviceToHost));

@@ -75,8 +75,10 @@ __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *
     const int32_t n = row_nnz[a];
     if (n == 0) continue;
     const int64_t b = row_base[a];
-    uint32_t *g = G + a * int64_t(M);
-    for (int32_t i = lane; i < n; i += 64) g[col[b + i]] += cnt[b + i];  // unique (a, col) per window
+    if (G) {  // dense global rows (sparse ones are merged by k_gs_merge)
+      uint32_t *g = G + a * int64_t(M);
+      for (int32_t i = lane; i < n; i += 64) g[col[b + i]] += cnt[b + i];  // unique (a, col) per window
+    }
     if (lane == 0) {
       const int64_t d = rowsum_delta[a];
       grs[a] += d;
@@ -332,6 +334,115 @@ __global__ void k_observed(const int64_t *__restrict__ rowsum, int32_t M, int64_
   }
 }
 
+// ---- sparse global rows (n_items >= 40,320): the rescorer's itemRows (ItemRowRescorer...java:35,
+// 171-177) as one sorted slab per row, g_len[a] (column, count) entries at g_base[a] of an arena.  A
+// window's packed delta rows (drp, dcol, dcnt; ascending columns) are merged into a new slab per
+// touched row: a delta entry whose column is new takes a slot, one whose column exists adds to it.
+__device__ inline int64_t lower_bound_col(const int32_t *__restrict__ c, int64_t n, int32_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (c[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// flag[e] = 1 when delta entry e's column is not yet in its row (one wave per row)
+__global__ __launch_bounds__(256) void k_gs_flags(int32_t M, const int64_t *__restrict__ drp,
+                                                  const int32_t *__restrict__ dcol, const int64_t *__restrict__ gbase,
+                                                  const int32_t *__restrict__ glen, const int32_t *__restrict__ gcol,
+                                                  int32_t *__restrict__ flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
+    const int64_t d0 = drp[a], d1 = drp[a + 1];
+    if (d0 == d1) continue;
+    const int32_t *old = gcol + gbase[a];
+    const int64_t n_old = glen[a];
+    for (int64_t e = d0 + lane; e < d1; e += 64) {
+      const int64_t p = lower_bound_col(old, n_old, dcol[e]);
+      flag[e] = (p < n_old && old[p] == dcol[e]) ? 0 : 1;
+    }
+  }
+}
+
+// new slab of every touched row: need = old + new columns, bump-allocated; live += new columns
+__global__ void k_gs_alloc(int32_t M, const int64_t *__restrict__ drp, const int64_t *__restrict__ newpre,
+                           const int32_t *__restrict__ glen, int64_t *__restrict__ nbase,
+                           unsigned long long *__restrict__ bump) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  const int64_t d0 = drp[a], d1 = drp[a + 1];
+  if (d0 == d1) {
+    nbase[a] = -1;
+    return;
+  }
+  const int64_t need = int64_t(glen[a]) + (newpre[d1] - newpre[d0]);
+  nbase[a] = int64_t(atomicAdd(bump, (unsigned long long)need));
+}
+
+// the merge: old entries shift right by the new columns before them (and take a matching delta's
+// count), new delta entries go after the old columns below them.  One wave per touched row.
+__global__ __launch_bounds__(256) void k_gs_merge(int32_t M, const int64_t *__restrict__ drp,
+                                                  const int32_t *__restrict__ dcol, const uint32_t *__restrict__ dcnt,
+                                                  const int64_t *__restrict__ newpre, const int32_t *__restrict__ flag,
+                                                  const int64_t *__restrict__ nbase, const int64_t *__restrict__ gbase,
+                                                  const int32_t *__restrict__ glen, int32_t *__restrict__ gcol,
+                                                  uint32_t *__restrict__ gcnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
+    const int64_t nb = nbase[a];
+    if (nb < 0) continue;
+    const int64_t d0 = drp[a], d = drp[a + 1] - d0, ob = gbase[a], n_old = glen[a];
+    for (int64_t i = lane; i < n_old; i += 64) {
+      const int32_t c = gcol[ob + i];
+      const int64_t p = lower_bound_col(dcol + d0, d, c);
+      const uint32_t add = (p < d && dcol[d0 + p] == c) ? dcnt[d0 + p] : 0u;
+      const int64_t pos = nb + i + (newpre[d0 + p] - newpre[d0]);
+      gcol[pos] = c;
+      gcnt[pos] = gcnt[ob + i] + add;
+    }
+    for (int64_t e = lane; e < d; e += 64) {
+      if (!flag[d0 + e]) continue;
+      const int32_t c = dcol[d0 + e];
+      const int64_t pos = nb + (newpre[d0 + e] - newpre[d0]) + lower_bound_col(gcol + ob, n_old, c);
+      gcol[pos] = c;
+      gcnt[pos] = dcnt[d0 + e];
+    }
+  }
+}
+
+__global__ void k_gs_commit(int32_t M, const int64_t *__restrict__ drp, const int64_t *__restrict__ newpre,
+                            const int64_t *__restrict__ nbase, int64_t *__restrict__ gbase, int32_t *__restrict__ glen) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M || nbase[a] < 0) return;
+  glen[a] += int32_t(newpre[drp[a + 1]] - newpre[drp[a]]);
+  gbase[a] = nbase[a];
+}
+
+// compaction: every row's slab to a fresh arena at the prefix of the row lengths (one wave per row)
+__global__ __launch_bounds__(256) void k_gs_compact(int32_t M, const int64_t *__restrict__ newbase,
+                                                    int64_t *__restrict__ gbase, const int32_t *__restrict__ glen,
+                                                    const int32_t *__restrict__ col_in, const uint32_t *__restrict__ cnt_in,
+                                                    int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
+    const int64_t from = gbase[a], to = newbase[a], n = glen[a];
+    for (int64_t i = lane; i < n; i += 64) {
+      col_out[to + i] = col_in[from + i];
+      cnt_out[to + i] = cnt_in[from + i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) gbase[a] = to;
+  }
+}
+
+struct WidenLen {
+  __host__ __device__ int64_t operator()(int32_t v) const { return int64_t(v); }
+};
+
 }  // namespace
 namespace {
 __global__ void k_llr(int64_t n, const int64_t *__restrict__ k, double *__restrict__ out) {
@@ -461,6 +572,87 @@ Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, c
                                out_size, out_val, out_score);
   return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, M, rowsum, obs3, exact,
                              topk, terms, out_size, out_val, out_score);
+}
+
+Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32_t *dcol, const uint32_t *dcnt,
+                       int64_t nnz, GlobalSparse &g, DevBuf &tmp, int64_t *new_cols) {
+  // 1. new-column flags, their exclusive prefix (newpre[nnz] = the window's new columns)
+  COOC_TRY(g.flag.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(nnz, 1))));
+  COOC_TRY(g.newpre.reserve(sizeof(int64_t) * size_t(nnz + 1)));
+  COOC_TRY(g.nbase.reserve(sizeof(int64_t) * size_t(M)));
+  int32_t *flag = g.flag.as<int32_t>();
+  int64_t *newpre = g.newpre.as<int64_t>();
+  COOC_HIP_TRY(hipMemsetAsync(newpre, 0, sizeof(int64_t), s));
+  const unsigned gw = std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192);
+  if (nnz > 0) {
+    k_gs_flags<<<gw, 256, 0, s>>>(M, drp, dcol, g.base.as<int64_t>(), g.len.as<int32_t>(), g.col.as<int32_t>(), flag);
+    hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> f64(flag, WidenLen{});
+    size_t b = 0;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, f64, newpre + 1, int(nnz), s));
+    COOC_TRY(tmp.reserve(b));
+    b = tmp.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, f64, newpre + 1, int(nnz), s));
+  }
+  COOC_HIP_TRY(hipMemcpyAsync(new_cols, newpre + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  // 2. room for the touched rows' new slabs (at most live + nnz entries): compact, then grow
+  const int64_t need = g.live + nnz;
+  if (g.bump + need > g.cap) {
+    COOC_TRY(compact_global(s, M, g, tmp, std::max<int64_t>(2 * (g.live + need), int64_t(1) << 12)));
+  }
+  COOC_TRY(g.bump_dev.reserve(sizeof(uint64_t)));
+  COOC_HIP_TRY(hipMemcpyAsync(g.bump_dev.p, &g.bump, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  k_gs_alloc<<<blocks_for(M, 256), 256, 0, s>>>(M, drp, newpre, g.len.as<int32_t>(), g.nbase.as<int64_t>(),
+                                                g.bump_dev.as<unsigned long long>());
+  k_gs_merge<<<gw, 256, 0, s>>>(M, drp, dcol, dcnt, newpre, flag, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
+                                g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>());
+  k_gs_commit<<<blocks_for(M, 256), 256, 0, s>>>(M, drp, newpre, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
+                                                 g.len.as<int32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  int64_t bump = 0;
+  COOC_HIP_TRY(hipMemcpyAsync(&bump, g.bump_dev.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  g.bump = bump;
+  g.live += *new_cols;
+  return Status::Ok();
+}
+
+Status compact_global(hipStream_t s, int32_t M, GlobalSparse &g, DevBuf &tmp, int64_t new_cap) {
+  DevBuf col2, cnt2;
+  COOC_TRY(col2.reserve(sizeof(int32_t) * size_t(new_cap)));
+  COOC_TRY(cnt2.reserve(sizeof(uint32_t) * size_t(new_cap)));
+  COOC_TRY(g.nbase.reserve(sizeof(int64_t) * size_t(M + 1)));
+  int64_t *nb = g.nbase.as<int64_t>();
+  COOC_HIP_TRY(hipMemsetAsync(nb, 0, sizeof(int64_t), s));
+  hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> l64(g.len.as<int32_t>(), WidenLen{});
+  size_t b = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, l64, nb + 1, M, s));
+  COOC_TRY(tmp.reserve(b));
+  b = tmp.cap;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, l64, nb + 1, M, s));
+  if (g.col.p)
+    k_gs_compact<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
+        M, nb, g.base.as<int64_t>(), g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>(), col2.as<int32_t>(),
+        cnt2.as<uint32_t>());
+  COOC_HIP_TRY(hipGetLastError());
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  g.col.release();
+  g.cnt.release();
+  g.col = col2;
+  g.cnt = cnt2;
+  col2.p = cnt2.p = nullptr;
+  col2.cap = cnt2.cap = 0;
+  g.cap = new_cap;
+  g.bump = g.live;
+  return Status::Ok();
+}
+
+Status launch_rescore_sparse(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const GlobalSparse &g,
+                             const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, DevBuf &terms,
+                             int32_t *out_size, int32_t *out_val, double *out_score) {
+  return launch_rescore_rows(s, touched, scal, max_rows,
+                             CsrRows{g.base.as<int64_t>(), g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>()},
+                             M, grs, scal + 2, exact, topk, terms, out_size, out_val, out_score);
 }
 
 }  // namespace cooc

@@ -34,4 +34,18 @@ Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, c
                             bool exact, int32_t topk,
                             int64_t *obs3, DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score);
 
+// Sparse global rows (n_items >= 40,320; the rescorer's itemRows, ItemRowRescorer...java:35,171-177):
+// row a = len[a] (column, count) entries in ascending column order at base[a] of the arena (col, cnt).
+// Rows move to a new bump-allocated slab when a window touches them; live = entries of all rows;
+// the arena is compacted (rows re-laid in order) when a window would not fit behind the bump
+// (struct GlobalSparse, cooc_device.h).
+// Merge a window's packed delta rows (drp int64[M+1], dcol, dcnt; nnz entries) into the rows;
+// *new_cols = the window's new (row, column) keys.  Synchronises the stream.
+Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32_t *dcol, const uint32_t *dcnt,
+                       int64_t nnz, GlobalSparse &g, DevBuf &tmp, int64_t *new_cols);
+Status compact_global(hipStream_t s, int32_t M, GlobalSparse &g, DevBuf &tmp, int64_t new_cap);
+Status launch_rescore_sparse(hipStream_t s, const int32_t *touched, const int64_t *scal, int32_t M, const GlobalSparse &g,
+                             const int64_t *grs, bool exact, int32_t topk, int32_t max_rows, DevBuf &terms,
+                             int32_t *out_size, int32_t *out_val, double *out_score);
+
 }  // namespace cooc

@@ -334,3 +334,44 @@ def test_item_counts_vs_bincount(pkg, torch_cuda):
         empty = core.item_counts(torch.zeros(0, dtype=torch.int32, device=dev)).cpu().numpy()
     assert np.array_equal(got, np.bincount(it, minlength=M))
     assert not empty.any()
+
+
+def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda):
+    """Streaming windows at n_items = 40,500 (above the batch planner's range, where the global rows are
+    sorted row slabs merged per window -- the rescorer's itemRows -- instead of the dense matrix; the
+    window counter for streaming covers n_items <= 40,704).  Every window's delta rows, row sums,
+    observed and top-k against the oracle's rescorer, then the final global rows, row sums and
+    accumulators; the slabs move and the arena compacts along the way."""
+    from flink_cooccurrence_amd import datagen
+    from tests._helpers import INT64_MAX, assert_windows_equal
+
+    M = 40_500
+    d = datagen.config_c1(seed=5, U=1500, M=M, mean=20.0)
+    users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
+    op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=M, top_k=10)
+    ref = oracle.OracleStream(1000, topk=10)
+    got, want = [], []
+    for lo in range(0, len(users), 5000):
+        sl = slice(lo, lo + 5000)
+        op.process_elements(users[sl], items[sl], ts[sl])
+        ref.process_elements(users[sl], items[sl], ts[sl])
+        wm = int(ts[sl][-1]) - 1
+        got += op.process_watermark(wm)
+        want += ref.process_watermark(wm)
+    got += op.process_watermark(INT64_MAX)
+    want += ref.process_watermark(INT64_MAX)
+    assert len(got) == len(want) > 5
+    for g, w in zip(got, want):
+        assert_windows_equal(g, w)
+    assert op.accumulators() == ref.counters()
+    rows, rp, cols, exact, v16 = ref.global_rows()
+    for r in list(range(0, len(rows), max(1, len(rows) // 200))) + [len(rows) - 1]:
+        a = int(rows[r])
+        c, n, n16 = op.core.global_row(a)
+        assert np.array_equal(c, cols[rp[r]:rp[r + 1]]), f"global row {a}"
+        assert np.array_equal(n.astype(np.int64), exact[rp[r]:rp[r + 1]])
+        assert np.array_equal(n16, v16[rp[r]:rp[r + 1]])
+    gi, gv32, gex = ref.global_rowsums()
+    ex, v32 = op.core.global_rowsums()
+    assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
+    op.close()
