@@ -42,6 +42,10 @@ class StreamState {
   Status ensure_global(cooc_ctx &ctx);
   int32_t slot_for(int32_t user_id);
   Status grow_arena(cooc_ctx &ctx, int64_t need);
+  // n_items > Counter::kMaxGeneralItems: the window's delta rows as C(full histories) - C(histories
+  // before the window) of its users, both counted by the large-universe planner
+  Status count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int32_t> &act_old,
+                            int64_t n_full, CountResult *r);
 
   // host metadata of the per-user histories
   std::unordered_map<int32_t, int32_t> slot_of_;  // user ids outside [0, 2^26)
@@ -61,6 +65,8 @@ class StreamState {
   std::vector<std::vector<int32_t>> staged_items_;  // reused across windows
   // device uploads of one window
   DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
+  // large-universe windows: contiguous full / old histories, the full histories' packed result
+  DevBuf d_lw_items_, d_lw_oldptr_, d_lw_rp_, d_lw_col_, d_lw_cnt_, d_lw_rs_;
   // global state
   bool global_ready_ = false;
   bool sparse_global_ = false;  // n_items >= 40,320: sorted row slabs (gs_) instead of the dense matrix

@@ -176,6 +176,13 @@ class Counter {
 
   // Pack the result of the last run into contiguous CSR (device), for copy-out.
   Status pack(hipStream_t stream, int64_t **row_ptr, int32_t **col, uint32_t **cnt);
+  // Streaming windows over large universes: the last result becomes the difference of two packed
+  // CSRs over all rows (f: the window's users' full histories, o: their histories before the window;
+  // o's keys are a subset of f's), entries whose difference is 0 dropped, rowsum = f_rs - o_rs (o_rs
+  // may be this counter's own last_rowsum()).  Afterwards pack / last_* / read_totals see it.
+  Status adopt_difference(hipStream_t stream, const int64_t *f_rp, const int32_t *f_col, const uint32_t *f_cnt,
+                          const int64_t *f_rs, const int64_t *o_rp, const int32_t *o_col, const uint32_t *o_cnt,
+                          const int64_t *o_rs, CountResult *out);
 
   // Copy the device totals of the last run (the stream must have drained).
   Status read_totals(PlanTotals *t);

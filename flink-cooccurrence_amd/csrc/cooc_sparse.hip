@@ -1338,6 +1338,61 @@ int bits_for(int64_t v) {
 }  // namespace
 
 namespace {
+__device__ inline int64_t lb_i32(const int32_t *__restrict__ c, int64_t n, int32_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (c[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Row a of f minus row a of o (one wave per row): pass 0 counts the non-zero differences into nnz[a],
+// pass 1 writes them at base[a] in column order.
+template <int PASS>
+__global__ __launch_bounds__(256) void k_diff_rows(int32_t M, const int64_t *__restrict__ f_rp,
+                                                   const int32_t *__restrict__ f_col, const uint32_t *__restrict__ f_cnt,
+                                                   const int64_t *__restrict__ o_rp, const int32_t *__restrict__ o_col,
+                                                   const uint32_t *__restrict__ o_cnt, int32_t *__restrict__ nnz,
+                                                   const int64_t *__restrict__ base, int32_t *__restrict__ col_out,
+                                                   uint32_t *__restrict__ cnt_out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
+    const int64_t f0 = f_rp[a], nf = f_rp[a + 1] - f0, o0 = o_rp[a], no = o_rp[a + 1] - o0;
+    int64_t k = PASS ? base[a] : 0;
+    for (int64_t i0 = 0; i0 < nf; i0 += 64) {
+      uint32_t d = 0u;
+      int32_t c = 0;
+      if (i0 + lane < nf) {
+        c = f_col[f0 + i0 + lane];
+        const int64_t p = lb_i32(o_col + o0, no, c);
+        d = f_cnt[f0 + i0 + lane] - ((p < no && o_col[o0 + p] == c) ? o_cnt[o0 + p] : 0u);
+      }
+      const uint64_t m = __ballot(d != 0u);
+      if (PASS && d) {
+        const int64_t pos = k + __popcll(m & lt);
+        col_out[pos] = c;
+        cnt_out[pos] = d;
+      }
+      k += __popcll(m);
+    }
+    if (!PASS && lane == 0) nnz[a] = int32_t(k);
+  }
+}
+
+__global__ void k_diff_rowsum(int32_t M, const int64_t *__restrict__ f_rs, const int64_t *__restrict__ o_rs,
+                              int64_t *__restrict__ out) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < M) out[a] = f_rs[a] - o_rs[a];
+}
+
+__global__ void k_set_nnz_total(PlanTotals *__restrict__ tot, const int64_t *__restrict__ base, int32_t M) {
+  tot->nnz_total = base[M];
+  tot->err = 0;
+}
+
 // Item frequencies of a log (the multi-GPU owner map and the planner's column estimate): ids below
 // kHistLds are counted in LDS (Zipf ranks: the hot ids; no contended global atomics), the rest with
 // global 64-bit atomics (each such bin is cold); the LDS bins are flushed once per workgroup.
@@ -1371,6 +1426,48 @@ Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_
         items, n, M, reinterpret_cast<unsigned long long *>(counts));
     COOC_HIP_TRY(hipGetLastError());
   }
+  return Status::Ok();
+}
+
+Status Counter::adopt_difference(hipStream_t s, const int64_t *f_rp, const int32_t *f_col, const uint32_t *f_cnt,
+                                 const int64_t *f_rs, const int64_t *o_rp, const int32_t *o_col, const uint32_t *o_cnt,
+                                 const int64_t *o_rs, CountResult *out) {
+  const int32_t M = M_;
+  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
+  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
+  const unsigned gw = unsigned(std::min<int64_t>((int64_t(M) * 64 + 255) / 256, 8192));
+  k_diff_rows<0><<<gw, 256, 0, s>>>(M, f_rp, f_col, f_cnt, o_rp, o_col, o_cnt, row_nnz_.as<int32_t>(), nullptr, nullptr,
+                                    nullptr);
+  int64_t *base = row_base_.as<int64_t>();
+  hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> n64(row_nnz_.as<int32_t>(), WidenCount{});
+  size_t b = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, n64, base + 1, M, s));
+  COOC_TRY(sort_tmp_.reserve(b));
+  b = sort_tmp_.cap;
+  COOC_HIP_TRY(hipMemsetAsync(base, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, n64, base + 1, M, s));
+  int64_t nnz = 0;
+  COOC_HIP_TRY(hipMemcpyAsync(&nnz, base + M, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(nnz + 1)));
+  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * size_t(nnz + 1)));
+  k_diff_rows<1><<<gw, 256, 0, s>>>(M, f_rp, f_col, f_cnt, o_rp, o_col, o_cnt, nullptr, base, col_.as<int32_t>(),
+                                    cnt_.as<uint32_t>());
+  k_diff_rowsum<<<nblocks(M, 256), 256, 0, s>>>(M, f_rs, o_rs, rowsum_.as<int64_t>());
+  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
+  k_set_nnz_total<<<1, 1, 0, s>>>(tot_.as<PlanTotals>(), base, M);
+  COOC_HIP_TRY(hipGetLastError());
+  dense_mode_ = false;
+  vec_ = false;
+  last_rows_ = M;
+  out->row_base = base;
+  out->row_nnz = row_nnz_.as<int32_t>();
+  out->col = col_.as<int32_t>();
+  out->cnt = cnt_.as<uint32_t>();
+  out->dense = nullptr;
+  out->rowsum = rowsum_.as<int64_t>();
+  out->nnz = nnz;
   return Status::Ok();
 }
 

@@ -39,6 +39,19 @@ __global__ void k_append(int64_t n, const int64_t *__restrict__ new_ptr, const i
   }
 }
 
+// Contiguous copies of arena slabs: list j (len[j] ids at off[j]) to out[dst[j] ..).  One wave per list.
+__global__ void k_gather_lists(int64_t n, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                               const int64_t *__restrict__ dst, const int32_t *__restrict__ arena,
+                               int32_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = wave; j < n; j += n_waves) {
+    const int64_t s = off[j], d = dst[j];
+    for (int64_t i = lane; i < len[j]; i += 64) out[d + i] = arena[s + i];
+  }
+}
+
 // kMax cap (UserInteractionCounter...java:168): capped length min(n_u, cut) of every user at
 // lens[u + 1]; an inclusive scan of lens[1..U] gives the capped offsets.
 __global__ void k_cut_lens(int64_t U, const int64_t *__restrict__ up, int32_t cut, int64_t *__restrict__ lens) {
@@ -460,6 +473,13 @@ Status launch_llr(hipStream_t s, int64_t n, const int64_t *d_k4, double *d_out) 
 
 Status launch_relocate(hipStream_t s, int64_t n, const int64_t *reloc, int32_t *arena) {
   if (n > 0) k_relocate<<<std::min<unsigned>(blocks_for(n * 64, 256), 4096), 256, 0, s>>>(n, reloc, arena);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_gather_lists(hipStream_t s, int64_t n, const int64_t *off, const int32_t *len, const int64_t *dst,
+                           const int32_t *arena, int32_t *out) {
+  if (n > 0) k_gather_lists<<<std::min<unsigned>(blocks_for(n * 64, 256), 4096), 256, 0, s>>>(n, off, len, dst, arena, out);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }

@@ -8,6 +8,9 @@ namespace cooc {
 Status launch_relocate(hipStream_t s, int64_t n, const int64_t *reloc, int32_t *arena);
 // LogLikelihood.logLikelihoodRatio (the rescorer's device scoring function) over n (k11, k12, k21, k22)
 Status launch_llr(hipStream_t s, int64_t n, const int64_t *d_k4, double *d_out);
+// list j of len[j] ids at arena offset off[j] -> out[dst[j] ..) (contiguous CSR of arena slabs)
+Status launch_gather_lists(hipStream_t s, int64_t n, const int64_t *off, const int32_t *len, const int64_t *dst,
+                           const int32_t *arena, int32_t *out);
 Status launch_append(hipStream_t s, int64_t n, const int64_t *new_ptr, const int64_t *new_dst, const int32_t *items,
                      int32_t *arena);
 // scal: [0] touched rows, [1] sum of the window's int row-sum deltas, [2] rescorer observed

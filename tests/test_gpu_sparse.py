@@ -336,16 +336,17 @@ def test_item_counts_vs_bincount(pkg, torch_cuda):
     assert not empty.any()
 
 
-def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda):
-    """Streaming windows at n_items = 40,500 (above the batch planner's range, where the global rows are
-    sorted row slabs merged per window -- the rescorer's itemRows -- instead of the dense matrix; the
-    window counter for streaming covers n_items <= 40,704).  Every window's delta rows, row sums,
-    observed and top-k against the oracle's rescorer, then the final global rows, row sums and
-    accumulators; the slabs move and the arena compacts along the way."""
+@pytest.mark.parametrize("M", [40_500, 1_000_000])
+def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda, M):
+    """Streaming windows above the batch planner's range: the global rows are sorted row slabs merged
+    per window (the rescorer's itemRows) instead of the dense matrix.  40,500 items: windows counted by
+    the general planner; 1e6 items (C3's universe): a window's delta rows are C(full histories) -
+    C(histories before the window) of its users, both from the large-universe planner.  Every window's
+    delta rows, row sums, observed and top-k against the oracle's rescorer, then the final global rows,
+    row sums and accumulators; the slabs move and the arena compacts along the way."""
     from flink_cooccurrence_amd import datagen
     from tests._helpers import INT64_MAX, assert_windows_equal
 
-    M = 40_500
     d = datagen.config_c1(seed=5, U=1500, M=M, mean=20.0)
     users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
     op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(1, "SECONDS", n_items=M, top_k=10)
