@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--copy", action="store_true", help="also copy every window's outputs to the host")
     ap.add_argument("--users", type=int, default=138_493)
     ap.add_argument("--planner", default="auto", choices=["auto", "general"])
+    ap.add_argument("--c3-shard", type=int, default=0,
+                    help="stream users [0, 1e7 / this) of the C3 log (1e6 items) instead of the C2 log")
     args = ap.parse_args()
 
     import torch
@@ -37,7 +39,12 @@ def main():
     from flink_cooccurrence_amd import datagen
 
     t0 = time.time()
-    if args.users == 138_493:
+    if args.c3_shard:
+        up3, it3 = datagen.c3_users(0, datagen.C3_USERS // args.c3_shard)
+        rng = np.random.Generator(np.random.PCG64(4))
+        d = {"user_ptr": up3, "items": it3, "n_items": datagen.C3_ITEMS,
+             "ts": datagen.spread_over_windows(rng, up3, args.windows, 1000)}
+    elif args.users == 138_493:
         d = datagen.config_c4(n_windows=args.windows)
     else:  # reduced log (same shape) for quick runs
         N = int(20_000_263 * args.users / 138_493)
@@ -80,7 +87,9 @@ def main():
     assert total_pairs == datagen.ordered_pairs(up), "sum of window pairs != pairs of the whole log"
     lat_ms = np.array(lat) * 1e3
     out = {
-        "config": "C4 streaming: C2-shaped log over %d x 1 s windows (seed 4)%s" % (
+        "config": "C4 streaming: %s over %d x 1 s windows (seed 4)%s" % (
+            f"users [0, 1e7/{args.c3_shard}) of the C3 log (1e6 items; sparse global rows, windows as "
+            "C(full) - C(old))" if args.c3_shard else "C2-shaped log",
             args.windows, f", LLR top-{args.topk} rescoring of touched rows" if args.topk else ""),
         "users": int(len(lens)), "interactions": int(up[-1]), "n_items": M,
         "windows": args.windows, "topk": args.topk, "planner": args.planner,

@@ -1,3 +1,3 @@
 set -u
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|^E " gpurun_out/pytest_gpu.log | head -20; exit $rc; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
+timeout -k 10 600 python -u scripts/bench_stream.py --c3-shard 640 --windows 100 --topk 10 > gpurun_out/stream_c3.json 2> gpurun_out/stream_c3.err || { tail -5 gpurun_out/stream_c3.err; exit 1; }
+cat gpurun_out/stream_c3.json
