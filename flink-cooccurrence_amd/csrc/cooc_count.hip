@@ -1117,7 +1117,8 @@ constexpr int kSlabRows = 4;
 // step's atomics.  Pad ids (= M) land on the sink counter acc[M], so the inner loop has no
 // compares: per partner id one shift/mask and one ds_add_u32.  Latency hiding across chunks: the
 // next chunk is dequeued when a chunk starts, and its descriptor and first descriptor batch are
-// loaded before this chunk's compaction.
+// loaded before this chunk's compaction (chunks are queued heaviest first, so a reservation made at
+// the start of a long chunk holds back only lighter ones at the tail).
 // Output: DENSE = the counts as a dense row-major uint32 [M x M] matrix in HBM (row a written whole
 // from LDS with coalesced stores; split rows add their chunks into the zeroed dense row with
 // global atomics); otherwise the column-order sparse compaction into a bump-allocated padded CSR.
