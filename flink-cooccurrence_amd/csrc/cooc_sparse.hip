@@ -432,11 +432,14 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
       } else {
         float cur = 0.f;
         int n_in = 0, cs = -1;
-        // a hash chunk's table: the smallest power of two >= 2 E[distinct] + 64 slots (kHashMin..kHashMax)
+        // a hash chunk's table: the smallest power of two >= SLACK * E[distinct] + 64 slots (kHashMin..kHashMax)
         auto close = [&]() {
           if (cs < 0) return;
           uint64_t code = 0;
-          for (int H = kHashMin; H < kHashMax && float(H) < 2.f * cur + 64.f; H <<= 1) code++;
+#ifndef COOC_SP_HASH_SLACK
+#define COOC_SP_HASH_SLACK 3.f  // table >= 3x the estimated distinct count: 1% faster than 2x at C3 (A/B)
+#endif
+          for (int H = kHashMin; H < kHashMax && float(H) < COOC_SP_HASH_SLACK * cur + 64.f; H <<= 1) code++;
           if (cs < 32) h0 |= code << (2 * cs); else h1 |= code << (2 * (cs - 32));
           cs = -1;
         };

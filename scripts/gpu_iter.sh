@@ -1,3 +1,6 @@
 set -u
-timeout -k 10 600 python -u scripts/bench_stream.py --c3-shard 640 --windows 100 --topk 10 > gpurun_out/stream_c3.json 2> gpurun_out/stream_c3.err || { tail -5 gpurun_out/stream_c3.err; exit 1; }
-cat gpurun_out/stream_c3.json
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -3 gpurun_out/t.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err || { tail -5 gpurun_out/bench_c3.err; exit 1; }
+cat gpurun_out/bench_c3.json
