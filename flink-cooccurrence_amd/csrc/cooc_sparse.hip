@@ -81,8 +81,14 @@ constexpr int64_t kSplitWork = int64_t(1) << 23;       // rows above this pair w
 constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
 constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups)
 constexpr int kGatherMinChunks = 3;                    // rows with this many chunks gather their tails
-constexpr float kHashFill = 0.5f * kHashMax;           // expected distinct keys per hash chunk
-constexpr float kDensePairs = 2.f * kTW;                 // a tile with more expected pairs is dense
+#ifndef COOC_SP_FILL
+#define COOC_SP_FILL 0.375f  // A/B at C3: 0.375 with 4x tables 4.5% faster than 0.5 with 3x
+#endif
+#ifndef COOC_SP_DENSE
+#define COOC_SP_DENSE 2.f
+#endif
+constexpr float kHashFill = COOC_SP_FILL * kHashMax;     // expected distinct keys per hash chunk
+constexpr float kDensePairs = COOC_SP_DENSE * kTW;       // a tile with more expected pairs is dense
 constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + kSpThreads;
 
 // One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
           if (cs < 0) return;
           uint64_t code = 0;
 #ifndef COOC_SP_HASH_SLACK
-#define COOC_SP_HASH_SLACK 3.f  // table >= 3x the estimated distinct count: 1% faster than 2x at C3 (A/B)
+#define COOC_SP_HASH_SLACK 4.f  // table >= 4x the estimated distinct count (A/B)
 #endif
           for (int H = kHashMin; H < kHashMax && float(H) < COOC_SP_HASH_SLACK * cur + 64.f; H <<= 1) code++;
           if (cs < 32) h0 |= code << (2 * cs); else h1 |= code << (2 * (cs - 32));
