@@ -77,10 +77,16 @@ constexpr int kSpDb = 512;                             // contribution descripto
 constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
 constexpr int kSpU = 4;                                // partner loads in flight per lane
 constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
-constexpr int64_t kSplitWork = int64_t(1) << 23;       // rows above this pair work are split
+#ifndef COOC_SP_SPLIT_LG
+#define COOC_SP_SPLIT_LG 23
+#endif
+#ifndef COOC_SP_GATHER_MIN
+#define COOC_SP_GATHER_MIN 3
+#endif
+constexpr int64_t kSplitWork = int64_t(1) << COOC_SP_SPLIT_LG;  // rows above this pair work are split
 constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
 constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups)
-constexpr int kGatherMinChunks = 3;                    // rows with this many chunks gather their tails
+constexpr int kGatherMinChunks = COOC_SP_GATHER_MIN;   // rows with this many chunks gather their tails
 #ifndef COOC_SP_FILL
 #define COOC_SP_FILL 0.375f  // A/B at C3: 0.375 with 4x tables 4.5% faster than 0.5 with 3x
 #endif
