@@ -1,8 +1,6 @@
 set -u
-D=flink-cooccurrence_amd/csrc
-cp $D/libcooc_hip.so $D/libcooc_hip_base.so
-for V in base g2 g5 s22 s24 base; do
-  cp $D/libcooc_hip_$V.so $D/libcooc_hip.so
-  timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/ab_$V.json'));print('$V',d['ms_per_step'],d['roofline']['kernel_ms'])"
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -3 gpurun_out/t.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err || { tail -5 gpurun_out/bench_c3.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/bench_c3.json'));print(d['value'],d['ms_per_step'],d['roofline']['kernel_ms'],d['roofline']['frac'],d['cpu_baseline']['value'])"
