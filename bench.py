@@ -48,7 +48,7 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
     the first users of the same log: a calibration run sizes a sample of ~target_s seconds."""
     from oracle import oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, nproc, avail = cpu_threads()
     n = np.diff(user_ptr)
     cum = np.cumsum(n * (n - 1))
 
@@ -68,9 +68,34 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
     dt = time.perf_counter() - t0
     assert pairs == P
     return {"value": P / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cpus_available": avail,
             "label": "CPU restatement, not the JVM reference (BASELINE.md)",
             "sample": f"first {nu} users of {what} ({len(it)} interactions, {P} ordered pairs, {nnz} keys), "
                       f"one window, {threads} threads, {dt:.1f} s"}
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may run on (nproc), capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box sets it to its CPU share per GPU).
+    Returns (threads, nproc, CPUs in the affinity mask)."""
+    nproc = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(avail, cap) if cap > 0 else avail), nproc, avail
+
+
+def source_digest() -> str:
+    """sha256 over the library's kernel and host sources (csrc/*.hip, *.cpp, *.h, Makefile): ties a
+    profiles/pmc_<kernel>.json to the code it was collected on (scripts/pmc_summary.py records it)."""
+    import hashlib
+
+    d = os.path.join(ROOT, "flink-cooccurrence_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile":
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def limiter(pmc: dict, traffic, k_ms: float):
@@ -159,6 +184,10 @@ def main():
                     "Zipf(0.9) without replacement, one window, numpy PCG64 seed 2 (+rank)")
     U, N = int(up.numel()) - 1, int(it.numel())
     torch.cuda.synchronize()
+    digest = source_digest()
+    pmc_stale = bool(pmc) and pmc.get("source_digest") != digest
+    if pmc_stale:  # counters of other code: not reported as this kernel's
+        pmc = {"kernel": pmc.get("kernel"), "stale_source_digest": pmc.get("source_digest")}
 
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
     core.set_kernel_timing(True)
@@ -206,6 +235,16 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # exactness checks of the last step's result on the device (outside the timed region): the in-kernel
+    # row-sum check already failed the step if any row's counts missed W_a - c_a; here the whole output
+    # is re-read: sum of all counts == sum of the row sums == the ordered pairs of the generator's
+    # lengths, every row's columns strictly ascending, no zero count (cooc_verify_batch)
+    chk = None
+    if world == 1 or large:  # (the C2 records exchange's owner result is checked inside cooc_shard_count)
+        chk = core.verify_batch()
+        P_res = res.observed if world == 1 else res.local_observed
+        assert chk["rows_bad_sum"] == 0 and chk["rows_bad_entries"] == 0, f"verify_batch: {chk}"
+        assert chk["sum_counts"] == chk["sum_rowsums"] == P_res, f"verify_batch: {chk}, pairs {P_res}"
     if world == 1:
         assert res.observed == P_local, "pair count mismatch"
         D, P_counted, N_seen, U_seen = int(res.nnz), int(res.observed), N, U
@@ -268,6 +307,9 @@ def main():
             "l2_hit_rate": pmc.get("l2_hit_rate"),
             "wave_wait_frac": pmc.get("wave_wait_frac"),
             "limiter": limiter(pmc, traffic, k_ms),
+            "pmc_source_digest": pmc.get("source_digest") or pmc.get("stale_source_digest"),
+            "source_digest": digest,
+            "pmc_stale": pmc_stale,
             "kernel_ms": k_ms,
             "algorithmic_bytes_per_launch": b_alg,
             "units_per_launch": {"ordered_pairs": P_counted, "interactions": N_seen, "users": U_seen,
@@ -278,6 +320,7 @@ def main():
                     "profiles/pmc_<kernel>.json) when collected; see DESIGN.md §4",
         },
         "cpu_baseline": None,
+        "checks": {"device_verify": chk, "in_kernel_row_sum_check": "every step (err bit -> exception)"},
     }
     if args.config == "c5":
         out["config"]["topk"] = args.topk

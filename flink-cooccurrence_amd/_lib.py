@@ -24,6 +24,7 @@ COOC_FLAG_EXACT_SCORES = 1
 COOC_FLAG_OUTPUT_CSR = 2
 COOC_FLAG_OUTPUT_DENSE = 4
 COOC_FLAG_GENERAL_PLANNER = 8
+COOC_VERIFY_SYMMETRY = 1
 
 i16p = ctypes.POINTER(ctypes.c_int16)
 i32p = ctypes.POINTER(ctypes.c_int32)
@@ -94,6 +95,7 @@ _SIGS = {
     "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),
     "cooc_finish_window": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_window_delta": (ctypes.c_int, [vp, i32p, i64p, i32p, u32p, i16p]),
+    "cooc_copy_window_delta_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, i32p, u32p, i16p]),
     "cooc_copy_window_rowsums": (ctypes.c_int, [vp, i32p, i64p, i32p]),
     "cooc_copy_window_topk": (ctypes.c_int, [vp, i32p, i32p, i32p, f64p]),
     "cooc_global_rowsums": (ctypes.c_int, [vp, i64p, i32p]),
@@ -117,6 +119,7 @@ _SIGS = {
     "cooc_records_decode": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i64p, i32p, i16p, i64p, i32p]),
     "cooc_parse_interactions": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p,
                                                i64p, i64p]),
+    "cooc_verify_batch": (ctypes.c_int, [vp, ctypes.c_int32, vp, i64p, vp]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }

@@ -54,6 +54,18 @@ def _stream_arg(stream, tensor):
     return None
 
 
+def _current_stream():
+    """torch's current stream on the current device when torch has a GPU, else the null stream."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    except ImportError:
+        pass
+    return None
+
+
 @dataclass
 class BatchResult:
     """C of one window over empty histories, as a packed CSR over all n_items rows."""
@@ -281,6 +293,21 @@ class CooccurrenceCore:
             ctypes.c_void_p(arena_all.data_ptr()), int(arena_stride),
             _stream_arg(stream, recv_row_counts), ctypes.byref(res)), self._h)
         return res
+
+    def verify_batch(self, symmetry: bool = False, row_checksum=None, stream=None) -> dict:
+        """cooc_verify_batch over the last count_device result: the reference's DEVELOPMENT_MODE row-sum
+        check (ItemRowRescorer...java:183-193) and the CSR contract's checks, on the device.
+        row_checksum: optional uint64-sized device tensor [n_items] (torch.int64 is fine) that receives
+        every row's fingerprint (sum of splitmix64(col << 32 ^ count); oracle.row_checksums restates it)."""
+        out = np.zeros(8, np.int64)
+        flags = _lib.COOC_VERIFY_SYMMETRY if symmetry else 0
+        cs = ctypes.c_void_p(row_checksum.data_ptr()) if row_checksum is not None else None
+        check(_lib.load().cooc_verify_batch(self._h, flags, cs, _p(out, i64p),
+                                            _stream_arg(stream, row_checksum) if row_checksum is not None else
+                                            _current_stream()), self._h)
+        return {"sum_counts": int(out[0]), "sum_rowsums": int(out[1]), "entries": int(out[2]),
+                "rows_bad_sum": int(out[3]), "rows_bad_entries": int(out[4]),
+                "asymmetric_entries": None if out[5] < 0 else int(out[5])}
 
     def set_kernel_timing(self, enable: bool = True) -> None:
         check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)

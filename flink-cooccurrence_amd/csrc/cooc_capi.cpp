@@ -228,6 +228,15 @@ int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32
   });
 }
 
+int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *cols, uint32_t *cnt,
+                                 int16_t *cnt16) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    Status s = ctx->stream_state.copy_delta_range(*ctx, row_begin, row_end, cols, cnt, cnt16);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
 int cooc_copy_window_rowsums(cooc_ctx *ctx, int32_t *items, int64_t *delta, int32_t *delta32) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;
@@ -418,6 +427,15 @@ int cooc_shard_count(cooc_ctx *ctx, int32_t n_parts, int32_t part, const int32_t
     out->rowsum = r.rowsum;
     out->dense = r.dense;
     return COOC_OK;
+  });
+}
+
+int cooc_verify_batch(cooc_ctx *ctx, int32_t flags, uint64_t *d_row_checksum, int64_t *out8, void *hip_stream) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !out8) return COOC_ERR_ARG;
+    if (flags & ~COOC_VERIFY_SYMMETRY) return fail(ctx, COOC_ERR_ARG, "unknown cooc_verify_batch flags");
+    Status s = ctx->verify_batch(flags, d_row_checksum, out8, static_cast<hipStream_t>(hip_stream));
+    return s.ok() ? COOC_OK : fail(ctx, s);
   });
 }
 

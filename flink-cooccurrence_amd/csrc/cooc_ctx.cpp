@@ -47,7 +47,7 @@ cooc_ctx::~cooc_ctx() {
   sharder.release();
   counter.release();
   cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
-                          &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms};
+                          &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms, &b_verify};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
   if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);
@@ -60,6 +60,7 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   have_batch = false;
   batch_topk = 0;
   COOC_TRY(apply_user_cut(n_users, &d_user_ptr, &d_items, &n_interactions, s));
+  batch_owned = false;
   cooc::CountResult r;
   if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
@@ -85,7 +86,9 @@ Status cooc_ctx::count_device_owned(int64_t n_users, const int64_t *d_user_ptr, 
   cooc::CountResult r;
   COOC_TRY(counter.run_sparse(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr,
                               d_owner, part, d_item_counts, n_total));
-  return finish_batch(r, s, out);
+  COOC_TRY(finish_batch(r, s, out));
+  batch_owned = true;
+  return Status::Ok();
 }
 
 Status cooc_ctx::apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, const int32_t **d_items,
@@ -128,14 +131,18 @@ cooc::Status cooc_ctx::count_general(int64_t n_users, const int64_t *d_user_ptr,
 cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, cooc_device_result *out) {
   COOC_HIP_TRY(hipStreamSynchronize(s));
   // totals (nnz, overflow flag) are written by the last kernels of the run
-  int64_t nnz = 0, err = 0;
+  int64_t nnz = 0, err = 0, bad_row = -1;
   {
     cooc::PlanTotals h;
     COOC_TRY(counter.read_totals(&h));
     nnz = h.nnz_total;
     err = h.err;
+    bad_row = counter.sparse() ? h.bad_row : -1;
   }
-  if (err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  if (err & 2)
+    return Status{COOC_ERR_OVERFLOW, "row-sum check failed" + (bad_row >= 0 ? " (row " + std::to_string(bad_row) + ")" : std::string()) +
+                                         ": a row's exact counts do not add up to its closed-form row sum (a co-occurrence "
+                                         "count exceeded uint32)"};
   if (err & 4) return Status{COOC_ERR_OOM, "the sparse output region is exhausted"};
   out->n_items = cfg.n_items;
   out->nnz = nnz;
@@ -284,5 +291,24 @@ Status cooc_ctx::copy_topk_batch(int32_t *sizes, int32_t *values, double *scores
   if (sizes) COOC_HIP_TRY(hipMemcpy(sizes, b_tk_size.p, sizeof(int32_t) * M, hipMemcpyDeviceToHost));
   if (values) COOC_HIP_TRY(hipMemcpy(values, b_tk_val.p, sizeof(int32_t) * M * k, hipMemcpyDeviceToHost));
   if (scores) COOC_HIP_TRY(hipMemcpy(scores, b_tk_score.p, sizeof(double) * M * k, hipMemcpyDeviceToHost));
+  return Status::Ok();
+}
+
+Status cooc_ctx::verify_batch(int32_t flags, uint64_t *d_row_checksum, int64_t *out8, hipStream_t s) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  const bool sym = (flags & COOC_VERIFY_SYMMETRY) != 0;
+  if (sym && batch_owned)
+    return Status{COOC_ERR_ARG, "COOC_VERIFY_SYMMETRY needs a whole result (not one part's owned rows)"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  COOC_TRY(b_verify.reserve(sizeof(uint64_t) * 8));
+  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  COOC_TRY(cooc::launch_verify(s, cfg.n_items, batch_result, sym && !batch_result.dense, d_row_checksum,
+                               b_verify.as<unsigned long long>()));
+  uint64_t h[8];
+  COOC_HIP_TRY(hipMemcpyAsync(h, b_verify.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  for (int i = 0; i < 8; i++) out8[i] = int64_t(h[i]);
+  if (!sym || batch_result.dense) out8[5] = -1;
+  out8[6] = out8[7] = 0;
   return Status::Ok();
 }

@@ -26,6 +26,8 @@ class StreamState {
                 const int32_t *items);
   Status finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info);
   Status copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+  // entries of the delta rows [r0, r1) (row indices as in copy_delta): a window streams out in row ranges
+  Status copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
   Status copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32);
   Status copy_topk(cooc_ctx &ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores);
   Status global_rowsums(cooc_ctx &ctx, int64_t *exact, int32_t *v32);
@@ -41,6 +43,8 @@ class StreamState {
  private:
   Status ensure_global(cooc_ctx &ctx);
   int32_t slot_for(int32_t user_id);
+  Status pack_delta(cooc_ctx &ctx);
+  Status copy_entries(int64_t e0, int64_t e1, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
   Status grow_arena(cooc_ctx &ctx, int64_t need);
   // n_items > Counter::kMaxGeneralItems: the window's delta rows as C(full histories) - C(histories
   // before the window) of its users, both counted by the large-universe planner
@@ -77,6 +81,13 @@ class StreamState {
   bool empty_window_ = false;  // the last window had no interaction left after user_cut
   cooc_window_info last_{};
   int32_t n_touched_ = 0;
+  // the last window's delta rows packed for copy-out (once per window)
+  bool delta_packed_ = false;
+  int64_t *pk_rp_ = nullptr;
+  int32_t *pk_col_ = nullptr;
+  uint32_t *pk_cnt_ = nullptr;
+  std::vector<int32_t> delta_rows_;
+  std::vector<int64_t> delta_start_;
 };
 
 // NonSampledUserInteractionCounterOneInputStreamOperator mirror: late-element drop, tumbling
@@ -125,6 +136,8 @@ struct cooc_ctx {
   cooc::Status topk_batch_device(int32_t topk, int32_t flags, const int64_t *d_rowsum_global, int32_t *d_sizes,
                                  int32_t *d_values, double *d_scores, hipStream_t s);
   cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
+  // cooc_verify_batch: invariant checks + row fingerprints of the last batch result
+  cooc::Status verify_batch(int32_t flags, uint64_t *d_row_checksum, int64_t *out8, hipStream_t s);
   cooc::Status llr(int64_t n, const int64_t *k, double *out);
   cooc::Status topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,
                           int32_t *values, double *scores);
@@ -146,9 +159,11 @@ struct cooc_ctx {
   cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3, b_llr_terms;
   // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
   cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
+  cooc::DevBuf b_verify;  // cooc_verify_batch totals
   int32_t batch_topk = 0;
   int32_t batch_topk_flags = 0;
   bool have_batch = false;
+  bool batch_owned = false;  // the last batch counted only the rows of one part (cooc_count_device_owned)
   int64_t batch_observed = 0;
   int64_t batch_nnz = 0;
   hipStream_t batch_stream = nullptr;

@@ -98,6 +98,7 @@ struct PlanTotals {
   int64_t max_tail;      // largest expected gather tail (pairs outside tile 0) of a work item
   int64_t n_gather_rows;  // whole rows in gather mode (their work items get bucket-start slots)
   int64_t n_gather;       // bucket-start slots handed out by the queue builder
+  int64_t bad_row;        // a row whose counts failed the row-sum check (err bit 1), for the message
 };
 
 // Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
@@ -235,6 +236,12 @@ Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr
 // Item frequencies of a device item array into counts int64[M] (zeroed first); ids outside [0, M) are
 // not counted.
 Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_t M, int64_t *counts);
+
+// Invariant checks + per-row fingerprints of a batch result (cooc_verify.hip): d_tot uint64[8] =
+// {sum of counts, sum of row sums, entries, rows whose counts miss their row sum, rows with a bad
+// entry, asymmetric entries (symmetry only), 0, 0}; d_cs (may be NULL) uint64[M] row checksums.
+Status launch_verify(hipStream_t s, int32_t M, const CountResult &r, bool symmetry, uint64_t *d_cs,
+                     unsigned long long *d_tot);
 
 // Sparse global rows of the streaming state (n_items >= 40,320; the rescorer's itemRows,
 // ItemRowRescorer...java:35,171-177): row a = len[a] (column, count) entries in ascending column order

@@ -134,6 +134,7 @@ struct SpArgs {
   int64_t n_contrib, n_users, n_groups;
   uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
   int64_t scr_cap;          // 0: gather mode off
+  const int64_t *rowsum;    // [M] closed-form row sums W_a - c_a (k_sp_plan): every whole row is checked
 };
 
 #ifdef COOC_SP_TRACE
@@ -599,6 +600,7 @@ struct SpStatic {
   uint32_t bstart[kSpMaxTiles + 1]; // gather mode: bucket starts in the workgroup's scratch
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
+  unsigned long long rsum;          // the current whole row's compacted counts, summed (row-sum check)
 #ifdef COOC_SP_STATS
   unsigned long long st[28];
 #endif
@@ -852,7 +854,8 @@ __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
 
 // Column-order compaction of w dense counters (16-B aligned), appended to the row's output; the
 // counters are left zero.  Waves own 256-column-aligned ranges, 4 counters per lane.
-__device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t w, int32_t c0) {
+__device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t w, int32_t c0,
+                                        uint64_t &rsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t *row = L.R;
   const int32_t per = ((w + kSpWaves - 1) / kSpWaves + 255) & ~255;
@@ -895,6 +898,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
     const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
     const uint32_t pre = uint32_t(__popcll(m0 & lt_mask)) + 2u * uint32_t(__popcll(m1 & lt_mask)) +
                          4u * uint32_t(__popcll(m2 & lt_mask));
+    rsum += uint64_t(v[0]) + v[1] + v[2] + v[3];
     if (c) {
       int64_t pos = base + off + pre;
 #pragma unroll
@@ -925,7 +929,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
 // block gets a 32-bit column mask (in the keys area) and a base (prefix of mask popcounts, in the
 // counts area); an entry goes to base + popcount(mask below its column).
 __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t H, int32_t c0,
-                                       int32_t c1) {
+                                       int32_t c1, uint64_t &rsum) {
   const int tid = threadIdx.x;
   const unsigned long long c_h0 = STAT_CLOCK();
   uint32_t *keys = L.R, *cnts = L.R + kHashMax;
@@ -946,6 +950,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
         const uint32_t col = k - 1u - uint32_t(c0);
         ek[i] = col;
         ec[i] = v;
+        rsum += v;
         atomicOr(&L.L1[col >> 10], 1u << ((col >> 5) & 31u));
       }
     }
@@ -1043,6 +1048,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
   __syncthreads();
+  uint64_t rsum = 0;  // this thread's share of the current whole row's count sum
   for (;;) {
     const int32_t w = uni(S_.work);
     if (w >= n_work) break;
@@ -1078,7 +1084,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       }
       S_.row_begin = S_.slab_cur;
       S_.row_n = 0;
+      S_.rsum = 0ull;
     }
+    // the closed-form row sum this row's counts must add up to (read now, compared at the end)
+    const int64_t rs_expect = (!split && tid == 0) ? A.rowsum[a] : 0;
     if (gather && tid < 64) {
       // bucket capacity of tile t >= 1 from the item's pair work Wi and contributions ci: a user
       // holds lambda = Wi g_t / ci of its ids on average, a (user, tile) segment of x ids takes
@@ -1177,7 +1186,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       } else if (dense) {
         if (tid == 0 && a >= c0 && a < c1) L.R[a - c0] -= self;
         __syncthreads();
-        sp_dense_compact(A, L, S_, c1 - c0, c0);
+        sp_dense_compact(A, L, S_, c1 - c0, c0, rsum);
         STAT_ADD(2, STAT_CLOCK() - c_walked);
       } else {
         if (tid == 0 && a >= c0 && a < c1) {
@@ -1191,7 +1200,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
           }
         }
         __syncthreads();
-        sp_hash_compact(A, L, S_, H, c0, c1);
+        sp_hash_compact(A, L, S_, H, c0, c1, rsum);
         STAT_ADD(3, STAT_CLOCK() - c_walked);
         STAT_ADD(14, H);
       }
@@ -1199,6 +1208,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       H = 0;
     }
     STAT_ADD(split ? 12 : 11, 1);
+    if (!split) {  // the row-sum check: every count of the row, summed exactly (u64), == W_a - c_a
+      for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
+      if ((tid & 63) == 0 && rsum) atomicAdd(&S_.rsum, (unsigned long long)rsum);
+    }
+    rsum = 0;
     if (!split && tid == 0) {
       A.row_base[a] = S_.row_n ? S_.row_begin : 0;
       A.row_nnz[a] = int32_t(S_.row_n);
@@ -1209,6 +1223,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     }
     if (tid == 0) S_.work = next;
     __syncthreads();
+    // a uint32 counter that wrapped, or any id lost or counted twice, breaks the sum
+    if (!split && tid == 0 && S_.rsum != (unsigned long long)rs_expect) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
+      A.tot->bad_row = a;
+    }
   }
 #ifdef COOC_SP_STATS
   if (tid == 0) {
@@ -1336,7 +1355,7 @@ __global__ void k_sp_nnz_total(const int32_t *__restrict__ row_nnz, int32_t M, P
 
 __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict__ qctr,
                                unsigned long long *__restrict__ bump) {
-  tot->err &= ~int64_t(4);
+  tot->err &= ~int64_t(6);  // the region (4) and row-sum (2) checks of the previous attempt
   tot->nnz_total = 0;
   qctr[0] = 0;
   bump[0] = 0;
@@ -1710,6 +1729,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.n_groups = n1 + 4;
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
+  proto.rowsum = rowsum_.as<int64_t>();
   int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));

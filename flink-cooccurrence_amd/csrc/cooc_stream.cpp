@@ -196,6 +196,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   const int32_t M = ctx.cfg.n_items;
   const int64_t n_act = n_staged_;
   PhaseTrace tr;
+  delta_packed_ = false;  // the packed copy-out view belongs to the previous window
   empty_window_ = n_act == 0;
   if (empty_window_) {
     // every interaction of the window was cut (user_cut): onEventTime emits nothing, no row is
@@ -396,38 +397,63 @@ Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, i
     if (row_ptr) row_ptr[0] = 0;
     return Status::Ok();
   }
+  COOC_TRY(pack_delta(ctx));
+  const int32_t R = int32_t(delta_rows_.size());
+  if (rows) std::memcpy(rows, delta_rows_.data(), sizeof(int32_t) * R);
+  if (row_ptr) std::memcpy(row_ptr, delta_start_.data(), sizeof(int64_t) * (R + 1));
+  return copy_entries(0, delta_start_[R], cols, cnt, cnt16);
+}
+
+// The window's delta rows packed (contiguous, ascending row then column) once per window, with the
+// host list of rows that have entries and their starts in the packed arrays.
+Status StreamState::pack_delta(cooc_ctx &ctx) {
+  if (delta_packed_) return Status::Ok();
   const int32_t M = ctx.cfg.n_items;
-  int64_t *d_rp;
-  int32_t *d_col;
-  uint32_t *d_cnt;
-  COOC_TRY(ctx.counter.pack(ctx.stream, &d_rp, &d_col, &d_cnt));
+  COOC_TRY(ctx.counter.pack(ctx.stream, &pk_rp_, &pk_col_, &pk_cnt_));
   COOC_HIP_TRY(hipStreamSynchronize(ctx.stream));
-  const int64_t nnz = last_.nnz;
-  if (rows || row_ptr) {
-    std::vector<int64_t> rp(M + 1);
-    COOC_HIP_TRY(hipMemcpy(rp.data(), d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
-    int32_t k = 0;
-    for (int32_t a = 0; a < M; a++) {
-      if (rp[a + 1] == rp[a]) continue;
-      if (rows) rows[k] = a;
-      if (row_ptr) row_ptr[k] = rp[a];
-      k++;
-    }
-    if (row_ptr) row_ptr[k] = rp[M];
+  std::vector<int64_t> rp(M + 1);
+  COOC_HIP_TRY(hipMemcpy(rp.data(), pk_rp_, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
+  delta_rows_.clear();
+  delta_start_.clear();
+  for (int32_t a = 0; a < M; a++) {
+    if (rp[a + 1] == rp[a]) continue;
+    delta_rows_.push_back(a);
+    delta_start_.push_back(rp[a]);
   }
-  if (cols && nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
-  if ((cnt || cnt16) && nnz) {
+  delta_start_.push_back(rp[M]);
+  delta_packed_ = true;
+  return Status::Ok();
+}
+
+Status StreamState::copy_entries(int64_t e0, int64_t e1, int32_t *cols, uint32_t *cnt, int16_t *cnt16) {
+  const int64_t n = e1 - e0;
+  if (n <= 0) return Status::Ok();
+  if (cols) COOC_HIP_TRY(hipMemcpy(cols, pk_col_ + e0, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (cnt || cnt16) {
     std::vector<uint32_t> tmp;
     uint32_t *dst = cnt;
     if (!dst) {
-      tmp.resize(nnz);
+      tmp.resize(n);
       dst = tmp.data();
     }
-    COOC_HIP_TRY(hipMemcpy(dst, d_cnt, sizeof(uint32_t) * nnz, hipMemcpyDeviceToHost));
+    COOC_HIP_TRY(hipMemcpy(dst, pk_cnt_ + e0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
     if (cnt16)  // ItemRowAggregator's Int2ShortOpenHashMap value (short addTo wraps)
-      for (int64_t i = 0; i < nnz; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
+      for (int64_t i = 0; i < n; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
   }
   return Status::Ok();
+}
+
+Status StreamState::copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int32_t *cols, uint32_t *cnt,
+                                     int16_t *cnt16) {
+  if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
+  COOC_HIP_TRY(hipSetDevice(ctx.device));
+  const int32_t R = empty_window_ ? 0 : last_.n_rows;
+  if (r0 < 0 || r1 < r0 || r1 > R)
+    return Status{COOC_ERR_ARG, "delta rows [" + std::to_string(r0) + ", " + std::to_string(r1) + ") outside [0, " +
+                                    std::to_string(R) + ")"};
+  if (r0 == r1) return Status::Ok();
+  COOC_TRY(pack_delta(ctx));
+  return copy_entries(delta_start_[r0], delta_start_[r1], cols, cnt, cnt16);
 }
 
 Status StreamState::copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32) {

@@ -5,9 +5,14 @@
  *       cooc_jni.c -L../csrc -lcooc_hip -Wl,-rpath,'$ORIGIN' -o libcooc_jni.so
  * (jvm/Makefile).  Error behaviour: COOC_ERR_ARG -> IllegalArgumentException, any other non-zero
  * status -> IllegalStateException, message = cooc_last_error(handle), as the reference throws
- * (ItemRowRescorerTwoInputStreamOperator.java:52-54,72-79,91-93).  Arrays are pinned with
- * Get/ReleasePrimitiveArrayCritical around one C call each; no caller pointer is kept (cooc.h
- * ownership rules). */
+ * (ItemRowRescorerTwoInputStreamOperator.java:52-54,72-79,91-93); a failed native allocation ->
+ * OutOfMemoryError.
+ *
+ * Java arrays are never pinned across a library call: the calls stage data, launch kernels and
+ * synchronise the GPU, and a JNI critical region around them would stall the garbage collector of
+ * every subtask sharing the TaskManager JVM.  Inputs are copied out of the Java heap with
+ * Get<Type>ArrayRegion into native scratch, outputs land in native scratch and are copied back with
+ * Set<Type>ArrayRegion after the call.  No caller pointer is kept (cooc.h ownership rules). */
 #include <jni.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -16,10 +21,14 @@
 
 #define H(h) ((cooc_ctx *)(intptr_t)(h))
 
-static void throw_status(JNIEnv *env, const cooc_ctx *ctx, int st) {
-  const char *cls = st == COOC_ERR_ARG ? "java/lang/IllegalArgumentException" : "java/lang/IllegalStateException";
+static void throw_class(JNIEnv *env, const char *cls, const char *msg) {
   jclass c = (*env)->FindClass(env, cls);
-  if (c) (*env)->ThrowNew(env, c, cooc_last_error(ctx));
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+static void throw_status(JNIEnv *env, const cooc_ctx *ctx, int st) {
+  throw_class(env, st == COOC_ERR_ARG ? "java/lang/IllegalArgumentException" : "java/lang/IllegalStateException",
+              cooc_last_error(ctx));
 }
 
 static int check(JNIEnv *env, const cooc_ctx *ctx, int st) {
@@ -27,20 +36,55 @@ static int check(JNIEnv *env, const cooc_ctx *ctx, int st) {
   return st;
 }
 
-/* A pinned primitive array (NULL array -> NULL pointer). */
+/* Native scratch for one Java array argument: n elements of elem bytes (a NULL array -> NULL). */
 typedef struct {
   jarray a;
+  jsize n;
   void *p;
-} pin;
+} scratch;
 
-static pin pin_get(JNIEnv *env, jarray a) {
-  pin x = {a, NULL};
-  if (a) x.p = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
-  return x;
+/* Allocates the scratch of array a (its length, or want elements when want >= 0); copy_in: fill it
+ * from the array.  Returns 0, or -1 with an exception pending. */
+static int scratch_get(JNIEnv *env, scratch *s, jarray a, size_t elem, jsize want, int copy_in, char type) {
+  s->a = a;
+  s->p = NULL;
+  s->n = 0;
+  if (!a) return 0;
+  const jsize len = (*env)->GetArrayLength(env, a);
+  s->n = want >= 0 ? want : len;
+  if (s->n > len) {
+    throw_class(env, "java/lang/ArrayIndexOutOfBoundsException", "array shorter than the native call needs");
+    return -1;
+  }
+  s->p = malloc(elem * (size_t)(s->n > 0 ? s->n : 1));
+  if (!s->p) {
+    throw_class(env, "java/lang/OutOfMemoryError", "cooc_jni: native scratch allocation failed");
+    return -1;
+  }
+  if (copy_in && s->n > 0) {
+    switch (type) {
+      case 'I': (*env)->GetIntArrayRegion(env, (jintArray)a, 0, s->n, (jint *)s->p); break;
+      case 'J': (*env)->GetLongArrayRegion(env, (jlongArray)a, 0, s->n, (jlong *)s->p); break;
+      case 'S': (*env)->GetShortArrayRegion(env, (jshortArray)a, 0, s->n, (jshort *)s->p); break;
+      case 'D': (*env)->GetDoubleArrayRegion(env, (jdoubleArray)a, 0, s->n, (jdouble *)s->p); break;
+    }
+    if ((*env)->ExceptionCheck(env)) return -1;
+  }
+  return 0;
 }
 
-static void pin_put(JNIEnv *env, pin x, int copy_back) {
-  if (x.a && x.p) (*env)->ReleasePrimitiveArrayCritical(env, x.a, x.p, copy_back ? 0 : JNI_ABORT);
+/* Copies the scratch back into its array (n elements) and frees it. */
+static void scratch_put(JNIEnv *env, scratch *s, int copy_out, char type, jsize n) {
+  if (s->a && s->p && copy_out && n > 0 && !(*env)->ExceptionCheck(env)) {
+    switch (type) {
+      case 'I': (*env)->SetIntArrayRegion(env, (jintArray)s->a, 0, n, (const jint *)s->p); break;
+      case 'J': (*env)->SetLongArrayRegion(env, (jlongArray)s->a, 0, n, (const jlong *)s->p); break;
+      case 'S': (*env)->SetShortArrayRegion(env, (jshortArray)s->a, 0, n, (const jshort *)s->p); break;
+      case 'D': (*env)->SetDoubleArrayRegion(env, (jdoubleArray)s->a, 0, n, (const jdouble *)s->p); break;
+    }
+  }
+  free(s->p);
+  s->p = NULL;
 }
 
 JNIEXPORT jlong JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_create(
@@ -48,10 +92,13 @@ JNIEXPORT jlong JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_create
     jshort userCut) {
   cooc_config cfg = {-1, nItems, topK, flags, windowMs, userCut, 0}; /* userCut 0 = the non-sampled path */
   cooc_ctx *h = NULL;
-  const jsize n = devices ? (*env)->GetArrayLength(env, devices) : 0;
-  jint *d = n ? (*env)->GetIntArrayElements(env, devices, NULL) : NULL;
-  int st = n ? cooc_create_on(&cfg, (const int32_t *)d, n, subtask, &h) : cooc_create(&cfg, &h);
-  if (d) (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
+  scratch d;
+  if (scratch_get(env, &d, devices, sizeof(jint), -1, 1, 'I')) {
+    scratch_put(env, &d, 0, 'I', 0);
+    return 0;
+  }
+  const int st = d.n ? cooc_create_on(&cfg, (const int32_t *)d.p, d.n, subtask, &h) : cooc_create(&cfg, &h);
+  scratch_put(env, &d, 0, 'I', 0);
   if (check(env, NULL, st)) return 0;
   return (jlong)(intptr_t)h;
 }
@@ -63,13 +110,16 @@ JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_destroy
 JNIEXPORT jlong JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_processElements(
     JNIEnv *env, jclass cls, jlong h, jint n, jintArray users, jintArray items, jlongArray ts) {
   int64_t late = 0;
-  pin u = pin_get(env, users), i = pin_get(env, items), t = pin_get(env, ts);
-  const int st = cooc_op_process_elements(H(h), n, (const int32_t *)u.p, (const int32_t *)i.p,
-                                          (const int64_t *)t.p, &late);
-  pin_put(env, t, 0);
-  pin_put(env, i, 0);
-  pin_put(env, u, 0);
-  check(env, H(h), st);
+  scratch u, i, t;
+  u.p = i.p = t.p = NULL;
+  if (!scratch_get(env, &u, users, sizeof(jint), n, 1, 'I') && !scratch_get(env, &i, items, sizeof(jint), n, 1, 'I') &&
+      !scratch_get(env, &t, ts, sizeof(jlong), n, 1, 'J')) {
+    check(env, H(h), cooc_op_process_elements(H(h), n, (const int32_t *)u.p, (const int32_t *)i.p,
+                                              (const int64_t *)t.p, &late));
+  }
+  scratch_put(env, &t, 0, 'J', 0);
+  scratch_put(env, &i, 0, 'I', 0);
+  scratch_put(env, &u, 0, 'I', 0);
   return late;
 }
 
@@ -83,35 +133,56 @@ JNIEXPORT jboolean JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_pro
   return JNI_TRUE;
 }
 
-JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyDelta(
-    JNIEnv *env, jclass cls, jlong h, jintArray rows, jlongArray rowPtr, jintArray cols, jshortArray cnt16) {
-  pin r = pin_get(env, rows), p = pin_get(env, rowPtr), c = pin_get(env, cols), v = pin_get(env, cnt16);
-  const int st = cooc_copy_window_delta(H(h), (int32_t *)r.p, (int64_t *)p.p, (int32_t *)c.p, NULL, (int16_t *)v.p);
-  pin_put(env, v, 1);
-  pin_put(env, c, 1);
-  pin_put(env, p, 1);
-  pin_put(env, r, 1);
-  check(env, H(h), st);
+/* The fired window's delta rows and their starts: rows int[nRows], rowPtr long[nRows + 1] (entry
+ * offsets; the entries themselves stream out with copyDeltaRange). */
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyDeltaRows(
+    JNIEnv *env, jclass cls, jlong h, jintArray rows, jlongArray rowPtr) {
+  scratch r, p;
+  r.p = p.p = NULL;
+  const jsize n = rows ? (*env)->GetArrayLength(env, rows) : 0;
+  if (!scratch_get(env, &r, rows, sizeof(jint), n, 0, 'I') && !scratch_get(env, &p, rowPtr, sizeof(jlong), n + 1, 0, 'J'))
+    check(env, H(h), cooc_copy_window_delta(H(h), (int32_t *)r.p, (int64_t *)p.p, NULL, NULL, NULL));
+  scratch_put(env, &p, 1, 'J', n + 1);
+  scratch_put(env, &r, 1, 'I', n);
+}
+
+/* Entries of delta rows [rowBegin, rowEnd): cols int[n], cnt16 short[n] with n = rowPtr[rowEnd] -
+ * rowPtr[rowBegin] (the caller sizes ranges so that n fits a Java array). */
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyDeltaRange(
+    JNIEnv *env, jclass cls, jlong h, jint rowBegin, jint rowEnd, jint n, jintArray cols, jshortArray cnt16) {
+  scratch c, v;
+  c.p = v.p = NULL;
+  if (!scratch_get(env, &c, cols, sizeof(jint), n, 0, 'I') && !scratch_get(env, &v, cnt16, sizeof(jshort), n, 0, 'S'))
+    check(env, H(h), cooc_copy_window_delta_range(H(h), rowBegin, rowEnd, (int32_t *)c.p, NULL, (int16_t *)v.p));
+  scratch_put(env, &v, 1, 'S', n);
+  scratch_put(env, &c, 1, 'I', n);
 }
 
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyRowSums(
     JNIEnv *env, jclass cls, jlong h, jintArray items, jintArray delta32) {
-  pin i = pin_get(env, items), d = pin_get(env, delta32);
-  const int st = cooc_copy_window_rowsums(H(h), (int32_t *)i.p, NULL, (int32_t *)d.p);
-  pin_put(env, d, 1);
-  pin_put(env, i, 1);
-  check(env, H(h), st);
+  scratch i, d;
+  i.p = d.p = NULL;
+  const jsize n = items ? (*env)->GetArrayLength(env, items) : 0;
+  if (!scratch_get(env, &i, items, sizeof(jint), n, 0, 'I') && !scratch_get(env, &d, delta32, sizeof(jint), n, 0, 'I'))
+    check(env, H(h), cooc_copy_window_rowsums(H(h), (int32_t *)i.p, NULL, (int32_t *)d.p));
+  scratch_put(env, &d, 1, 'I', n);
+  scratch_put(env, &i, 1, 'I', n);
 }
 
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyTopK(
     JNIEnv *env, jclass cls, jlong h, jintArray rows, jintArray sizes, jintArray values, jdoubleArray scores) {
-  pin r = pin_get(env, rows), z = pin_get(env, sizes), v = pin_get(env, values), s = pin_get(env, scores);
-  const int st = cooc_copy_window_topk(H(h), (int32_t *)r.p, (int32_t *)z.p, (int32_t *)v.p, (double *)s.p);
-  pin_put(env, s, 1);
-  pin_put(env, v, 1);
-  pin_put(env, z, 1);
-  pin_put(env, r, 1);
-  check(env, H(h), st);
+  scratch r, z, v, s;
+  r.p = z.p = v.p = s.p = NULL;
+  const jsize n = rows ? (*env)->GetArrayLength(env, rows) : 0;
+  const jsize nv = values ? (*env)->GetArrayLength(env, values) : 0;
+  if (!scratch_get(env, &r, rows, sizeof(jint), n, 0, 'I') && !scratch_get(env, &z, sizes, sizeof(jint), n, 0, 'I') &&
+      !scratch_get(env, &v, values, sizeof(jint), nv, 0, 'I') &&
+      !scratch_get(env, &s, scores, sizeof(jdouble), nv, 0, 'D'))
+    check(env, H(h), cooc_copy_window_topk(H(h), (int32_t *)r.p, (int32_t *)z.p, (int32_t *)v.p, (double *)s.p));
+  scratch_put(env, &s, 1, 'D', nv);
+  scratch_put(env, &v, 1, 'I', nv);
+  scratch_put(env, &z, 1, 'I', n);
+  scratch_put(env, &r, 1, 'I', n);
 }
 
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_counters(JNIEnv *env, jclass cls, jlong h,
@@ -126,11 +197,14 @@ JNIEXPORT jlongArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_c
     JNIEnv *env, jclass cls, jlong h, jlongArray userPtr, jintArray items) {
   const jsize n_users = (*env)->GetArrayLength(env, userPtr) - 1;
   cooc_window_info wi;
-  pin p = pin_get(env, userPtr), i = pin_get(env, items);
-  const int st = cooc_count_host(H(h), n_users, (const int64_t *)p.p, (const int32_t *)i.p, &wi);
-  pin_put(env, i, 0);
-  pin_put(env, p, 0);
-  if (check(env, H(h), st)) return NULL;
+  scratch p, i;
+  p.p = i.p = NULL;
+  int st = -1;
+  if (!scratch_get(env, &p, userPtr, sizeof(jlong), -1, 1, 'J') && !scratch_get(env, &i, items, sizeof(jint), -1, 1, 'I'))
+    st = check(env, H(h), cooc_count_host(H(h), n_users, (const int64_t *)p.p, (const int32_t *)i.p, &wi));
+  scratch_put(env, &i, 0, 'I', 0);
+  scratch_put(env, &p, 0, 'J', 0);
+  if (st) return NULL;
   jlongArray out = (*env)->NewLongArray(env, 2);
   if (out) {
     const jlong v[2] = {wi.nnz, wi.observed};
@@ -141,25 +215,31 @@ JNIEXPORT jlongArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_c
 
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyBatch(
     JNIEnv *env, jclass cls, jlong h, jlongArray rowPtr, jintArray cols, jshortArray cnt16, jintArray rowSums32) {
-  pin p = pin_get(env, rowPtr), c = pin_get(env, cols), v = pin_get(env, cnt16), r = pin_get(env, rowSums32);
-  const int st = cooc_copy_batch(H(h), (int64_t *)p.p, (int32_t *)c.p, NULL, (int16_t *)v.p, NULL, (int32_t *)r.p);
-  pin_put(env, r, 1);
-  pin_put(env, v, 1);
-  pin_put(env, c, 1);
-  pin_put(env, p, 1);
-  check(env, H(h), st);
+  scratch p, c, v, r;
+  p.p = c.p = v.p = r.p = NULL;
+  if (!scratch_get(env, &p, rowPtr, sizeof(jlong), -1, 0, 'J') && !scratch_get(env, &c, cols, sizeof(jint), -1, 0, 'I') &&
+      !scratch_get(env, &v, cnt16, sizeof(jshort), -1, 0, 'S') &&
+      !scratch_get(env, &r, rowSums32, sizeof(jint), -1, 0, 'I'))
+    check(env, H(h), cooc_copy_batch(H(h), (int64_t *)p.p, (int32_t *)c.p, NULL, (int16_t *)v.p, NULL, (int32_t *)r.p));
+  scratch_put(env, &r, 1, 'I', r.n);
+  scratch_put(env, &v, 1, 'S', v.n);
+  scratch_put(env, &c, 1, 'I', c.n);
+  scratch_put(env, &p, 1, 'J', p.n);
 }
 
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_topKItems(
     JNIEnv *env, jclass cls, jlong h, jint k, jint flags, jintArray items, jintArray sizes, jintArray values,
     jdoubleArray scores) {
-  const jsize n = (*env)->GetArrayLength(env, items);
-  pin i = pin_get(env, items), z = pin_get(env, sizes), v = pin_get(env, values), s = pin_get(env, scores);
-  const int st = cooc_topk_items(H(h), k, flags, n, (const int32_t *)i.p, (int32_t *)z.p, (int32_t *)v.p,
-                                 (double *)s.p);
-  pin_put(env, s, 1);
-  pin_put(env, v, 1);
-  pin_put(env, z, 1);
-  pin_put(env, i, 0);
-  check(env, H(h), st);
+  scratch i, z, v, s;
+  i.p = z.p = v.p = s.p = NULL;
+  const jsize n = items ? (*env)->GetArrayLength(env, items) : 0;
+  if (!scratch_get(env, &i, items, sizeof(jint), n, 1, 'I') && !scratch_get(env, &z, sizes, sizeof(jint), n, 0, 'I') &&
+      !scratch_get(env, &v, values, sizeof(jint), n * k, 0, 'I') &&
+      !scratch_get(env, &s, scores, sizeof(jdouble), n * k, 0, 'D'))
+    check(env, H(h), cooc_topk_items(H(h), k, flags, n, (const int32_t *)i.p, (int32_t *)z.p, (int32_t *)v.p,
+                                     (double *)s.p));
+  scratch_put(env, &s, 1, 'D', n * k);
+  scratch_put(env, &v, 1, 'I', n * k);
+  scratch_put(env, &z, 1, 'I', n);
+  scratch_put(env, &i, 0, 'I', 0);
 }

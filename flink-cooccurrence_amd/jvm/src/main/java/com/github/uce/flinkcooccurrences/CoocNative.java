@@ -42,10 +42,18 @@ final class CoocNative {
   static native boolean processWatermark(long handle, long watermark, long[] info);
 
   /**
-   * cooc_copy_window_delta of the fired window: rows int[nRows], rowPtr long[nRows + 1], cols int[nnz],
-   * cnt16 short[nnz] -- the window's reduced ItemRowAggregator rows (Int2ShortOpenHashMap values).
+   * cooc_copy_window_delta of the fired window, rows only: rows int[nRows] (ascending items with a delta
+   * row), rowPtr long[nRows + 1] (their entry offsets).  The entries stream out with copyDeltaRange, so
+   * that a window larger than one Java array (2^31 - 1 entries) never needs one.
    */
-  static native void copyDelta(long handle, int[] rows, long[] rowPtr, int[] cols, short[] cnt16);
+  static native void copyDeltaRows(long handle, int[] rows, long[] rowPtr);
+
+  /**
+   * cooc_copy_window_delta_range: the entries of delta rows [rowBegin, rowEnd) -- cols int[n], cnt16
+   * short[n] with n = rowPtr[rowEnd] - rowPtr[rowBegin] -- the window's reduced ItemRowAggregator rows
+   * (Int2ShortOpenHashMap values, ItemRowAggregator.java:26-31).
+   */
+  static native void copyDeltaRange(long handle, int rowBegin, int rowEnd, int n, int[] cols, short[] cnt16);
 
   /** cooc_copy_window_rowsums: items int[nRows], delta32 int[nRows] (RowSumAggregator values). */
   static native void copyRowSums(long handle, int[] items, int[] delta32);

@@ -1,5 +1,6 @@
 package com.github.uce.flinkcooccurrences;
 
+import it.unimi.dsi.fastutil.ints.Int2ShortOpenHashMap;
 import java.util.Arrays;
 import java.util.concurrent.TimeUnit;
 import org.apache.flink.api.common.accumulators.IntCounter;
@@ -15,49 +16,41 @@ import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 import org.apache.flink.util.OutputTag;
 
 /**
- * Drop-in for {@link NonSampledUserInteractionCounterOneInputStreamOperator} (same class shape,
- * constructor arguments, output type and side-output tags, NonSampled...java:31-34,41-46,61,174-176)
- * whose pair expansion and per-window reduction run on an MI355X through libcooc_hip.so.
- *
- * <p>Keyed state moves to the device: the per-user histories of this subtask live in the handle.
- * processElement only buffers the record; processWatermark hands the batch to the device (late
- * records are dropped there, NonSampled...java:89-91) and emits every window the watermark closes,
- * already reduced:
+ * The pair emitter AND both keyed window reducers of the {@code --skip-cuts} graph on an MI355X: it
+ * replaces NonSampledUserInteractionCounterOneInputStreamOperator (FlinkCooccurrences.java:65-74) plus
+ * the ItemRowAggregator and RowSumAggregator windows (FlinkCooccurrences.java:135-157).  No
+ * ItemCooccurrences record is created: every window the watermark closes leaves the device already
+ * reduced, on two side outputs whose records are exactly what the two reference windows emit:
  * <ul>
- *   <li>{@code itemCooccurrences}: one {@link ItemCooccurrences} per (row, column) of the window's delta
- *   rows with {@code increment = (short) count}, so the reference's ItemRowAggregator (addTo,
- *   ItemRowAggregator.java:26-31) rebuilds the same Int2ShortOpenHashMap: addTo is modular, so one
- *   wrapped add of the reduced count equals the reference's count of +1 adds;</li>
- *   <li>{@code rowSums}: one Tuple2(item, delta) per row with a non-zero int delta (RowSumAggregator.java:25-27,66).</li>
+ *   <li>{@link #ROWS_TAG}: one {@code Tuple2<Integer, Int2ShortOpenHashMap>} per item with a delta row
+ *   (ItemCooccurrenceRowWindowFunction.process, ItemRowAggregator.java:50-56): the map holds every
+ *   touched column with the count as a Java short (addTo wraps, ItemRowAggregator.java:29);</li>
+ *   <li>{@link #ROW_SUM_TAG}: one {@code Tuple2<Integer, Integer>} per item whose int row-sum delta is
+ *   non-zero (RowSumProcessWindow.process, RowSumAggregator.java:54-71), and the
+ *   RowSumProcessWindowRowSum accumulator (:50,67).</li>
  * </ul>
- * Every record carries the window's maxTimestamp (NonSampled...java:115,126-127).  With parallelism p,
- * each subtask owns a user shard (keyBy(0) upstream) and the GPU devices[subtask % devices.length];
- * the downstream keyBy(item) aggregators sum the shards' partial rows exactly as before.
- *
- * <p>This variant keeps the reference's keyed reducers (one record per (row, column) crosses the shuffle
- * into ItemRowAggregator); {@link GpuNonSampledCooccurrenceRowsOperator} replaces them as well.
- *
- * <p>Wiring (FlinkCooccurrences.java:70-74):
- * <pre>
- *   interactionStream.keyBy(0).transform("GpuNonSampledUserInteractionCounter",
- *       GpuNonSampledUserInteractionCounterOneInputStreamOperator.getOutputType(),
- *       new GpuNonSampledUserInteractionCounterOneInputStreamOperator(windowSize, windowUnit, nItems, devices));
- * </pre>
- * Uncompiled in the build container (no JDK, Flink 1.3.2 jars absent).
+ * Every record carries the window's maxTimestamp, as a window operator's output does.  With one subtask
+ * the rows and row sums are final and feed ItemRowRescorerTwoInputStreamOperator directly; with p > 1
+ * each subtask holds a user shard (keyBy(0)), so its rows are partial and one keyed reduce per stream
+ * ({@link GpuCooccurrenceJob}) sums the p partial rows per item and window -- p records per row
+ * instead of one record per ordered pair.  Emitted objects are fresh (the rescorer buffers them by
+ * timestamp, ItemRowRescorer...java:83-113, and object reuse is on, FlinkCooccurrences.java:44).
+ * Uncompiled in the build container (no JDK, Flink 1.3.2 / fastutil jars absent); the C-ABI call
+ * sequence it makes is replayed by tests/test_boundary_sequence.py.
  */
-public class GpuNonSampledUserInteractionCounterOneInputStreamOperator
+public class GpuNonSampledCooccurrenceRowsOperator
     extends AbstractStreamOperator<Void>
     implements OneInputStreamOperator<Tuple3<Integer, Integer, Long>, Void> {
 
-  private static final long serialVersionUID = 4120558829541227043L;
+  private static final long serialVersionUID = 7321170436981573315L;
 
   @SuppressWarnings("serial")
-  private static final OutputTag<ItemCooccurrences> ITEM_TAG =
-      new OutputTag<ItemCooccurrences>("itemCooccurrences") {};
+  static final OutputTag<Tuple2<Integer, Int2ShortOpenHashMap>> ROWS_TAG =
+      new OutputTag<Tuple2<Integer, Int2ShortOpenHashMap>>("itemCooccurrenceRows") {};
 
   @SuppressWarnings("serial")
-  private static final OutputTag<Tuple2<Integer, Integer>> ROW_SUM_TAG =
-      new OutputTag<Tuple2<Integer, Integer>>("rowSums") {};
+  static final OutputTag<Tuple2<Integer, Integer>> ROW_SUM_TAG =
+      new OutputTag<Tuple2<Integer, Integer>>("rowSumsReduced") {};
 
   private final long windowSizeMs;
   private final int nItems;
@@ -70,15 +63,11 @@ public class GpuNonSampledUserInteractionCounterOneInputStreamOperator
   private transient long[] timestamps;
   private transient long[] info;
   private transient CoocWindowReader reader;
-  private transient Tuple2<Integer, Integer> rowSumsReuse;
-  private transient StreamRecord<Tuple2<Integer, Integer>> rowSumsOutputRecord;
-  private transient ItemCooccurrences itemCooccurrencesReuse;
-  private transient StreamRecord<ItemCooccurrences> itemCooccurrencesOutputRecord;
   private transient IntCounter lateElements;
   private transient LongCounter observedCooccurrences;
+  private transient LongCounter rowSumCounter;
 
-  GpuNonSampledUserInteractionCounterOneInputStreamOperator(int windowSize, TimeUnit windowUnit, int nItems,
-      int[] devices) {
+  GpuNonSampledCooccurrenceRowsOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices) {
     this.windowSizeMs = windowUnit.toMillis(windowSize);
     this.nItems = nItems;
     this.devices = devices.clone();
@@ -94,12 +83,9 @@ public class GpuNonSampledUserInteractionCounterOneInputStreamOperator
     this.timestamps = new long[1 << 16];
     this.info = new long[6];
     this.reader = new CoocWindowReader();
-    this.rowSumsReuse = new Tuple2<>();
-    this.rowSumsOutputRecord = new StreamRecord<>(rowSumsReuse);
-    this.itemCooccurrencesReuse = new ItemCooccurrences();
-    this.itemCooccurrencesOutputRecord = new StreamRecord<>(itemCooccurrencesReuse);
     this.lateElements = getRuntimeContext().getIntCounter("UserInteractionCounterLateElements");
     this.observedCooccurrences = getRuntimeContext().getLongCounter("UserInteractionCounterObservedCooccurrences");
+    this.rowSumCounter = getRuntimeContext().getLongCounter("RowSumProcessWindowRowSum");
   }
 
   @Override
@@ -128,28 +114,23 @@ public class GpuNonSampledUserInteractionCounterOneInputStreamOperator
     super.processWatermark(mark);
   }
 
-  /** The fired window's delta rows and row sums, on the reference's two side outputs. */
   private void emitWindow() {
     final long timestamp = info[0];
     final int nRows = (int) info[3];
-    rowSumsOutputRecord.setTimestamp(timestamp);
-    itemCooccurrencesOutputRecord.setTimestamp(timestamp);
-
-    // rows stream out in ranges (a C3-sized window holds more entries than one Java array)
     reader.forEachRow(handle, nRows, (item, cols, cnt16, from, to) -> {
+      final Int2ShortOpenHashMap row = new Int2ShortOpenHashMap(to - from);
       for (int j = from; j < to; j++) {
-        itemCooccurrencesReuse.setFields(item, cols[j], cnt16[j]);
-        output.collect(ITEM_TAG, itemCooccurrencesOutputRecord);
+        row.put(cols[j], cnt16[j]);
       }
+      output.collect(ROWS_TAG, new StreamRecord<>(Tuple2.of(item, row), timestamp));
     });
-
     final int[] sumItems = new int[nRows];
     final int[] delta32 = new int[nRows];
     CoocNative.copyRowSums(handle, sumItems, delta32);
     for (int r = 0; r < nRows; r++) {
-      if (delta32[r] != 0) {
-        rowSumsReuse.setFields(sumItems[r], delta32[r]);
-        output.collect(ROW_SUM_TAG, rowSumsOutputRecord);
+      if (delta32[r] != 0) {  // RowSumAggregator.java:66
+        rowSumCounter.add(delta32[r]);
+        output.collect(ROW_SUM_TAG, new StreamRecord<>(Tuple2.of(sumItems[r], delta32[r]), timestamp));
       }
     }
     observedCooccurrences.add(info[2]);
@@ -166,8 +147,6 @@ public class GpuNonSampledUserInteractionCounterOneInputStreamOperator
       super.close();
     }
   }
-
-  // -------------------------------------------------------------------------------------------------------------------
 
   static TypeInformation<Void> getOutputType() {
     return new TypeHint<Void>() {}.getTypeInfo();

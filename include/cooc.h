@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 3
+#define COOC_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -213,6 +213,12 @@ COOC_API int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_in
  * rows int32[n_rows] ascending, row_ptr int64[n_rows+1], cols/cnt/cnt16 [nnz].  NULLs skipped. */
 COOC_API int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,
                            int16_t *cnt16);
+/* The entries of delta rows [row_begin, row_end) only (row indices as in cooc_copy_window_delta's rows[]):
+ * cols/cnt/cnt16 [row_ptr[row_end] - row_ptr[row_begin]].  A window whose delta holds more entries than
+ * one Java array can (2^31 - 1) streams out in row ranges: first cooc_copy_window_delta(rows, row_ptr,
+ * NULL, NULL, NULL), then ranges sized from row_ptr.  The packed copy-out view is built once per window. */
+COOC_API int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *cols,
+                                          uint32_t *cnt, int16_t *cnt16);
 /* Row-sum updates of the last window, one per delta row (same order as rows): exact int64 and the
  * reference's int view (RowSumAggregator.java:25-27; the reference drops an update whose int
  * value is 0, RowSumAggregator.java:66 -- the caller applies that filter on delta32). */
@@ -315,6 +321,26 @@ COOC_API int cooc_records_decode(const uint8_t *bytes, int64_t n_bytes, int64_t 
  * AscendingTimestampExtractor after a prefix of records is (largest timestamp so far) - 1. */
 COOC_API int cooc_parse_interactions(const char *text, int64_t n_bytes, int64_t cap, int32_t *users, int32_t *items,
                                      int64_t *ts, int64_t *n_records, int64_t *bad_line);
+
+/* ---- invariant checks of a batch result (the reference's DEVELOPMENT_MODE checks) ---------------
+ * FlinkCooccurrences.java:34 switches on, among others, the row-sum consistency check of the rescorer
+ * (ItemRowRescorer...java:183-193: the sum of a row == the item's row sum).  cooc_verify_batch runs it,
+ * and the checks of this library's CSR contract, over the whole last cooc_count_device /
+ * cooc_count_device_owned result on hip_stream (then synchronises it).  out8 (host int64[8]):
+ *   [0] sum of all counts         [1] sum of the row sums (== [0] == observed for a whole result)
+ *   [2] entries                   [3] rows whose counts do not sum to their row sum
+ *   [4] rows with a bad entry: columns not strictly ascending or outside [0, n_items), a count of 0
+ *       (dense layout: row_nnz[a] != the row's non-zero cells)
+ *   [5] entries with C[a,b] != C[b,a] (only with COOC_VERIFY_SYMMETRY, padded CSR of a whole result;
+ *       else -1)                  [6], [7] 0
+ * d_row_checksum (device uint64[n_items], may be NULL): per row, the sum over its keys of
+ * splitmix64((col << 32) ^ count) mod 2^64 (splitmix64(x): x += 0x9E3779B97F4A7C15;
+ * x = (x ^ x >> 30) * 0xBF58476D1CE4E5B9; x = (x ^ x >> 27) * 0x94D049BB133111EB; x ^ x >> 31), a
+ * fingerprint to compare the result row by row with an independent restatement without copying it
+ * out. */
+#define COOC_VERIFY_SYMMETRY 1
+COOC_API int cooc_verify_batch(cooc_ctx *ctx, int32_t flags, uint64_t *d_row_checksum, int64_t *out8,
+                               void *hip_stream);
 
 /* ---- diagnostics (not part of the reference surface) ------------------------------------------
  * Kernel timing of the dominant kernel (the accumulate kernel) with HIP events recorded on the

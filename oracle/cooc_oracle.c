@@ -868,7 +868,20 @@ typedef struct {
   const int32_t *items;
   int32_t n_items, n_threads, t;
   int64_t nnz, pairs;
+  uint64_t *row_cs;  /* optional per-row outputs (oc_row_key_hash below) */
+  int64_t *row_nnz, *row_sum;
 } mt_job;
+
+/* Row checksum entry hash (the same definition as the library's cooc_verify_batch, include/cooc.h):
+ * splitmix64 of (column << 32 | exact count); a row's checksum is the sum of its entries' hashes
+ * mod 2^64, so it does not depend on the order the row's keys are visited in. */
+static uint64_t oc_row_key_hash(int32_t col, uint64_t count) {
+  uint64_t x = ((uint64_t)(uint32_t)col << 32) ^ count;
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 
 static void *mt_run(void *arg) {
   mt_job *j = (mt_job *)arg;
@@ -900,8 +913,22 @@ static void *mt_run(void *arg) {
     }
   }
   int64_t nnz = 0;
-  for (int32_t i = 0; i < n_own; i++)
+  for (int32_t i = 0; i < n_own; i++) {
+    if (j->row_cs) { /* row a = i * T + t (rows without keys stay 0) */
+      const int64_t a = (int64_t)i * T + t;
+      uint64_t cs = 0;
+      int64_t sum = 0;
+      if (live[i])
+        for (int32_t e = 0; e < rows[i].n; e++) {
+          cs += oc_row_key_hash(rows[i].col[e], (uint64_t)rows[i].exact[e]);
+          sum += rows[i].exact[e];
+        }
+      j->row_cs[a] = cs;
+      j->row_nnz[a] = live[i] ? rows[i].n : 0;
+      j->row_sum[a] = sum;
+    }
     if (live[i]) { nnz += rows[i].n; rowmap_free(&rows[i]); }
+  }
   free(rows);
   free(live);
   j->nnz = nnz;
@@ -909,13 +936,16 @@ static void *mt_run(void *arg) {
   return NULL;
 }
 
-EXPORT int64_t oc_count_batch_mt(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int32_t n_items,
-                                 int32_t n_threads, int64_t *pairs) {
+/* The restatement above, with optional per-row outputs: checksum (sum of oc_row_key_hash over the
+ * row's keys), distinct keys and the sum of the exact counts (int64 [n_items] each, or all NULL). */
+EXPORT int64_t oc_count_batch_mt_rows(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int32_t n_items,
+                                      int32_t n_threads, int64_t *pairs, uint64_t *row_cs, int64_t *row_nnz,
+                                      int64_t *row_sum) {
   if (n_threads < 1) n_threads = 1;
   mt_job *jobs = (mt_job *)calloc((size_t)n_threads, sizeof(mt_job));
   pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
   for (int32_t t = 0; t < n_threads; t++) {
-    jobs[t] = (mt_job){n_users, user_ptr, items, n_items, n_threads, t, 0, 0};
+    jobs[t] = (mt_job){n_users, user_ptr, items, n_items, n_threads, t, 0, 0, row_cs, row_nnz, row_sum};
     pthread_create(&th[t], NULL, mt_run, &jobs[t]);
   }
   int64_t nnz = 0, pr = 0;
@@ -926,6 +956,114 @@ EXPORT int64_t oc_count_batch_mt(int64_t n_users, const int64_t *user_ptr, const
   }
   free(jobs);
   free(th);
+  if (pairs) *pairs = pr;
+  return nnz;
+}
+
+EXPORT int64_t oc_count_batch_mt(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int32_t n_items,
+                                 int32_t n_threads, int64_t *pairs) {
+  return oc_count_batch_mt_rows(n_users, user_ptr, items, n_items, n_threads, pairs, NULL, NULL, NULL);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Per-row checksums in closed form, for exactness checks at the benchmark's size (1e10 pairs).  */
+/* Row a of C = A^T A - diag(colsum A) (the sum over windows of NonSampled:113-165, SURVEY.md     */
+/* §0.3) is the sum of the lists of the users holding a (once per occurrence of a), minus one at  */
+/* column a per occurrence.  Gustavson row by row: the users of every item by a counting sort     */
+/* (the transpose of A), then a dense int64 accumulator per thread and a touched-column list.     */
+/* Rows are handed out in blocks of 64 from an atomic counter.  Writes the same per-row checksum, */
+/* key count and count sum as oc_count_batch_mt_rows (it is cross-checked against it and against */
+/* scipy in tests/test_oracle_semantics.py).  Returns the distinct keys; *pairs = ordered pairs.  */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const int64_t *user_ptr;
+  const int32_t *items;
+  const int64_t *item_ptr; /* [n_items + 1] */
+  const int64_t *item_users;
+  int32_t n_items;
+  int64_t *next;           /* shared row-block counter */
+  uint64_t *row_cs;
+  int64_t *row_nnz, *row_sum;
+  int64_t nnz, pairs;
+} gus_job;
+
+static void *gus_run(void *arg) {
+  gus_job *j = (gus_job *)arg;
+  const int32_t M = j->n_items;
+  int64_t *acc = (int64_t *)calloc((size_t)M, sizeof(int64_t));
+  int32_t *touched = (int32_t *)malloc(sizeof(int32_t) * (size_t)M);
+  int64_t nnz = 0, pairs = 0;
+  for (;;) {
+    const int64_t b0 = __atomic_fetch_add(j->next, 64, __ATOMIC_RELAXED);
+    if (b0 >= M) break;
+    const int64_t b1 = b0 + 64 < M ? b0 + 64 : M;
+    for (int64_t a = b0; a < b1; a++) {
+      int32_t nt = 0;
+      for (int64_t k = j->item_ptr[a]; k < j->item_ptr[a + 1]; k++) {
+        const int64_t u = j->item_users[k];
+        for (int64_t p = j->user_ptr[u]; p < j->user_ptr[u + 1]; p++) {
+          const int32_t b = j->items[p];
+          if (acc[b]++ == 0) touched[nt++] = b;
+        }
+      }
+      const int64_t occ = j->item_ptr[a + 1] - j->item_ptr[a];
+      acc[a] -= occ; /* the pair of a position with itself */
+      uint64_t cs = 0;
+      int64_t n = 0, sum = 0;
+      for (int32_t i = 0; i < nt; i++) {
+        const int32_t b = touched[i];
+        if (acc[b]) {
+          cs += oc_row_key_hash(b, (uint64_t)acc[b]);
+          n++;
+          sum += acc[b];
+        }
+        acc[b] = 0;
+      }
+      j->row_cs[a] = cs;
+      j->row_nnz[a] = n;
+      j->row_sum[a] = sum;
+      nnz += n;
+      pairs += sum;
+    }
+  }
+  free(acc);
+  free(touched);
+  j->nnz = nnz;
+  j->pairs = pairs;
+  return NULL;
+}
+
+EXPORT int64_t oc_row_checksums(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int32_t n_items,
+                                int32_t n_threads, int64_t *pairs, uint64_t *row_cs, int64_t *row_nnz,
+                                int64_t *row_sum) {
+  if (n_threads < 1) n_threads = 1;
+  const int64_t n = n_users > 0 ? user_ptr[n_users] : 0;
+  int64_t *item_ptr = (int64_t *)calloc((size_t)n_items + 1, sizeof(int64_t));
+  int64_t *item_users = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  for (int64_t p = 0; p < n; p++) item_ptr[items[p] + 1]++;
+  for (int32_t a = 0; a < n_items; a++) item_ptr[a + 1] += item_ptr[a];
+  int64_t *cur = (int64_t *)malloc(sizeof(int64_t) * (size_t)n_items);
+  memcpy(cur, item_ptr, sizeof(int64_t) * (size_t)n_items);
+  for (int64_t u = 0; u < n_users; u++)
+    for (int64_t p = user_ptr[u]; p < user_ptr[u + 1]; p++) item_users[cur[items[p]]++] = u;
+  free(cur);
+  int64_t next = 0;
+  gus_job *jobs = (gus_job *)calloc((size_t)n_threads, sizeof(gus_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+  for (int32_t t = 0; t < n_threads; t++) {
+    jobs[t] = (gus_job){user_ptr, items, item_ptr, item_users, n_items, &next, row_cs, row_nnz, row_sum, 0, 0};
+    pthread_create(&th[t], NULL, gus_run, &jobs[t]);
+  }
+  int64_t nnz = 0, pr = 0;
+  for (int32_t t = 0; t < n_threads; t++) {
+    pthread_join(th[t], NULL);
+    nnz += jobs[t].nnz;
+    pr += jobs[t].pairs;
+  }
+  free(jobs);
+  free(th);
+  free(item_ptr);
+  free(item_users);
   if (pairs) *pairs = pr;
   return nnz;
 }

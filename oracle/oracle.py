@@ -38,6 +38,7 @@ i32p = ctypes.POINTER(ctypes.c_int32)
 i64p = ctypes.POINTER(ctypes.c_int64)
 i16p = ctypes.POINTER(ctypes.c_int16)
 f64p = ctypes.POINTER(ctypes.c_double)
+u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
 def build() -> str:
@@ -96,6 +97,10 @@ def lib():
         "oc_global_rowsums": (None, [vp, i32p, i32p, i64p]),
         "oc_batch_dense": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, i64p, i64p]),
         "oc_count_batch_mt": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, ctypes.c_int32, i64p]),
+        "oc_count_batch_mt_rows": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, ctypes.c_int32, i64p,
+                                                    u64p, i64p, i64p]),
+        "oc_row_checksums": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, ctypes.c_int32, i64p,
+                                              u64p, i64p, i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -325,6 +330,65 @@ def count_batch_mt(user_ptr: np.ndarray, items: np.ndarray, n_items: int, n_thre
     pairs = np.zeros(1, np.int64)
     nnz = lib().oc_count_batch_mt(len(up) - 1, _p(up, i64p), _p(it, i32p), n_items, n_threads, _p(pairs, i64p))
     return int(nnz), int(pairs[0])
+
+
+@dataclass
+class RowChecks:
+    """Per-row exactness fingerprint of a count matrix: checksum = sum over the row's keys of
+    splitmix64(col << 32 ^ exact count) mod 2^64 (row_key_hash; the library's cooc_verify_batch
+    computes the same), distinct keys and the sum of the counts; plus the totals."""
+    checksum: np.ndarray  # uint64 [n_items]
+    nnz: np.ndarray       # int64 [n_items]
+    rowsum: np.ndarray    # int64 [n_items]
+    distinct: int
+    pairs: int
+
+
+def _row_checks(fn, user_ptr, items, n_items: int, n_threads: int) -> RowChecks:
+    up = np.ascontiguousarray(user_ptr, np.int64)
+    it = np.ascontiguousarray(items, np.int32)
+    cs = np.zeros(n_items, np.uint64)
+    nz = np.zeros(n_items, np.int64)
+    rs = np.zeros(n_items, np.int64)
+    pairs = np.zeros(1, np.int64)
+    nnz = fn(len(up) - 1, _p(up, i64p), _p(it, i32p), n_items, n_threads, _p(pairs, i64p), _p(cs, u64p), _p(nz, i64p),
+             _p(rs, i64p))
+    return RowChecks(cs, nz, rs, int(nnz), int(pairs[0]))
+
+
+def count_batch_mt_rows(user_ptr, items, n_items: int, n_threads: int) -> RowChecks:
+    """count_batch_mt (the record-by-record restatement, NonSampled...java:129-161 into
+    Int2ShortOpenHashMap restatements) with its per-row fingerprints."""
+    return _row_checks(lib().oc_count_batch_mt_rows, user_ptr, items, n_items, n_threads)
+
+
+def row_checksums(user_ptr, items, n_items: int, n_threads: int) -> RowChecks:
+    """The same fingerprints from the closed form (C = A^T A - diag(colsum A), row by row with a dense
+    accumulator per thread): fast enough for the benchmark's 3.4e10-pair shard."""
+    return _row_checks(lib().oc_row_checksums, user_ptr, items, n_items, n_threads)
+
+
+def row_key_hash(cols, counts) -> np.ndarray:
+    """splitmix64((col << 32) ^ count) per entry (uint64), the checksum term of RowChecks."""
+    with np.errstate(over="ignore"):
+        x = (np.asarray(cols, np.int64).astype(np.uint64) << np.uint64(32)) ^ np.asarray(counts, np.int64).astype(np.uint64)
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def csr_row_checks(row_ptr, cols, counts) -> RowChecks:
+    """RowChecks of a sorted CSR (e.g. closed_form's)."""
+    rp = np.asarray(row_ptr, np.int64)
+    M = len(rp) - 1
+    rows = np.repeat(np.arange(M), np.diff(rp))
+    h = row_key_hash(cols, counts)
+    cs = np.zeros(M, np.uint64)
+    np.add.at(cs, rows, h)
+    rs = np.zeros(M, np.int64)
+    np.add.at(rs, rows, np.asarray(counts, np.int64))
+    return RowChecks(cs, np.diff(rp), rs, int(rp[-1]), int(rs.sum()))
 
 
 def cut_csr(user_ptr: np.ndarray, items: np.ndarray, user_cut: int):

@@ -38,6 +38,13 @@ if "SQ_LDS_IDX_ACTIVE" in avg and "GRBM_GUI_ACTIVE" in avg:
     res["lds_bank_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"]
 if "SQ_WAIT_ANY" in avg:
     res["wave_wait_frac"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
+# the code the counters belong to: bench.py reports traffic / limiter only when its own source digest matches
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_digest  # noqa: E402
+
+res["source_digest"] = source_digest()
+sha_file = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), ".build_sha")
+res["git_sha"] = open(sha_file).read().strip() if os.path.exists(sha_file) else None
 os.makedirs(os.path.dirname(out), exist_ok=True)
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "counters_avg"}, indent=1))

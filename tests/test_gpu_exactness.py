@@ -1,0 +1,93 @@
+"""Exactness of the large-universe path (k_sp_main, the C3 / C5 hot path) at the benchmark's sizes.
+
+Every row of the device result is compared with an independent CPU restatement through per-row
+fingerprints (cooc_verify_batch: checksum = sum over the row's keys of splitmix64(col << 32 ^ count),
+key count, count sum; oracle.RowChecks restates the same):
+
+* 1/256 of the C3 log (39,062 users, ~1e9 ordered pairs) against the record-by-record restatement
+  (oracle.count_batch_mt_rows: NonSampled...java:129-161 records into Int2ShortOpenHashMap
+  restatements, ItemRowAggregator.java:26-31), plus the symmetry of every entry;
+* 1/64 (~4.2e9 pairs) and the benchmark's own workload, 1/8 of C3 (1.25e6 users, 3.36e10 pairs, what
+  bench.py times), against the closed-form restatement (oracle.row_checksums; it agrees with the
+  record-by-record one and with scipy in tests/test_oracle_semantics.py).
+
+Bar: bit-exact (every row's fingerprint, key count and count sum equal), plus the device-side
+invariants (sum of counts == sum of row sums == P, sorted rows, no zero count).  Needs an MI355X.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _threads():
+    from bench import cpu_threads
+
+    return cpu_threads()[0]
+
+
+def _device_checks(pkg, torch, up_d, it_d, M, symmetry):
+    dev = up_d.device
+    with pkg.CooccurrenceCore(n_items=M, device=dev.index or 0) as core:
+        res = core.count_device(up_d, it_d)
+        cs = torch.zeros(M, dtype=torch.int64, device=dev)
+        chk = core.verify_batch(symmetry=symmetry, row_checksum=cs)
+        torch.cuda.synchronize()
+        nnz = np.zeros(M, np.int32)
+        import ctypes
+
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(nnz.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(res.row_nnz),
+                             ctypes.c_size_t(nnz.nbytes), ctypes.c_int(2)) == 0
+        return res, chk, cs.cpu().numpy().view(np.uint64), nnz
+
+
+def _compare(res, chk, cs, nnz, want, P):
+    assert res.observed == P == want.pairs
+    assert chk["rows_bad_sum"] == 0 and chk["rows_bad_entries"] == 0
+    assert chk["sum_counts"] == chk["sum_rowsums"] == P
+    assert chk["entries"] == res.nnz == want.distinct
+    assert np.array_equal(nnz.astype(np.int64), want.nnz), "per-row key counts differ"
+    bad = np.flatnonzero(cs != want.checksum)
+    assert len(bad) == 0, f"{len(bad)} rows differ from the oracle, e.g. {bad[:10].tolist()}"
+
+
+def test_c3_256th_every_row_vs_record_by_record_oracle(pkg, oracle, torch_cuda):
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    U, M = datagen.C3_USERS // 256, datagen.C3_ITEMS
+    up, it = datagen.c3_users(0, U)
+    dev = torch.device("cuda", 0)
+    res, chk, cs, nnz = _device_checks(pkg, torch, torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev), M,
+                                       symmetry=True)
+    assert chk["asymmetric_entries"] == 0
+    want = oracle.count_batch_mt_rows(up, it, M, _threads())
+    _compare(res, chk, cs, nnz, want, datagen.ordered_pairs(up))
+
+
+@pytest.mark.parametrize("share", [64, 8])
+def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share):
+    """share = 8 is the benchmark's workload (bench.py, N = 1): users [0, 1.25e6) of the 1B log."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    U, M = datagen.C3_USERS // share, datagen.C3_ITEMS
+    dev = torch.device("cuda", 0)
+    up_d, it_d = datagen.c3_users(0, U, device=dev)
+    res, chk, cs, nnz = _device_checks(pkg, torch, up_d, it_d, M, symmetry=share >= 64)
+    if share >= 64:
+        assert chk["asymmetric_entries"] == 0
+    up, it = up_d.cpu().numpy(), it_d.cpu().numpy()
+    del up_d, it_d
+    want = oracle.row_checksums(up, it, M, _threads())
+    _compare(res, chk, cs, nnz, want, datagen.c3_ordered_pairs(0, U))

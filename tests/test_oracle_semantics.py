@@ -134,3 +134,35 @@ def test_user_cut_restatements_agree(oracle, cut):
     assert s.counters()["UserInteractionCounterObservedCooccurrences"] == obs == obs_lit
     with pytest.raises(ValueError):
         oracle.OracleStream(1000, user_cut=40000)  # a Java short
+
+
+@pytest.mark.parametrize("seed,U,M", [(4, 300, 40), (5, 2000, 5000), (6, 1, 3), (7, 0, 5)])
+def test_row_checksum_oracles_agree(oracle, seed, U, M):
+    """The per-row fingerprints (checksum, keys, count sum) of the record-by-record restatement
+    (count_batch_mt_rows), of the fast closed-form restatement (row_checksums: the benchmark's
+    exactness check at full size) and of scipy's A^T A - diag(colsum A) agree; repeats included."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 30, U)
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    it = (rng.zipf(1.3, int(up[-1])) % M).astype(np.int32)
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    want = oracle.csr_row_checks(rp, cols, data)
+    for threads in (1, 3):
+        for got in (oracle.count_batch_mt_rows(up, it, M, threads), oracle.row_checksums(up, it, M, threads)):
+            assert np.array_equal(got.checksum, want.checksum)
+            assert np.array_equal(got.nnz, want.nnz)
+            assert np.array_equal(got.rowsum, rowsums) and np.array_equal(want.rowsum, rowsums)
+            assert got.distinct == len(cols) and got.pairs == observed
+
+
+def test_row_checksum_detects_a_changed_count(oracle):
+    up = np.array([0, 3, 5], np.int64)
+    it = np.array([1, 2, 2, 1, 0], np.int32)
+    rp, cols, data, _, _ = oracle.closed_form(up, it, 3)
+    base = oracle.csr_row_checks(rp, cols, data).checksum
+    data2 = data.copy()
+    data2[0] += 1
+    assert not np.array_equal(oracle.csr_row_checks(rp, cols, data2).checksum, base)
+    cols2 = cols.copy()
+    cols2[-1] = 0 if cols2[-1] else 1
+    assert not np.array_equal(oracle.csr_row_checks(rp, cols2, data).checksum, base)
