@@ -157,7 +157,8 @@ int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cn
 int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;
-    Status s = ctx->topk_batch(topk, flags, hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->batch_stream);
+    // NULL: the context's own stream (the count it scores has already drained; see cooc.h)
+    Status s = ctx->topk_batch(topk, flags, hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream);
     return s.ok() ? COOC_OK : fail(ctx, s);
   });
 }
@@ -325,7 +326,7 @@ int cooc_partition_plan(cooc_ctx *ctx, int32_t n_parts, int64_t *h_entries) {
     if (!ctx || !h_entries) return COOC_ERR_ARG;
     if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result to partition");
     Status s = hipSetDevice(ctx->device) == hipSuccess
-                   ? ctx->sharder.plan(ctx->batch_result, ctx->cfg.n_items, n_parts, ctx->batch_stream, h_entries)
+                   ? ctx->sharder.plan(ctx->batch_result, ctx->cfg.n_items, n_parts, ctx->stream, h_entries)
                    : Status{COOC_ERR_HIP, "hipSetDevice"};
     return s.ok() ? COOC_OK : fail(ctx, s);
   });
@@ -337,7 +338,6 @@ int cooc_partition_pack(cooc_ctx *ctx, int32_t n_parts, int32_t *d_row_nnz, uint
     if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result to partition");
     (void)hipSetDevice(ctx->device);
     hipStream_t s = stream_of(ctx, hip_stream);
-    if (s != ctx->batch_stream) (void)hipStreamSynchronize(ctx->batch_stream);
     Status st = ctx->sharder.pack(ctx->batch_result, ctx->cfg.n_items, n_parts, s, d_row_nnz, d_entries);
     return st.ok() ? COOC_OK : fail(ctx, st);
   });

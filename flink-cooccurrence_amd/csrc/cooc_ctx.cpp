@@ -158,7 +158,6 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
   batch_result.nnz = nnz;
   batch_observed = r.observed;
   batch_nnz = nnz;
-  batch_stream = s;
   return Status::Ok();
 }
 
@@ -193,8 +192,8 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
   int64_t *d_rp;
   int32_t *d_col;
   uint32_t *d_cnt;
-  COOC_TRY(counter.pack(batch_stream, &d_rp, &d_col, &d_cnt));
-  COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  COOC_TRY(counter.pack(stream, &d_rp, &d_col, &d_cnt));
+  COOC_HIP_TRY(hipStreamSynchronize(stream));
   if (row_ptr) COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
   if (cols && batch_nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
   if ((cnt || cnt16) && batch_nnz) {
@@ -241,7 +240,7 @@ Status cooc_ctx::topk_batch_device(int32_t topk, int32_t flags, const int64_t *d
   COOC_HIP_TRY(hipSetDevice(device));
   const int32_t M = cfg.n_items;
   COOC_TRY(b_obs3.reserve(sizeof(int64_t) * 4));
-  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  // (the batch is complete: cooc_count_device* returned after draining its stream)
   const cooc::CountResult &r = batch_result;
   return cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense,
                                     d_rowsum_global ? d_rowsum_global : r.rowsum, (flags & COOC_FLAG_EXACT_SCORES) != 0,
@@ -255,10 +254,10 @@ Status cooc_ctx::llr(int64_t n, const int64_t *k, double *out) {
   Status st = [&]() -> Status {
     COOC_TRY(dk.reserve(sizeof(int64_t) * 4 * size_t(n)));
     COOC_TRY(dout.reserve(sizeof(double) * size_t(n)));
-    COOC_HIP_TRY(hipMemcpyAsync(dk.p, k, sizeof(int64_t) * 4 * size_t(n), hipMemcpyHostToDevice, batch_stream));
-    COOC_TRY(cooc::launch_llr(batch_stream, n, dk.as<int64_t>(), dout.as<double>()));
-    COOC_HIP_TRY(hipMemcpyAsync(out, dout.p, sizeof(double) * size_t(n), hipMemcpyDeviceToHost, batch_stream));
-    COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+    COOC_HIP_TRY(hipMemcpyAsync(dk.p, k, sizeof(int64_t) * 4 * size_t(n), hipMemcpyHostToDevice, stream));
+    COOC_TRY(cooc::launch_llr(stream, n, dk.as<int64_t>(), dout.as<double>()));
+    COOC_HIP_TRY(hipMemcpyAsync(out, dout.p, sizeof(double) * size_t(n), hipMemcpyDeviceToHost, stream));
+    COOC_HIP_TRY(hipStreamSynchronize(stream));
     return Status::Ok();
   }();
   dk.release();
@@ -272,7 +271,7 @@ Status cooc_ctx::topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *
   const int32_t M = cfg.n_items;
   for (int32_t i = 0; i < n; i++)
     if (items[i] < 0 || items[i] >= M) return Status{COOC_ERR_ARG, std::to_string(items[i]) + " is not an item"};
-  if (batch_topk != k || batch_topk_flags != (flags & COOC_FLAG_EXACT_SCORES)) COOC_TRY(topk_batch(k, flags, batch_stream));
+  if (batch_topk != k || batch_topk_flags != (flags & COOC_FLAG_EXACT_SCORES)) COOC_TRY(topk_batch(k, flags, stream));
   COOC_HIP_TRY(hipSetDevice(device));
   const size_t kk = size_t(k);
   for (int32_t i = 0; i < n; i++) {
@@ -301,7 +300,7 @@ Status cooc_ctx::verify_batch(int32_t flags, uint64_t *d_row_checksum, int64_t *
     return Status{COOC_ERR_ARG, "COOC_VERIFY_SYMMETRY needs a whole result (not one part's owned rows)"};
   COOC_HIP_TRY(hipSetDevice(device));
   COOC_TRY(b_verify.reserve(sizeof(uint64_t) * 8));
-  if (s != batch_stream) COOC_HIP_TRY(hipStreamSynchronize(batch_stream));
+  // (the batch is complete: cooc_count_device* returned after draining its stream)
   COOC_TRY(cooc::launch_verify(s, cfg.n_items, batch_result, sym && !batch_result.dense, d_row_checksum,
                                b_verify.as<unsigned long long>()));
   uint64_t h[8];

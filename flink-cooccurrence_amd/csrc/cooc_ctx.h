@@ -166,5 +166,4 @@ struct cooc_ctx {
   bool batch_owned = false;  // the last batch counted only the rows of one part (cooc_count_device_owned)
   int64_t batch_observed = 0;
   int64_t batch_nnz = 0;
-  hipStream_t batch_stream = nullptr;
 };

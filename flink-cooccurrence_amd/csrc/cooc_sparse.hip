@@ -153,10 +153,13 @@ struct SpArgs {
 // explicitly uniform so that the branches on them are scalar and no barrier sits in exec-masked code.
 __device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline int32_t uni(int32_t v) { return int32_t(__builtin_amdgcn_readfirstlane(uint32_t(v))); }
+// (readfirstlane returns an int: each half goes through uint32_t, or a low half >= 2^31 would
+// sign-extend over the high half -- output positions >= 2^31 came out negative and their rows unwritten)
 __device__ inline int64_t uni(int64_t v) {
   const uint64_t u = uint64_t(v);
-  return int64_t((uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(u >> 32))) << 32) |
-                 uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(u))));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(u >> 32)));
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(u)));
+  return int64_t((uint64_t(hi) << 32) | uint64_t(lo));
 }
 
 __device__ inline uint32_t wave_incl_scan(uint32_t v) {

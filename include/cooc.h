@@ -176,6 +176,9 @@ COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uin
  * COOC_FLAG_EXACT_SCORES to score exact counts instead of the reference's wrapped int16/int32.
  * cooc_copy_topk_batch: sizes int32[n_items], values int32[n_items*topk], scores double[n_items*topk]
  * (heap positions 1..size, least score first; rows without entries have size 0). */
+/* hip_stream NULL = the context's own stream (no caller stream is kept between calls: the count this
+ * scores has drained before cooc_count_device returned, and cooc_topk_batch synchronises the stream it
+ * runs on before returning). */
 COOC_API int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream);
 COOC_API int cooc_copy_topk_batch(cooc_ctx *ctx, int32_t *sizes, int32_t *values, double *scores);
 /* The same top-k into caller DEVICE buffers on hip_stream (ordered after the count on the caller's

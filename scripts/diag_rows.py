@@ -27,12 +27,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--sample", type=int, default=3000)
+    ap.add_argument("--lib", default=None, help="another build of libcooc_hip.so (e.g. an older one)")
     args = ap.parse_args()
     import torch
 
     import __graft_entry__
 
     pkg = __graft_entry__.load_package()
+    if args.lib:  # before the first call loads the library
+        sys.modules["flink_cooccurrence_amd._lib"].LIB_PATH = os.path.abspath(args.lib)
+        sys.modules["flink_cooccurrence_amd._lib"]._SIGS.pop("cooc_verify_batch", None)
+        sys.modules["flink_cooccurrence_amd._lib"]._SIGS.pop("cooc_copy_window_delta_range", None)
     from flink_cooccurrence_amd import datagen
 
     dev = torch.device("cuda", 0)
@@ -40,7 +45,7 @@ def main():
     up, it = datagen.c3_users(0, U, device=dev)
     core = pkg.CooccurrenceCore(n_items=M, device=0)
     res = core.count_device(up, it)
-    chk = core.verify_batch()
+    chk = core.verify_batch() if not args.lib else None
     base = d2h(res.row_base, M, np.int64)
     nnz = d2h(res.row_nnz, M, np.int32)
     rs = d2h(res.rowsum, M, np.int64)
