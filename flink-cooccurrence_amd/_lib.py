@@ -11,7 +11,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libcooc_hip.so")
+# COOC_LIB: another build of the library (A/B runs of kernel variants built next to the release one)
+LIB_PATH = os.environ.get("COOC_LIB") or os.path.join(HERE, "csrc", "libcooc_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "cooc.h")
 
 COOC_OK = 0

@@ -216,31 +216,34 @@ def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     counts = core.item_counts(items, stream=stream)  # (torch.bincount: global atomics on Zipf-hot bins)
     dist.all_reduce(counts, group=group)
     owner = snake_owner(counts, world)
-    # all-gather the histories: lengths and items, padded to the largest rank's share
+    # all-gather the histories straight into one compact CSR: every rank's lengths and items are
+    # broadcast from it into their exact place (uneven parts: no padding, no compacting copy)
     sizes = torch.tensor([n_users, n], dtype=torch.int64, device=dev)
     all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(all_sizes, sizes, group=group)
     sz = all_sizes.view(world, 2).cpu().tolist()
-    max_u, max_n = max(s[0] for s in sz), max(max(s[1] for s in sz), 1)
-    lens = torch.zeros(max_u, dtype=torch.int64, device=dev)
-    lens[:n_users] = user_ptr[1:] - user_ptr[:-1]
-    lens_all = torch.empty(world * max_u, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(lens_all, lens, group=group)
-    it_pad = torch.zeros(max_n, dtype=torch.int32, device=dev)
-    it_pad[:n] = items
-    it_all = torch.empty(world * max_n, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(it_all, it_pad, group=group)
-    lens_cat = torch.cat([lens_all[r * max_u:r * max_u + sz[r][0]] for r in range(world)])
-    items_cat = torch.cat([it_all[r * max_n:r * max_n + sz[r][1]] for r in range(world)])
-    del it_all, it_pad
-    up_all = torch.zeros(lens_cat.numel() + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(lens_cat, 0, out=up_all[1:])
-    n_all = int(items_cat.numel())
-    res = core.count_device_owned(up_all, items_cat, owner, rank, counts, n_all, stream)
+    n_users_all = sum(s_[0] for s_ in sz)
+    n_all = sum(s_[1] for s_ in sz)
+    up_all = torch.zeros(n_users_all + 1, dtype=torch.int64, device=dev)
+    it_all = torch.empty(max(n_all, 1), dtype=torch.int32, device=dev)
+    lens_all = up_all[1:]
+    uo = io = 0
+    for r in range(world):
+        ru, rn = sz[r]
+        if r == rank:
+            torch.sub(user_ptr[1:], user_ptr[:-1], out=lens_all[uo:uo + ru])
+            it_all[io:io + rn] = items
+        if ru:
+            dist.broadcast(lens_all[uo:uo + ru], src=dist.get_global_rank(group, r) if group else r, group=group)
+        if rn:
+            dist.broadcast(it_all[io:io + rn], src=dist.get_global_rank(group, r) if group else r, group=group)
+        uo, io = uo + ru, io + rn
+    lens_all.cumsum_(0)  # lengths -> offsets, in place (up_all[0] == 0)
+    res = core.count_device_owned(up_all, it_all, owner, rank, counts, n_all, stream)
     obs = torch.tensor([res.observed], dtype=torch.int64, device=dev)
     dist.all_reduce(obs, group=group)
-    return OwnedResult(rank, world, res, owner, int(obs.item()), int(res.observed), int(lens_cat.numel()), n_all,
-                       4 * (n_all - n) + 8 * (int(lens_cat.numel()) - n_users))
+    return OwnedResult(rank, world, res, owner, int(obs.item()), int(res.observed), n_users_all, n_all,
+                       4 * (n_all - n) + 8 * (n_users_all - n_users))
 
 
 @dataclass
