@@ -46,9 +46,9 @@ class StreamState {
   Status pack_delta(cooc_ctx &ctx);
   Status copy_entries(int64_t e0, int64_t e1, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
   Status grow_arena(cooc_ctx &ctx, int64_t need);
-  // n_items > Counter::kMaxGeneralItems: the window's delta rows as C(full histories) - C(histories
-  // before the window) of its users, both counted by the large-universe planner
-  Status count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int32_t> &act_old,
+  // n_items >= 40,320: one window through the large-universe planner, old / new positions in one pass
+  Status count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int64_t> &act_off,
+                            const std::vector<int32_t> &act_len, const std::vector<int32_t> &act_old,
                             int64_t n_full, CountResult *r);
 
   // host metadata of the per-user histories
@@ -69,8 +69,8 @@ class StreamState {
   std::vector<std::vector<int32_t>> staged_items_;  // reused across windows
   // device uploads of one window
   DevBuf d_act_off_, d_act_len_, d_act_old_, d_cbase_, d_new_items_, d_new_dst_ptr_, d_new_dst_, d_reloc_;
-  // large-universe windows: contiguous full / old histories, the full histories' packed result
-  DevBuf d_lw_items_, d_lw_oldptr_, d_lw_rp_, d_lw_col_, d_lw_cnt_, d_lw_rs_;
+  // large-universe windows: the users' whole histories and new items side by side (2 lists per user)
+  DevBuf d_lw_items_, d_lw_up2_, d_lw_dsta_, d_lw_dstb_, d_lw_srcb_, d_lw_lenb_;
   // global state
   bool global_ready_ = false;
   bool sparse_global_ = false;  // n_items >= 40,320: sorted row slabs (gs_) instead of the dense matrix

@@ -99,6 +99,18 @@ struct PlanTotals {
   int64_t n_gather_rows;  // whole rows in gather mode (their work items get bucket-start slots)
   int64_t n_gather;       // bucket-start slots handed out by the queue builder
   int64_t bad_row;        // a row whose counts failed the row-sum check (err bit 1), for the message
+  int64_t self_total;     // contributions whose walk includes their own position (pairs p == p removed)
+};
+
+// One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR
+// handed to run_sparse holds 2 lists per user, A_j = the history after the window and B_j = the window's
+// new items; a new position of A_j walks A_j, an old one walks B_j (k_sp_window_contribs).  All device
+// pointers; n_contrib = sum of the |A_j| = cbase[n_users] (host copy).
+struct SparseWindow {
+  int64_t n_users = 0;
+  const int32_t *old = nullptr;    // [n_users] history length before the window
+  const int64_t *cbase = nullptr;  // [n_users + 1] exclusive prefix of |A_j|
+  int64_t n_contrib = 0;
 };
 
 // Result of a run: padded CSR over all M rows, device pointers owned by the Counter.
@@ -145,7 +157,8 @@ class Counter {
   // the global log's item counts); other rows come out empty.
   Status run_sparse(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                     CountResult *out, KernelTimer *timer = nullptr, const int32_t *owner = nullptr,
-                    int32_t part = 0, const int64_t *freq = nullptr, int64_t n_freq = 0);
+                    int32_t part = 0, const int64_t *freq = nullptr, int64_t n_freq = 0,
+                    const SparseWindow *win = nullptr);
   bool sparse() const { return M_ >= kBatchMaxItems; }
   // run() (the streaming general planner) keeps one LDS row per chunk: n_items <= kMaxGeneralItems
   static constexpr int32_t kMaxGeneralItems = 40704;
@@ -177,14 +190,6 @@ class Counter {
 
   // Pack the result of the last run into contiguous CSR (device), for copy-out.
   Status pack(hipStream_t stream, int64_t **row_ptr, int32_t **col, uint32_t **cnt);
-  // Streaming windows over large universes: the last result becomes the difference of two packed
-  // CSRs over all rows (f: the window's users' full histories, o: their histories before the window;
-  // o's keys are a subset of f's), entries whose difference is 0 dropped, rowsum = f_rs - o_rs (o_rs
-  // may be this counter's own last_rowsum()).  Afterwards pack / last_* / read_totals see it.
-  Status adopt_difference(hipStream_t stream, const int64_t *f_rp, const int32_t *f_col, const uint32_t *f_cnt,
-                          const int64_t *f_rs, const int64_t *o_rp, const int32_t *o_col, const uint32_t *o_cnt,
-                          const int64_t *o_rs, CountResult *out);
-
   // Copy the device totals of the last run (the stream must have drained).
   Status read_totals(PlanTotals *t);
   const int64_t *last_rowsum() const { return rowsum_.as<int64_t>(); }
@@ -223,6 +228,7 @@ class Counter {
   DevBuf dense_, send_, witems_;
   // large-universe path: tile-grouped arena, tile starts, per-row work and plan, estimates, queue
   DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_, sp_pbase_, sp_scr_, sp_hz_;
+  DevBuf sp_spre_;  // streaming windows: prefix of the contributions' self flags
   bool general_only_ = false;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
   static constexpr int64_t chunk_work_ = int64_t(1) << 22;  // pairs per chunk of the batch planner

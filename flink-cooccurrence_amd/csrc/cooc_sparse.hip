@@ -142,6 +142,7 @@ struct SpArgs {
   uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
   int64_t scr_cap;          // 0: gather mode off
   const int64_t *rowsum;    // [M] closed-form row sums W_a - c_a (k_sp_plan): every whole row is checked
+  const int64_t *spre;      // streaming window: [n_contrib + 1] prefix of the kSelfBit flags; NULL: all set
 };
 
 #ifdef COOC_SP_TRACE
@@ -260,8 +261,10 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
       }
       atomicAdd(&c[it >> kTShift], 1);
       if (!owner) {
-        keys[s + p] = uint32_t(it);
-        vals[s + p] = uint32_t(j);
+        if (keys) {  // (NULL: the contributions come from elsewhere, k_sp_window_contribs)
+          keys[s + p] = uint32_t(it);
+          vals[s + p] = uint32_t(j);
+        }
       } else {
         mine += owner[it] == part;
       }
@@ -302,6 +305,11 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
 // tb[j][t] = the absolute 16-B group index of tile t's segment (tb[j][T] = the end of j's list), so
 // that a walk needs one descriptor line per user.
 constexpr uint32_t kSink = 0xFFFFFFFFu;
+// A contribution's value: the index of the list its row walks; in a streaming window (spre != NULL) with
+// kSelfBit when the walk includes the contribution's own position (a new position walks its user's whole
+// history, an old one only the window's new items, see k_sp_window_contribs).  In a one-window batch every
+// walk includes it (no bit: the self count of a row is its contribution count).
+constexpr uint32_t kSelfBit = 0x80000000u, kListMask = 0x7FFFFFFFu;
 __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__restrict__ up,
                                                     const int32_t *__restrict__ items, int32_t M, int32_t T,
                                                     const int64_t *__restrict__ pbase, int32_t *__restrict__ tb,
@@ -366,6 +374,30 @@ __global__ __launch_bounds__(256) void k_sp_owned_contribs(int64_t U, const int6
   }
 }
 
+// Streaming window (old / new positions, NonSampled...java:129-161): user j's two lists are A_j (the whole
+// history after the window, at up2[2j]) and B_j (its new items, positions >= old[j], at up2[2j + 1]).
+// Position p of A_j is a contribution of row x_p: a new position (p >= old[j]) walks A_j (every pair with
+// it as the later one, the pair with itself removed: kSelfBit), an old one walks B_j (its pairs with the
+// window's items).  Contribution p of user j lands at cbase[j] + p.  One wave per user.
+__global__ __launch_bounds__(256) void k_sp_window_contribs(int64_t U, const int64_t *__restrict__ up2,
+                                                           const int32_t *__restrict__ items,
+                                                           const int32_t *__restrict__ old,
+                                                           const int64_t *__restrict__ cbase,
+                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up2[2 * j];
+    const int32_t n = int32_t(up2[2 * j + 1] - s), o = old[j];
+    const int64_t c = cbase[j];
+    for (int32_t p = lane; p < n; p += 64) {
+      keys[c + p] = uint32_t(items[s + p]);
+      vals[c + p] = p >= o ? (uint32_t(2 * j) | kSelfBit) : uint32_t(2 * j + 1);
+    }
+  }
+}
+
 struct WidenCount {
   __host__ __device__ int64_t operator()(int32_t v) const { return int64_t(v); }
 };
@@ -381,9 +413,13 @@ __global__ void k_sp_row_ptr(const uint32_t *__restrict__ keys, int64_t n, int32
   row_ptr[a] = lo;
 }
 
-struct UserLen {  // list length of a contribution's user
+struct UserLen {  // list length of a contribution's list
   const int64_t *up;
-  __host__ __device__ int64_t operator()(uint32_t u) const { return up[u + 1] - up[u]; }
+  __host__ __device__ int64_t operator()(uint32_t u) const { return up[(u & kListMask) + 1] - up[u & kListMask]; }
+};
+
+struct SelfFlag {  // 1 for a contribution whose walk includes its own position
+  __host__ __device__ int64_t operator()(uint32_t u) const { return int64_t(u >> 31); }
 };
 
 // est[t][k] = sum over the columns b of tile t of 1 - exp(-2^(k/2) f_b / N); gmass[t] = tile t's
@@ -427,14 +463,15 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
                                                  uint64_t *__restrict__ skey,
                                                  int32_t *__restrict__ order, int32_t *__restrict__ nwork,
                                                  int32_t *__restrict__ row_nnz, int64_t *__restrict__ row_base,
-                                                 PlanTotals *__restrict__ tot) {
+                                                 PlanTotals *__restrict__ tot, const int64_t *__restrict__ spre) {
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
-    rowsum[a] = W - c;
+    const int64_t self = spre ? spre[k0 + c] - spre[k0] : c;  // pairs of a position with itself
+    rowsum[a] = W - self;
     row_w[a] = W;
     row_nnz[a] = 0;
     row_base[a] = 0;
@@ -444,7 +481,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     int32_t nw = 0;
     if (c > 0) {
       n_active = 1;
-      bound = uint64_t(min<int64_t>(W - c, M));
+      bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
         n_split = 1;
@@ -582,10 +619,11 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
   }
 }
 
-__global__ void k_sp_totals(PlanTotals *__restrict__ tot, const int64_t *__restrict__ epre, int64_t n,
-                            int32_t *__restrict__ qctr) {
+__global__ void k_sp_totals(PlanTotals *__restrict__ tot, const int64_t *__restrict__ epre,
+                            const int64_t *__restrict__ spre, int64_t n, int32_t *__restrict__ qctr) {
   tot->n_chunks = tot->n_split_work + (tot->n_active - tot->n_split);
   tot->work_total = epre[n];
+  tot->self_total = spre ? spre[n] : n;
   qctr[0] = 0;
 }
 
@@ -899,7 +937,7 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
     int64_t start = 0;
     STAT_ADD(19, op.mode == 1 ? 1 : 0);
     if (tid < nb) {  // the segment of tiles [t0, t1) (full: the whole list) in 16-B groups
-      const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] : 0u;
+      const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] & kListMask : 0u;
       const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
       const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
       const int32_t s0 = okt ? tbu[full ? 0 : t0] : 0;
@@ -1287,7 +1325,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         __syncthreads();  // every wave has read the flags before the retry resets them
         continue;
       }
-      const uint32_t self = uint32_t(k1 - k0);  // the -1 at column a per contribution (whole rows)
+      // the -1 at column a per contribution whose walk includes its own position (whole rows)
+      const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
       if (split) {
         uint32_t *dst = A.staging + int64_t(A.split_slot[a]) * A.sstride + c0;
         for (int32_t i = tid; i < c1 - c0; i += kSpThreads) {
@@ -1367,14 +1406,15 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
                                                                     unsigned long long *__restrict__ bump, int64_t cap,
                                                                     int64_t *__restrict__ row_base,
                                                                     int32_t *__restrict__ row_nnz,
-                                                                    PlanTotals *__restrict__ tot) {
+                                                                    PlanTotals *__restrict__ tot,
+                                                                    const int64_t *__restrict__ spre) {
   __shared__ uint32_t s_w[kFinWaves];
   __shared__ uint64_t s_red[kFinWaves];
   __shared__ int64_t s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t s = blockIdx.x;
   const int32_t a = split_row[s];
-  const uint32_t self = uint32_t(row_ptr[a + 1] - row_ptr[a]);
+  const uint32_t self = uint32_t(spre ? spre[row_ptr[a + 1]] - spre[row_ptr[a]] : row_ptr[a + 1] - row_ptr[a]);
   const uint32_t *row = staging + int64_t(s) * stride;
   constexpr int32_t kStep = 64 * 4 * kFinU;  // columns per wave step
   const int32_t per = ((M + kFinWaves - 1) / kFinWaves + kStep - 1) / kStep * kStep;
@@ -1488,60 +1528,6 @@ int bits_for(int64_t v) {
 }  // namespace
 
 namespace {
-__device__ inline int64_t lb_i32(const int32_t *__restrict__ c, int64_t n, int32_t x) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (c[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// Row a of f minus row a of o (one wave per row): pass 0 counts the non-zero differences into nnz[a],
-// pass 1 writes them at base[a] in column order.
-template <int PASS>
-__global__ __launch_bounds__(256) void k_diff_rows(int32_t M, const int64_t *__restrict__ f_rp,
-                                                   const int32_t *__restrict__ f_col, const uint32_t *__restrict__ f_cnt,
-                                                   const int64_t *__restrict__ o_rp, const int32_t *__restrict__ o_col,
-                                                   const uint32_t *__restrict__ o_cnt, int32_t *__restrict__ nnz,
-                                                   const int64_t *__restrict__ base, int32_t *__restrict__ col_out,
-                                                   uint32_t *__restrict__ cnt_out) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
-    const int64_t f0 = f_rp[a], nf = f_rp[a + 1] - f0, o0 = o_rp[a], no = o_rp[a + 1] - o0;
-    int64_t k = PASS ? base[a] : 0;
-    for (int64_t i0 = 0; i0 < nf; i0 += 64) {
-      uint32_t d = 0u;
-      int32_t c = 0;
-      if (i0 + lane < nf) {
-        c = f_col[f0 + i0 + lane];
-        const int64_t p = lb_i32(o_col + o0, no, c);
-        d = f_cnt[f0 + i0 + lane] - ((p < no && o_col[o0 + p] == c) ? o_cnt[o0 + p] : 0u);
-      }
-      const uint64_t m = __ballot(d != 0u);
-      if (PASS && d) {
-        const int64_t pos = k + __popcll(m & lt);
-        col_out[pos] = c;
-        cnt_out[pos] = d;
-      }
-      k += __popcll(m);
-    }
-    if (!PASS && lane == 0) nnz[a] = int32_t(k);
-  }
-}
-
-__global__ void k_diff_rowsum(int32_t M, const int64_t *__restrict__ f_rs, const int64_t *__restrict__ o_rs,
-                              int64_t *__restrict__ out) {
-  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a < M) out[a] = f_rs[a] - o_rs[a];
-}
-
-__global__ void k_set_nnz_total(PlanTotals *__restrict__ tot, const int64_t *__restrict__ base, int32_t M) {
-  tot->nnz_total = base[M];
-  tot->err = 0;
-}
 
 // Item frequencies of a log (the multi-GPU owner map and the planner's column estimate): ids below
 // kHistLds are counted in LDS (Zipf ranks: the hot ids; no contended global atomics), the rest with
@@ -1579,51 +1565,9 @@ Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_
   return Status::Ok();
 }
 
-Status Counter::adopt_difference(hipStream_t s, const int64_t *f_rp, const int32_t *f_col, const uint32_t *f_cnt,
-                                 const int64_t *f_rs, const int64_t *o_rp, const int32_t *o_col, const uint32_t *o_cnt,
-                                 const int64_t *o_rs, CountResult *out) {
-  const int32_t M = M_;
-  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
-  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
-  const unsigned gw = unsigned(std::min<int64_t>((int64_t(M) * 64 + 255) / 256, 8192));
-  k_diff_rows<0><<<gw, 256, 0, s>>>(M, f_rp, f_col, f_cnt, o_rp, o_col, o_cnt, row_nnz_.as<int32_t>(), nullptr, nullptr,
-                                    nullptr);
-  int64_t *base = row_base_.as<int64_t>();
-  hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> n64(row_nnz_.as<int32_t>(), WidenCount{});
-  size_t b = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, n64, base + 1, M, s));
-  COOC_TRY(sort_tmp_.reserve(b));
-  b = sort_tmp_.cap;
-  COOC_HIP_TRY(hipMemsetAsync(base, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, n64, base + 1, M, s));
-  int64_t nnz = 0;
-  COOC_HIP_TRY(hipMemcpyAsync(&nnz, base + M, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  COOC_HIP_TRY(hipStreamSynchronize(s));
-  COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(nnz + 1)));
-  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * size_t(nnz + 1)));
-  k_diff_rows<1><<<gw, 256, 0, s>>>(M, f_rp, f_col, f_cnt, o_rp, o_col, o_cnt, nullptr, base, col_.as<int32_t>(),
-                                    cnt_.as<uint32_t>());
-  k_diff_rowsum<<<nblocks(M, 256), 256, 0, s>>>(M, f_rs, o_rs, rowsum_.as<int64_t>());
-  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
-  k_set_nnz_total<<<1, 1, 0, s>>>(tot_.as<PlanTotals>(), base, M);
-  COOC_HIP_TRY(hipGetLastError());
-  dense_mode_ = false;
-  vec_ = false;
-  last_rows_ = M;
-  out->row_base = base;
-  out->row_nnz = row_nnz_.as<int32_t>();
-  out->col = col_.as<int32_t>();
-  out->cnt = cnt_.as<uint32_t>();
-  out->dense = nullptr;
-  out->rowsum = rowsum_.as<int64_t>();
-  out->nnz = nnz;
-  return Status::Ok();
-}
-
 Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, int64_t n, hipStream_t s,
                            CountResult *out, KernelTimer *timer, const int32_t *owner, int32_t part,
-                           const int64_t *freq, int64_t n_freq) {
+                           const int64_t *freq, int64_t n_freq, const SparseWindow *win) {
   const int32_t M = M_;
   const int32_t T = int32_t((int64_t(M) + kTW - 1) / kTW);
   if (T > kSpMaxTiles)
@@ -1690,8 +1634,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
   }
   if (U > 0) {
-    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, sp_tb_.as<int32_t>(), keys_in,
-                                                           vals_in, owner, part, sp_ownc_.as<int32_t>(), tot);
+    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, sp_tb_.as<int32_t>(),
+                                                           win ? nullptr : keys_in, vals_in, owner, part,
+                                                           sp_ownc_.as<int32_t>(), tot);
     COOC_HIP_TRY(hipGetLastError());
   }
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(int64_t), s));
@@ -1702,7 +1647,14 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                                          sp_arena_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
-  int64_t n_c = n;  // contributions: every interaction, or those of the owned rows
+  int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
+  if (win) {
+    n_c = win->n_contrib;
+    if (win->n_users > 0)
+      k_sp_window_contribs<<<nblocks(std::min<int64_t>(win->n_users, 65536) * 64, 256), 256, 0, s>>>(
+          win->n_users, up, items, win->old, win->cbase, keys_in, vals_in);
+    COOC_HIP_TRY(hipGetLastError());
+  }
   if (owner) {
     int64_t *ownoff = sp_ownoff_.as<int64_t>();
     COOC_HIP_TRY(hipMemsetAsync(ownoff, 0, sizeof(int64_t), s));
@@ -1728,11 +1680,25 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, len_it, epre + 1, int(n_c), s));
   }
+  int64_t *spre = nullptr;  // a window's self flags, prefix in row order
+  if (win) {
+    COOC_TRY(sp_spre_.reserve(sizeof(int64_t) * size_t(n_c + 2)));
+    spre = sp_spre_.as<int64_t>();
+    COOC_HIP_TRY(hipMemsetAsync(spre, 0, sizeof(int64_t), s));
+    if (n_c > 0) {
+      hipcub::TransformInputIterator<int64_t, SelfFlag, const uint32_t *> sf(vals, SelfFlag{});
+      size_t b = 0;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, sf, spre + 1, int(n_c), s));
+      COOC_TRY(sort_tmp_.reserve(b));
+      b = sort_tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, sf, spre + 1, int(n_c), s));
+    }
+  }
   SPT("sort+scan");
   k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n_c, M, row_ptr);
   // 5. expected distinct keys per tile; 6. per-row plan
   // column frequencies: of this log's interactions (owner == NULL), else the caller's global counts
-  const int64_t n_est = freq ? n_freq : n;
+  const int64_t n_est = freq ? n_freq : win ? n_c : n;
   if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, freq, M, n_est, est, gmass);
   else COOC_HIP_TRY(hipMemsetAsync(est, 0, sizeof(float) * (T * kEstK + T), s));
   SPT("est");
@@ -1741,15 +1707,15 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                             sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
                                             order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
-                                            row_base_.as<int64_t>(), tot);
-  k_sp_totals<<<1, 1, 0, s>>>(tot, epre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
+                                            row_base_.as<int64_t>(), tot, spre);
+  k_sp_totals<<<1, 1, 0, s>>>(tot, epre, spre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
   const int64_t n_split = h_tot_->n_split;
   const int64_t n_work = h_tot_->n_chunks;
-  const int64_t work_total = h_tot_->work_total;
+  const int64_t work_total = h_tot_->work_total, self_total = h_tot_->self_total;
   const int64_t bound = h_tot_->cap_total, est_nnz = h_tot_->est_nnz;
 
   SPT("plan+sync");
@@ -1846,6 +1812,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   proto.rowsum = rowsum_.as<int64_t>();
+  proto.spre = spre;
   int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
@@ -1908,7 +1875,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       k_sp_split_finalize<<<unsigned(n_split), kFinThreads, 0, s>>>(
           split_row_.as<int32_t>(), staging_.as<uint32_t>(), sstride, M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
           cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-          tot);
+          tot, spre);
       COOC_HIP_TRY(hipGetLastError());
     }
   SPT("finalize");
@@ -1955,7 +1922,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   out->dense = nullptr;
   out->rowsum = rowsum_.as<int64_t>();
   out->work = work_total;
-  out->observed = work_total - n_c;  // ordered pairs of the counted rows
+  out->observed = work_total - self_total;  // ordered pairs of the counted rows
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
   return Status::Ok();
 }

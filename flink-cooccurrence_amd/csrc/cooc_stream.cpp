@@ -60,8 +60,8 @@ void StreamState::release() {
   DevBuf *all[] = {&arena_,      &d_act_off_,      &d_act_len_,     &d_act_old_,   &d_cbase_,
                    &d_new_items_, &d_new_dst_ptr_, &d_new_dst_,     &d_reloc_,     &d_global_,
                    &d_grs_,       &d_touched_,     &d_scan_tmp_,    &d_scal_,      &d_topk_val_,
-                   &d_topk_score_, &d_topk_size_, &d_llr_terms_, &d_lw_items_, &d_lw_oldptr_,
-                   &d_lw_rp_,     &d_lw_col_,      &d_lw_cnt_,      &d_lw_rs_};
+                   &d_topk_score_, &d_topk_size_, &d_llr_terms_, &d_lw_items_, &d_lw_up2_,
+                   &d_lw_dsta_,   &d_lw_dstb_,     &d_lw_srcb_,     &d_lw_lenb_};
   for (DevBuf *b : all) b->release();
   gs_.release();
   global_ready_ = false;
@@ -272,10 +272,10 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   tr.mark("upload_append", s);
   if (ctx.counter.batch_ok())  // n_items < 40,320: the batch planner + k_acc_batch
     COOC_TRY(ctx.counter.run_window(au, s, &r));
-  else if (M <= Counter::kMaxGeneralItems)
+  else if (!ctx.counter.sparse())  // COOC_FLAG_GENERAL_PLANNER (A/B of the batch planner)
     COOC_TRY(ctx.counter.run(au, s, &r));
-  else
-    COOC_TRY(count_large_window(ctx, s, n_act, act_old, cbase[n_act], &r));
+  else  // n_items >= 40,320: the large-universe planner, old / new positions in one pass
+    COOC_TRY(count_large_window(ctx, s, n_act, act_off, act_len, act_old, cbase[n_act], &r));
   tr.mark("count", s);
 
   // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
@@ -342,51 +342,42 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   return Status::Ok();
 }
 
-Status StreamState::count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int32_t> &act_old,
+Status StreamState::count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int64_t> &act_off,
+                                      const std::vector<int32_t> &act_len, const std::vector<int32_t> &act_old,
                                       int64_t n_full, CountResult *r) {
-  const int32_t M = ctx.cfg.n_items;
-  // every pair whose later position is new = C(full lists) - C(lists before the window), per user
-  std::vector<int64_t> old_ptr(n_act + 1, 0);
-  for (int64_t j = 0; j < n_act; j++) old_ptr[j + 1] = old_ptr[j] + act_old[j];
-  const int64_t n_old = old_ptr[n_act];
-  COOC_TRY(upload(d_lw_oldptr_, old_ptr, s));
-  COOC_TRY(d_lw_items_.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(n_full, 1))));
-  int32_t *lists = d_lw_items_.as<int32_t>();
-  // 1. the full histories (contiguous) -> counts, packed and kept
-  COOC_TRY(launch_gather_lists(s, n_act, d_act_off_.as<int64_t>(), d_act_len_.as<int32_t>(), d_cbase_.as<int64_t>(),
-                               arena_.as<int32_t>(), lists));
-  CountResult rf;
-  COOC_TRY(ctx.counter.run_sparse(n_act, d_cbase_.as<int64_t>(), lists, n_full, s, &rf, nullptr));
-  PlanTotals t;
-  COOC_HIP_TRY(hipStreamSynchronize(s));
-  COOC_TRY(ctx.counter.read_totals(&t));
-  if (t.err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
-  int64_t *rp;
-  int32_t *col;
-  uint32_t *cnt;
-  COOC_TRY(ctx.counter.pack(s, &rp, &col, &cnt));
-  const int64_t nnz_f = t.nnz_total;
-  COOC_TRY(d_lw_rp_.reserve(sizeof(int64_t) * size_t(M + 1)));
-  COOC_TRY(d_lw_col_.reserve(sizeof(int32_t) * size_t(nnz_f + 1)));
-  COOC_TRY(d_lw_cnt_.reserve(sizeof(uint32_t) * size_t(nnz_f + 1)));
-  COOC_TRY(d_lw_rs_.reserve(sizeof(int64_t) * size_t(M)));
-  COOC_HIP_TRY(hipMemcpyAsync(d_lw_rp_.p, rp, sizeof(int64_t) * size_t(M + 1), hipMemcpyDeviceToDevice, s));
-  if (nnz_f) {
-    COOC_HIP_TRY(hipMemcpyAsync(d_lw_col_.p, col, sizeof(int32_t) * size_t(nnz_f), hipMemcpyDeviceToDevice, s));
-    COOC_HIP_TRY(hipMemcpyAsync(d_lw_cnt_.p, cnt, sizeof(uint32_t) * size_t(nnz_f), hipMemcpyDeviceToDevice, s));
+  // every pair whose later position is new (NonSampled...java:129-161), in one pass: user j's lists A_j
+  // (its whole history) and B_j (the window's items, the tail of A_j) side by side; a new position
+  // walks A_j, an old one B_j (run_sparse's SparseWindow, k_sp_window_contribs): 2 new |A_j| pair work
+  // per user instead of |A_j|^2 + |old|^2
+  std::vector<int64_t> up2(2 * n_act + 1), dst_a(n_act), dst_b(n_act), src_b(n_act);
+  std::vector<int32_t> len_b(n_act);
+  int64_t o = 0;
+  for (int64_t j = 0; j < n_act; j++) {
+    up2[2 * j] = dst_a[j] = o;
+    o += act_len[j];
+    up2[2 * j + 1] = dst_b[j] = o;
+    src_b[j] = act_off[j] + act_old[j];
+    len_b[j] = act_len[j] - act_old[j];
+    o += len_b[j];
   }
-  COOC_HIP_TRY(hipMemcpyAsync(d_lw_rs_.p, ctx.counter.last_rowsum(), sizeof(int64_t) * size_t(M), hipMemcpyDeviceToDevice, s));
-  // 2. the histories before the window -> counts, packed
-  COOC_TRY(launch_gather_lists(s, n_act, d_act_off_.as<int64_t>(), d_act_old_.as<int32_t>(), d_lw_oldptr_.as<int64_t>(),
+  up2[2 * n_act] = o;
+  COOC_TRY(upload(d_lw_up2_, up2, s));
+  COOC_TRY(upload(d_lw_dsta_, dst_a, s));
+  COOC_TRY(upload(d_lw_dstb_, dst_b, s));
+  COOC_TRY(upload(d_lw_srcb_, src_b, s));
+  COOC_TRY(upload(d_lw_lenb_, len_b, s));
+  COOC_TRY(d_lw_items_.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(o, 1))));
+  int32_t *lists = d_lw_items_.as<int32_t>();
+  COOC_TRY(launch_gather_lists(s, n_act, d_act_off_.as<int64_t>(), d_act_len_.as<int32_t>(), d_lw_dsta_.as<int64_t>(),
                                arena_.as<int32_t>(), lists));
-  CountResult ro;
-  COOC_TRY(ctx.counter.run_sparse(n_act, d_lw_oldptr_.as<int64_t>(), lists, n_old, s, &ro, nullptr));
-  COOC_TRY(ctx.counter.pack(s, &rp, &col, &cnt));
-  // 3. the difference becomes the counter's last result (the delta rows and row-sum deltas)
-  COOC_TRY(ctx.counter.adopt_difference(s, d_lw_rp_.as<int64_t>(), d_lw_col_.as<int32_t>(), d_lw_cnt_.as<uint32_t>(),
-                                        d_lw_rs_.as<int64_t>(), rp, col, cnt, ctx.counter.last_rowsum(), r));
-  r->observed = rf.observed - ro.observed;
-  return Status::Ok();
+  COOC_TRY(launch_gather_lists(s, n_act, d_lw_srcb_.as<int64_t>(), d_lw_lenb_.as<int32_t>(), d_lw_dstb_.as<int64_t>(),
+                               arena_.as<int32_t>(), lists));
+  SparseWindow w;
+  w.n_users = n_act;
+  w.old = d_act_old_.as<int32_t>();
+  w.cbase = d_cbase_.as<int64_t>();
+  w.n_contrib = n_full;
+  return ctx.counter.run_sparse(2 * n_act, d_lw_up2_.as<int64_t>(), lists, o, s, r, nullptr, nullptr, 0, nullptr, 0, &w);
 }
 
 Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,

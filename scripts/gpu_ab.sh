@@ -7,9 +7,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 V=${V:?variant}
 K=${AB_TESTS:-"sparse or exactness"}
+if [ "$K" != "none" ]; then
 COOC_LIB=flink-cooccurrence_amd/csrc/libcooc_hip_$V.so timeout -k 10 900 python -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_exactness.py \
   -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > gpurun_out/ab_pytest_$V.log 2>&1
 rc=$?; echo "variant $V tests rc=$rc"; tail -3 gpurun_out/ab_pytest_$V.log; [ $rc -eq 0 ] || exit $rc
+fi
 for lib in release $V release $V; do
   L=flink-cooccurrence_amd/csrc/libcooc_hip_$lib.so; [ $lib = release ] && L=flink-cooccurrence_amd/csrc/libcooc_hip.so
   timeout -k 10 300 python -u scripts/bench_c3.py --steps ${STEPS:-3} --lib $L > gpurun_out/ab_$lib.json 2> gpurun_out/ab_$lib.err
