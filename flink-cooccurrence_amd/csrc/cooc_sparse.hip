@@ -69,17 +69,10 @@ constexpr int kSpWaves = kSpThreads / 64;
 constexpr int kTShift = COOC_SP_TSHIFT;
 constexpr int kTW = 1 << kTShift;  // dense tile width (16384: 64 KB of uint32 LDS counters)
 constexpr int kSpMaxTiles = 64;                        // per-row plans are 64-bit tile masks
-constexpr int kHashMax = 8192;                        // slots: packed (key, count) words, the dense tile's first 32 KB
-constexpr int kStage = kTW - kHashMax;                 // hash chunks stage their partner ids in the rest (8192 ids)
-#ifndef COOC_SP_INS_U
-#define COOC_SP_INS_U 8
-#endif
-constexpr int kInsU = COOC_SP_INS_U;                   // staged ids inserted per thread at once (their probes overlap)
-constexpr uint32_t kCntBits = 12;                      // a slot: (column offset + 1) << 12 | count (< 4096)
-constexpr uint32_t kCntMask = (1u << kCntBits) - 1u;
+constexpr int kHashMax = 8192;                        // slots: keys + counts = the dense tile's 128 KB
 constexpr int kHashMin = 1024;                         // one slot per thread at least
-constexpr int kHashMaxTiles = (1 << 20) / kTW - 1;      // a hash chunk spans < 2^20 columns (20-bit keys) ...
-constexpr int kL1Words = (1 << 20) / 1024;             // ... so its block bitmap is <= 1024 words
+constexpr int kHashMaxTiles = (1 << 20) / kTW;          // a hash chunk spans <= 2^20 columns ...
+constexpr int kL1Words = kHashMaxTiles * kTW / 1024;   // ... so its block bitmap is <= 1024 words
 constexpr int kSpDb = 512;                             // contribution descriptors per batch
 constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
 constexpr int kSpU = 4;                                // partner loads in flight per lane
@@ -649,63 +642,48 @@ struct SpStatic {
   uint32_t bcur[kSpMaxTiles];       // ... and fill cursors
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
   unsigned long long rsum;          // the current whole row's compacted counts, summed (row-sum check)
-  uint32_t nst[2];                  // hash chunks: staged ids of the current / next round
-  uint32_t cflag;                   // hash chunks: a count reached 2^12 - 1 (the chunk is redone as dense tiles)
 #ifdef COOC_SP_STATS
   unsigned long long st[28];
 #endif
 };
 
-// Insert the n staged partner ids (st[0, n): absolute columns of the chunk [c0, c1)) into the LDS table
-// of packed slots (column offset + 1) << 12 | count, 0 = empty -- the Int2ShortOpenHashMap of
-// ItemRowAggregator.java:21-31 in LDS, with an exact 12-bit count.  Every thread takes kInsU ids at a time
-// and probes them in lockstep, so that their LDS round trips overlap: a returning compare-and-swap
-// claims an empty slot with count 1 or returns the word that holds it; on the same key a count add
-// follows (its returned value is only checked after the round).  A count that reaches 2^12 - 1 raises
-// cflag (the chunk is redone as dense tiles); an id that finds no slot within kMaxProbe probes raises
-// flag (the chunk is redone with a 4x table).
-__device__ inline void sp_hash_insert_staged(const SpShared &L, SpStatic &S_, uint32_t n, uint32_t c0, uint32_t hshift,
-                                             uint32_t hmask) {
-  uint32_t *tab = L.R;
-  const uint32_t *st = L.R + kHashMax;
-  const uint32_t tid = threadIdx.x;
-  bool probe_ovf = false, cnt_ovf = false;
-  for (uint32_t b0 = 0; b0 < n; b0 += uint32_t(kSpThreads * kInsU)) {
-    uint32_t key[kInsU], h[kInsU], added[kInsU];
+// Insert the (up to 4) partner ids of one 16-B group into the LDS table (keys store id + 1; 0 =
+// empty), linear probing from a multiplicative hash.  The ids are probed in lockstep so that their
+// LDS round trips overlap; each probe is one returning compare-and-swap (it claims an empty slot or
+// returns the key that holds it) followed, on a hit, by a non-returning count add.  An id that finds
+// no slot within kMaxProbe probes raises the overflow flag (the chunk is redone with a larger table);
+// the planner sizes tables at <= 1/2 fill, so probe chains stay short.
+__device__ inline void sp_hash_insert4(uint32_t *keys, uint32_t *cnts, const uint4 &v, uint32_t hshift, uint32_t hmask,
+                                       SpStatic &S_) {
+  uint32_t k[4] = {v.x + 1u, v.y + 1u, v.z + 1u, v.w + 1u};  // kSink + 1 == 0: a pad is never inserted
+  uint32_t h[4];
 #pragma unroll
-    for (int i = 0; i < kInsU; i++) {
-      const uint32_t j = b0 + tid + uint32_t(i * kSpThreads);
-      const uint32_t off = j < n ? st[j] - c0 : 0u;
-      key[i] = j < n ? (off + 1u) << kCntBits : 0u;
-      h[i] = (off * 0x9E3779B1u) >> hshift;
-      added[i] = 0u;
-    }
-    bool left = true;
-    for (int p = 0; p < kMaxProbe && left; p++) {
-      uint32_t cur[kInsU];
+  for (int i = 0; i < 4; i++) h[i] = (k[i] - 1u) * 0x9E3779B1u >> hshift;
+#ifdef COOC_SP_STATS
+  if (threadIdx.x == 0) S_.st[24] += (k[0] != 0u) + (k[1] != 0u) + (k[2] != 0u) + (k[3] != 0u);
+#endif
+  for (int p = 0; p < kMaxProbe; p++) {
+#ifdef COOC_SP_STATS
+    if (threadIdx.x == 0) S_.st[25] += 1;
+#endif
+    uint32_t cur[4];
 #pragma unroll
-      for (int i = 0; i < kInsU; i++) cur[i] = key[i] ? atomicCAS(tab + h[i], 0u, key[i] | 1u) : 0u;
-      left = false;
+    for (int i = 0; i < 4; i++) cur[i] = k[i] ? atomicCAS(keys + h[i], 0u, k[i]) : 0u;
+    bool left = false;
 #pragma unroll
-      for (int i = 0; i < kInsU; i++) {
-        if (!key[i]) continue;
-        if (cur[i] == 0u) {
-          key[i] = 0u;  // claimed, count 1
-        } else if ((cur[i] & ~kCntMask) == key[i]) {
-          added[i] = atomicAdd(tab + h[i], 1u);  // the old word, checked after the round
-          key[i] = 0u;
-        } else {
-          h[i] = (h[i] + 1u) & hmask;
-          left = true;
-        }
+    for (int i = 0; i < 4; i++) {
+      if (!k[i]) continue;
+      if (cur[i] == 0u || cur[i] == k[i]) {
+        atomicAdd(cnts + h[i], 1u);
+        k[i] = 0u;
+      } else {
+        h[i] = (h[i] + 1u) & hmask;
+        left = true;
       }
     }
-    probe_ovf |= left;
-#pragma unroll
-    for (int i = 0; i < kInsU; i++) cnt_ovf |= (added[i] & kCntMask) == kCntMask;
+    if (!left) return;
   }
-  if (probe_ovf) S_.flag = 1u;
-  if (cnt_ovf) S_.cflag = 1u;
+  S_.flag = 1u;
 }
 
 struct WalkOp {
@@ -736,6 +714,10 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
       const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
       if (slot < S_.bstart[t + 1] - S_.bstart[t]) A.scratch[op.sbase + S_.bstart[t] + slot] = v;  // else overflow
     }
+    return;
+  }
+  if (op.mode == 1) {
+    sp_hash_insert4(L.R, L.R + kHashMax, v, op.hshift, op.hmask, S_);
     return;
   }
   atomicAdd(&L.R[v.x - op.c0], 1u);
@@ -830,103 +812,6 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   return total;
 }
 
-// sp_walk_batch for a hash chunk: the same walkers and loads, but every walk step first STAGES the
-// partner ids it loaded (pads dropped) in LDS -- at most kSpU x 4 per lane, kStage in all -- and then
-// the whole workgroup inserts them kInsU per thread at a time (sp_hash_insert_staged): the inserts no
-// longer sit one 16-B group at a time between two dependent loads.  Two barriers per step.
-__device__ inline uint32_t sp_walk_batch_hash(const SpArgs &A, const SpShared &L, SpStatic &S_,
-                                              const uint4 *__restrict__ ar, int64_t nsrc, int nb, uint32_t len,
-                                              int64_t start, const WalkOp &op) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const unsigned long long c_b0 = STAT_CLOCK();
-  uint32_t total;
-  const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
-  if (total == 0) return 0;  // uniform (scalar branch)
-  const uint32_t mean = total / uint32_t(nb);
-  const uint32_t S = mean >= 12 ? 16u : 4u;
-  const uint32_t nW = kSpThreads / S;
-  if (tid < nb) {
-    L.vst[tid] = ex;
-    L.seg[tid] = start - int64_t(ex);
-    if (len) {
-      const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
-      const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
-      for (uint32_t q = q0; q < q1 && q < nW; q++) L.qstart[q] = tid;
-    }
-  }
-  if (tid == 0) {
-    L.vst[nb] = total;
-    S_.nst[0] = S_.nst[1] = 0u;
-  }
-  __syncthreads();
-  const unsigned long long c_b1 = STAT_CLOCK();
-  STAT_ADD(16, c_b1 - c_b0);
-  STAT_ADD(18, total);
-  const uint32_t q = uint32_t(tid) / S, ql = uint32_t(tid) % S;
-  const uint32_t lo = uint32_t(uint64_t(total) * q / nW), hi = uint32_t(uint64_t(total) * (q + 1) / nW);
-  // every walker's share is within one group of total / nW: the steps of the longest share, for all
-  const uint32_t share = (total + nW - 1) / nW;
-  const uint32_t steps = (share + S * kSpU - 1) / (S * kSpU);
-  uint32_t g = lo + ql;
-  int32_t cur = g < hi ? L.qstart[q] : 0;
-  uint32_t next = g < hi ? L.vst[cur + 1] : 0u;
-  int64_t base = g < hi ? L.seg[cur] : 0;
-  auto load = [&](uint32_t g0, uint4 v[kSpU]) {
-#pragma unroll
-    for (int k = 0; k < kSpU; k++) {
-      const uint32_t gk = g0 + S * k;
-      v[k] = make_uint4(kSink, kSink, kSink, kSink);
-      if (gk < hi) {
-        while (gk >= next) {
-          cur++;
-          next = L.vst[cur + 1];
-          base = L.seg[cur];
-        }
-        if (BCHK(A, base + gk >= 0 && base + gk < nsrc, 16)) v[k] = ar[base + gk];
-      }
-    }
-  };
-  uint4 v[kSpU];
-  load(g, v);
-  uint32_t *st = L.R + kHashMax;
-  for (uint32_t r = 0; r < steps; r++) {
-    uint4 vn[kSpU];
-    load(g + S * kSpU, vn);  // the next step's groups, in flight during this step's inserts
-    // stage this step's ids: wave prefix of the per-lane counts, one LDS reservation per wave
-    uint32_t nid = 0;
-#pragma unroll
-    for (int k = 0; k < kSpU; k++)
-      nid += (v[k].x != kSink) + (v[k].y != kSink) + (v[k].z != kSink) + (v[k].w != kSink);
-    const uint32_t inc = wave_incl_scan(nid);
-    uint32_t wbase = 0;
-    if (lane == 63 && inc) wbase = atomicAdd(&S_.nst[r & 1u], inc);
-    wbase = uint32_t(__shfl(int(wbase), 63, 64));
-    uint32_t o = wbase + inc - nid;
-#pragma unroll
-    for (int k = 0; k < kSpU; k++) {
-      if (v[k].x != kSink) st[o++] = v[k].x;
-      if (v[k].y != kSink) st[o++] = v[k].y;
-      if (v[k].z != kSink) st[o++] = v[k].z;
-      if (v[k].w != kSink) st[o++] = v[k].w;
-    }
-    if (tid == 0) S_.nst[(r + 1u) & 1u] = 0u;  // (read by every thread before the last round's end)
-    __syncthreads();
-    sp_hash_insert_staged(L, S_, S_.nst[r & 1u], op.c0, op.hshift, op.hmask);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kSpU; k++) v[k] = vn[k];
-    g += S * kSpU;
-  }
-  STAT_ADD(17, STAT_CLOCK() - c_b1);
-  return total;
-}
-
-__device__ inline uint32_t sp_walk_any(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
-                                       int64_t nsrc, int nb, uint32_t len, int64_t start, const WalkOp &op) {
-  return op.mode == 1 ? sp_walk_batch_hash(A, L, S_, ar, nsrc, nb, len, start, op)
-                      : sp_walk_batch(A, L, S_, ar, nsrc, nb, len, start, op);
-}
-
 __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0,
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
@@ -944,8 +829,8 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
       len = okt ? uint32_t(tbu[full ? A.T : t1] - s0) : 0u;
       start = s0;
     }
-    walked += sp_walk_any(A, L, S_, A.tarena, A.n_groups, nb, len, start, op);
-    if (uni(S_.flag | S_.cflag)) break;
+    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, len, start, op);
+    if (uni(S_.flag)) break;
   }
   return walked;
 }
@@ -1088,7 +973,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
                                        int32_t c1, uint64_t &rsum) {
   const int tid = threadIdx.x;
   const unsigned long long c_h0 = STAT_CLOCK();
-  uint32_t *keys = L.R, *cnts = L.R + kHashMax;  // slots; cnts: block bases (the staging area, free now)
+  uint32_t *keys = L.R, *cnts = L.R + kHashMax;
   const int per = H / kSpThreads;
   const int32_t nL1 = (c1 - c0 + 1023) >> 10;
   uint32_t ek[kHashMax / kSpThreads], ec[kHashMax / kSpThreads], er[kHashMax / kSpThreads];
@@ -1099,10 +984,11 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     er[i] = 0u;
     if (i < per) {
       const int j = tid + i * kSpThreads;
-      const uint32_t w = keys[j], k = w >> kCntBits, v = w & kCntMask;
+      const uint32_t k = keys[j], v = cnts[j];
       keys[j] = 0u;
+      cnts[j] = 0u;
       if (k && v) {
-        const uint32_t col = k - 1u;
+        const uint32_t col = k - 1u - uint32_t(c0);
         ek[i] = col;
         ec[i] = v;
         rsum += v;
@@ -1169,9 +1055,10 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   __syncthreads();
   STAT_ADD(22, STAT_CLOCK() - c_h2);
   STAT_ADD(23, ne);
-  for (uint32_t r = tid; r < nblk; r += kSpThreads) keys[r] = 0u;
-  // the block bases and the staged ids: the next chunk may be a dense tile
-  for (int32_t i = tid; i < kStage / 4; i += kSpThreads) reinterpret_cast<uint4 *>(cnts)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t r = tid; r < nblk; r += kSpThreads) {
+    keys[r] = 0u;
+    cnts[r] = 0u;
+  }
   for (int32_t i = tid; i < nL1; i += kSpThreads) L.L1[i] = 0u;
   __syncthreads();
 }
@@ -1283,7 +1170,6 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       op.hmask = uint32_t(H) - 1u;
       if (tid == 0) {
         S_.flag = 0u;
-        S_.cflag = 0u;
       }
       __syncthreads();
       const unsigned long long c_walk = STAT_CLOCK();
@@ -1303,7 +1189,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         const int nb = t1 - t;
         const uint32_t len = tid < nb ? S_.bcur[t + tid] : 0u;
         const int64_t start = tid < nb ? op.sbase + S_.bstart[t + tid] : 0;
-        walked = sp_walk_any(A, L, S_, A.scratch, int64_t(gridDim.x) * A.scr_cap, nb, len, start, op);
+        walked = sp_walk_batch(A, L, S_, A.scratch, int64_t(gridDim.x) * A.scr_cap, nb, len, start, op);
       } else {  // (also a gathered chunk whose bucket overflowed)
         walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
       }
@@ -1311,18 +1197,20 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       STAT_ADD(split ? 4 : dense ? 0 : 1, c_walked - c_walk);
       STAT_ADD(dense ? 9 : 10, walked);
       STAT_ADD(dense ? 5 : 6, 1);
-      if (!dense && uni(S_.flag | S_.cflag)) {
+      if (!dense && uni(S_.flag)) {
         STAT_ADD(H < kHashMax ? 7 : 8, 1);
-        // overflow: clear the table and the staging ids; retry with a 4x table, at the largest size (or
-        // when a count outgrew its 12 bits) as dense tiles
-        for (int32_t j = tid; j < kTW; j += kSpThreads) L.R[j] = 0u;
-        if (H < kHashMax && !uni(S_.cflag)) {
+        // overflow: clear the table; retry with a 4x table, at the largest size as dense tiles
+        for (int32_t j = tid; j < H; j += kSpThreads) {
+          L.R[j] = 0u;
+          L.R[kHashMax + j] = 0u;
+        }
+        if (H < kHashMax) {
           H = min(kHashMax, H * 4);
         } else {
           dense_until = t1;
           H = 0;
         }
-        __syncthreads();  // every wave has read the flags before the retry resets them
+        __syncthreads();  // every wave has read the flag before the retry resets it
         continue;
       }
       // the -1 at column a per contribution whose walk includes its own position (whole rows)
@@ -1344,11 +1232,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         STAT_ADD(2, STAT_CLOCK() - c_walked);
       } else {
         if (tid == 0 && a >= c0 && a < c1) {
-          const uint32_t off = uint32_t(a - c0);
-          uint32_t h = (off * 0x9E3779B1u) >> op.hshift;
+          uint32_t h = (uint32_t(a) * 0x9E3779B1u) >> op.hshift;
           for (int p = 0; p < H; p++) {
-            if ((L.R[h] & ~kCntMask) == (off + 1u) << kCntBits) {
-              L.R[h] -= self;  // (its count holds >= self: one occurrence of a per contribution)
+            if (L.R[h] == uint32_t(a) + 1u) {
+              L.R[kHashMax + h] -= self;
               break;
             }
             h = (h + 1u) & op.hmask;
