@@ -70,6 +70,7 @@ constexpr int kTShift = COOC_SP_TSHIFT;
 constexpr int kTW = 1 << kTShift;  // dense tile width (16384: 64 KB of uint32 LDS counters)
 constexpr int kSpMaxTiles = 64;                        // per-row plans are 64-bit tile masks
 constexpr int kHashMax = 8192;                        // slots: keys + counts = the dense tile's 128 KB
+constexpr int kWStage = kHashMax / 2;                  // hash compaction: entries staged in LDS for 16-B stores
 constexpr int kHashMin = 1024;                         // one slot per thread at least
 constexpr int kHashMaxTiles = (1 << 20) / kTW;          // a hash chunk spans <= 2^20 columns ...
 constexpr int kL1Words = kHashMaxTiles * kTW / 1024;   // ... so its block bitmap is <= 1024 words
@@ -1040,6 +1041,45 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   const int64_t base = sp_reserve(A, S_, ne);  // (barrier: bases visible)
   const unsigned long long c_h2 = STAT_CLOCK();
   STAT_ADD(21, c_h2 - c_h1);
+#ifndef COOC_SP_NO_STAGED_WRITE
+  if (base >= 0 && ne <= uint32_t(kWStage)) {
+    // the chunk's entries land in LDS at their sorted positions (the free upper halves of the emptied key
+    // and count areas), then leave in order: 16-B stores of whole column / count runs instead of one
+    // scattered 4-B store per entry and array
+    uint32_t *sc = keys + kWStage, *sn = cnts + kWStage;
+#pragma unroll
+    for (int i = 0; i < kHashMax / kSpThreads; i++) {
+      if (ek[i] == ~0u) continue;
+      const uint32_t col = ek[i], r = er[i];
+      const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
+      sc[q] = uint32_t(c0) + col;
+      sn[q] = ec[i];
+    }
+    __syncthreads();
+    const uint32_t head = min(ne, uint32_t((4 - (base & 3)) & 3));  // entries before the first 16-B boundary
+    const uint32_t body = (ne - head) >> 2;
+    for (uint32_t j = tid; j < head; j += kSpThreads) {
+      A.col_out[base + j] = int32_t(sc[j]);
+      A.cnt_out[base + j] = sn[j];
+    }
+    int4 *co4 = reinterpret_cast<int4 *>(A.col_out + base + head);
+    uint4 *cn4 = reinterpret_cast<uint4 *>(A.cnt_out + base + head);
+    for (uint32_t j = tid; j < body; j += kSpThreads) {
+      const uint32_t q = head + 4 * j;
+      co4[j] = make_int4(int32_t(sc[q]), int32_t(sc[q + 1]), int32_t(sc[q + 2]), int32_t(sc[q + 3]));
+      cn4[j] = make_uint4(sn[q], sn[q + 1], sn[q + 2], sn[q + 3]);
+    }
+    for (uint32_t q = head + 4 * body + tid; q < ne; q += kSpThreads) {
+      A.col_out[base + q] = int32_t(sc[q]);
+      A.cnt_out[base + q] = sn[q];
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < ne; q += kSpThreads) {  // the areas go back to zero for the next chunk
+      sc[q] = 0u;
+      sn[q] = 0u;
+    }
+  } else
+#endif
   if (base >= 0) {
 #pragma unroll
     for (int i = 0; i < kHashMax / kSpThreads; i++) {
