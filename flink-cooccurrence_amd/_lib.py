@@ -25,6 +25,7 @@ COOC_FLAG_EXACT_SCORES = 1
 COOC_FLAG_OUTPUT_CSR = 2
 COOC_FLAG_OUTPUT_DENSE = 4
 COOC_FLAG_GENERAL_PLANNER = 8
+COOC_FLAG_SORT_ROWS = 16
 COOC_VERIFY_SYMMETRY = 1
 
 i16p = ctypes.POINTER(ctypes.c_int16)
@@ -123,6 +124,7 @@ _SIGS = {
     "cooc_verify_batch": (ctypes.c_int, [vp, ctypes.c_int32, vp, i64p, vp]),
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+    "cooc_last_sort_rows": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _lib = None

@@ -104,7 +104,9 @@ class CooccurrenceCore:
                  exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0,
                  devices=None, subtask: int = 0):
         """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
-        planner: "auto" (the batch planner below 40,320 items) or "general" (the sort-based planner).
+        planner: "auto" (the batch planner below 40,320 items, the large-universe planner above), "large"
+        (the large-universe planner at any n_items; "general" is an alias) or "sort" (large, with every
+        whole row through the sort + segmented-reduce path: packed 64-bit pair keys, radix sort, runs).
         user_cut: kMax, 0 = off; else only the first user_cut interactions of every user are expanded
         (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped)."""
         L = _lib.load()
@@ -112,9 +114,10 @@ class CooccurrenceCore:
         if output not in ("auto", "csr", "dense"):
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown output layout {output!r}")
         flags |= {"auto": 0, "csr": _lib.COOC_FLAG_OUTPUT_CSR, "dense": _lib.COOC_FLAG_OUTPUT_DENSE}[output]
-        if planner not in ("auto", "general"):
+        if planner not in ("auto", "general", "large", "sort"):
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown planner {planner!r}")
-        flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner == "general" else 0
+        flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner != "auto" else 0
+        flags |= _lib.COOC_FLAG_SORT_ROWS if planner == "sort" else 0
         cfg = CoocConfig(device, n_items, topk, flags, window_size_ms, user_cut, 0)
         h = ctypes.c_void_p()
         if devices is None:
@@ -311,6 +314,13 @@ class CooccurrenceCore:
 
     def set_kernel_timing(self, enable: bool = True) -> None:
         check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)
+
+    def last_sort_rows(self) -> tuple:
+        """(rows, ordered pairs) the last large-universe count sent through the sort + segmented-reduce
+        path (rows whose LDS hash table overflowed, or every whole row with planner="sort")."""
+        rows, pairs = ctypes.c_int64(), ctypes.c_int64()
+        check(_lib.load().cooc_last_sort_rows(self._h, ctypes.byref(rows), ctypes.byref(pairs)), self._h)
+        return rows.value, pairs.value
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

@@ -457,4 +457,13 @@ int cooc_last_kernel_ms(cooc_ctx *ctx, float *accumulate_ms) {
   });
 }
 
+int cooc_last_sort_rows(cooc_ctx *ctx, int64_t *rows, int64_t *pairs) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !rows || !pairs) return COOC_ERR_ARG;
+    *rows = ctx->counter.last_deferred_rows();
+    *pairs = ctx->counter.last_deferred_pairs();
+    return COOC_OK;
+  });
+}
+
 }  // extern "C"

@@ -5,17 +5,10 @@
 //   ItemRowAggregator.java:26-31                                            per-(itemA, window) row reduce
 //   RowSumAggregator.java:25-27,54-71                                       per-(item, window) row-sum reduce
 //
-// Pipeline for one window (all on one HIP stream):
-//   1. k_build_contribs   one record per (user, position): key = the row item, value = (user, kind)
-//   2. radix sort by row  (hipCUB onesweep, ceil(log2 M) key bits) — the keyBy(item) regrouping
-//   3. k_row_ptr          CSR row pointer of the row-sorted contributions
-//   4. inclusive scan     of each contribution's segment length = its pair work
-//   5. k_plan_rows        per-row work, split into chunks of <= kChunkWork pairs, output capacity
-//   6. k_make_chunks      chunk table, heaviest rows first
-//   7. k_accumulate2      ★ persistent: per chunk a dense M-counter LDS row, one ds_add_u32 per pair,
-//                           compacted in column order into the padded CSR (or flushed into a
-//                           staging row when the row is split over chunks)
-//   8. k_finalize_split   compacts staging rows of split rows
+// Two planners cover every universe: this file's BATCH planner (n_items < 40,320: one dense LDS row per
+// chunk, k_acc_batch, for one-window batches, streaming windows and the C2 records exchange) and the
+// LARGE-UNIVERSE planner of cooc_sparse.hip (n_items >= 40,320, or any n_items with
+// COOC_FLAG_GENERAL_PLANNER: per-row workgroups over LDS hash / dense-tile chunks, k_sp_main).
 // HBM model per window: the ordered pairs P stream 4 B partner ids (mostly served by MALL/L2:
 // every user list is re-read once per item in it), 12 B per output entry; see DESIGN.md.
 #include <cstdio>
@@ -29,85 +22,8 @@ namespace {
 
 constexpr int kAccThreads = 1024;
 constexpr int kAccWaves = kAccThreads / 64;
-constexpr int64_t kChunkWork = int64_t(1) << 22;  // pairs per chunk (balances heavy rows)
-constexpr int kLdsBudget = 160 * 1024 - 512;      // dynamic LDS left after the kernels' static LDS
 constexpr int kBatchLdsBudget = 160 * 1024 - 1536;  // k_acc_batch: its static LDS is under 1.5 KB
 
-template <class T>
-__device__ inline int64_t lower_bound_i64(const T *a, int64_t n, T x) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// ---- 1. contributions ---------------------------------------------------------------------------
-// One wave per active user: lanes walk its history.  Key = the item at the position (the row the
-// contribution adds into), value = (active index << 1) | (position is OLD).  Validates item ids.
-__global__ __launch_bounds__(256) void k_build_contribs(int64_t n_active, const int64_t *__restrict__ off,
-                                                        const int32_t *__restrict__ len,
-                                                        const int32_t *__restrict__ old,
-                                                        const int64_t *__restrict__ cbase,
-                                                        const int32_t *__restrict__ arena, int32_t M,
-                                                        uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                                                        int64_t *__restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  bool bad = false;
-  for (int64_t j = wave; j < n_active; j += n_waves) {
-    const int32_t *h = arena + off[j];
-    const int32_t n = len[j], o = old[j];
-    const int64_t base = cbase[j];
-    for (int32_t p = lane; p < n; p += 64) {
-      int32_t item = h[p];
-      if (item < 0 || item >= M) { bad = true; item = 0; }
-      keys[base + p] = uint32_t(item);
-      vals[base + p] = (uint32_t(j) << 1) | uint32_t(p < o);
-    }
-  }
-  if (bad) atomicOr(reinterpret_cast<unsigned long long *>(err), 1ull);
-}
-
-// ---- 3. row pointer -------------------------------------------------------------------------------
-__global__ void k_row_ptr(const uint32_t *__restrict__ keys, int64_t n, int32_t M, int64_t *__restrict__ row_ptr) {
-  const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (a <= M) row_ptr[a] = lower_bound_i64<uint32_t>(keys, n, uint32_t(a));
-}
-
-struct WorkOp {  // pair work of a contribution = its segment length
-  const int32_t *len;
-  const int32_t *old;
-  __host__ __device__ int64_t operator()(uint32_t v) const {
-    const uint32_t j = v >> 1;
-    return (v & 1u) ? int64_t(len[j] - old[j]) : int64_t(len[j]);
-  }
-};
-
-// ---- 5. per-row plan ------------------------------------------------------------------------------
-__global__ void k_plan_rows(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ epre, int32_t M,
-                            uint64_t *__restrict__ row_work, int32_t *__restrict__ order,
-                            int32_t *__restrict__ row_nch, int32_t *__restrict__ row_split) {
-  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= M) return;
-  const int64_t w = epre[row_ptr[a + 1]] - epre[row_ptr[a]];
-  const int32_t nch = w > 0 ? int32_t((w + kChunkWork - 1) / kChunkWork) : 0;
-  row_work[a] = uint64_t(w);
-  order[a] = a;
-  row_nch[a] = nch;
-  row_split[a] = nch > 1 ? 1 : 0;
-}
-
-// Output capacity of a row: min(M, pair work of the whole row) (its entry count cannot exceed either).
-__global__ void k_row_cap(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ epre, int32_t M,
-                          int64_t *__restrict__ row_cap) {
-  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= M) return;
-  const int64_t w = epre[row_ptr[a + 1]] - epre[row_ptr[a]];
-  row_cap[a] = w < M ? w : int64_t(M);
-}
 
 __global__ void k_gather_i32(const int32_t *__restrict__ order, const int32_t *__restrict__ src, int32_t n,
                              int32_t *__restrict__ dst) {
@@ -127,78 +43,6 @@ __global__ void k_totals(const int32_t *__restrict__ ord_cbase, const int32_t *_
   tot->n_split = split_slot[M];
   queue[0] = 0;
   queue[1] = 0;
-}
-
-__global__ void k_cap_total(const int64_t *__restrict__ row_base, const int64_t *__restrict__ epre, int32_t M,
-                            int64_t n_contrib, PlanTotals *__restrict__ tot) {
-  tot->cap_total = row_base[M];
-  tot->work_total = epre[n_contrib];
-  tot->nnz_total = 0;
-}
-
-
-// The general path reads partner ids as u16 (n_items <= 40,704): half the bytes per pair.
-__global__ void k_narrow(const int32_t *__restrict__ src, int64_t n, uint16_t *__restrict__ dst) {
-  const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
-  if (i + 3 < n) {
-    const int4 v = *reinterpret_cast<const int4 *>(src + i);
-    *reinterpret_cast<ushort4 *>(dst + i) = make_ushort4(uint16_t(v.x), uint16_t(v.y), uint16_t(v.z), uint16_t(v.w));
-  } else {
-    for (int64_t k = i; k < n; k++) dst[k] = uint16_t(src[k]);
-  }
-}
-
-// Padded u16 arena for the vector path: user j's list at poff[j] (16-B aligned), padded to a
-// multiple of 8 ids with 0xFFFF.
-__global__ void k_pad_lens(int64_t n, const int32_t *__restrict__ len, int64_t *__restrict__ plen) {
-  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) plen[j] = (int64_t(len[j]) + 7) & ~int64_t(7);
-}
-
-__global__ void k_narrow_pad(int64_t n_users, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
-                             const int64_t *__restrict__ poff, const int32_t *__restrict__ arena,
-                             uint16_t *__restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t j = wave; j < n_users; j += n_waves) {
-    const int32_t *h = arena + off[j];
-    uint16_t *o = out + poff[j];
-    const int32_t n = len[j], pn = (n + 7) & ~7;
-    for (int32_t i = lane; i < pn; i += 64) o[i] = i < n ? uint16_t(h[i]) : uint16_t(0xFFFF);
-  }
-}
-
-struct PadLenOp {  // padded segment length of a (kind-0) contribution
-  const int64_t *plen;
-  __host__ __device__ int64_t operator()(uint32_t v) const { return plen[v >> 1]; }
-};
-
-__global__ void k_seg_start_pad(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ poff,
-                                int64_t *__restrict__ seg) {
-  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (c < n) seg[c] = poff[cvals[c] >> 1] | (int64_t(1) << 63);
-}
-
-// ---- 6. chunk table -------------------------------------------------------------------------------
-__global__ void k_make_chunks(const int32_t *__restrict__ order, const int32_t *__restrict__ ord_nch,
-                              const int32_t *__restrict__ ord_cbase, const int64_t *__restrict__ row_ptr,
-                              const int64_t *__restrict__ epre, const int32_t *__restrict__ split_slot, int32_t M,
-                              Chunk *__restrict__ chunks) {
-  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= M) return;
-  const int32_t nch = ord_nch[r];
-  if (nch == 0) return;
-  const int32_t a = order[r];
-  const int64_t c0 = row_ptr[a], c1 = row_ptr[a + 1];
-  const int64_t w0 = epre[c0];
-  const int32_t slot = nch > 1 ? split_slot[a] : -1;
-  int64_t b = c0;
-  for (int32_t j = 0; j < nch; j++) {
-    const int64_t e = (j == nch - 1) ? c1 : c0 + lower_bound_i64<int64_t>(epre + c0, c1 - c0, w0 + (j + 1) * kChunkWork);
-    chunks[ord_cbase[r] + j] = Chunk{a, slot, b, e, (int64_t(j) << 32) | int64_t(r)};
-    b = e;
-  }
 }
 
 // Block-wide sum of a uint64 (kAccThreads threads).
@@ -419,194 +263,6 @@ __device__ inline uint32_t compact_row_ranges4(uint32_t *row, int32_t M, int32_t
   return tot;
 }
 
-// Segment start of every row-sorted contribution (arena offset of its first partner id), with
-// bit 63 set for a NEW position (the -1 self correction applies to it).
-__global__ void k_seg_start(const uint32_t *__restrict__ cvals, int64_t n, const int64_t *__restrict__ aoff,
-                            const int32_t *__restrict__ aold, int64_t *__restrict__ seg) {
-  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const uint32_t v = cvals[c];
-  const uint32_t j = v >> 1;
-  const int64_t off = aoff[j];
-  seg[c] = (v & 1u) ? off + aold[j] : (off | (int64_t(1) << 63));
-}
-
-// ★ general path (streaming windows with resident histories, n_items <= 40,704): the chunk's
-// contributions are flattened into one virtual pair range.  Up to `db` segment descriptors
-// (virtual start, arena start) are staged in LDS per batch; the 16 waves split the batch's range
-// into equal contiguous pieces and walk it 64 lanes wide, so every lane stays busy whatever the
-// user-list lengths, and no wave waits on a per-user descriptor chain.
-// VEC: every segment starts 16-B aligned and spans a multiple of 8 ids (user lists padded with
-// 0xFFFF in the arena, virtual starts from the padded prefix `vpre`), so each lane loads 8 partner
-// ids with one 16-B load: 8x fewer load instructions in flight for the same bytes.
-template <int U, bool VEC>
-__global__ __launch_bounds__(kAccThreads) void k_accumulate2(
-    const Chunk *__restrict__ chunks, const PlanTotals *__restrict__ tot, int32_t *__restrict__ queue,
-    const int64_t *__restrict__ seg, const uint16_t *__restrict__ arena, const int64_t *__restrict__ epre,
-    const int64_t *__restrict__ vpre, int32_t M, int32_t db, const int64_t *__restrict__ row_base,
-    int32_t *__restrict__ row_nnz, int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
-    uint32_t *__restrict__ staging, int64_t *__restrict__ split_sum, int64_t *__restrict__ rowsum,
-    int64_t *__restrict__ err) {
-  extern __shared__ int64_t lds64[];
-  int64_t *s_seg = lds64;                                            // [db] arena start - virtual start
-  uint32_t *s_vst = reinterpret_cast<uint32_t *>(lds64 + db);        // [db + 1] virtual starts
-  uint32_t *acc = s_vst + db + 1;                                    // [M]
-  __shared__ int32_t s_chunk;
-  __shared__ uint32_t s_self;
-  __shared__ uint32_t s_wave[kAccWaves];
-  __shared__ uint64_t s_red[kAccWaves];
-  __shared__ int64_t s_base;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t n_chunks = tot->n_chunks;
-  for (int32_t b = tid; b < M; b += kAccThreads) acc[b] = 0;
-  for (;;) {
-    if (tid == 0) {
-      s_chunk = atomicAdd(queue, 1);
-      s_self = 0;
-    }
-    __syncthreads();
-    const int32_t ch = s_chunk;
-    if (ch >= n_chunks) break;
-    const Chunk c = chunks[ch];
-    const int64_t chunk_work = epre[c.end] - epre[c.begin];
-    for (int64_t b0 = c.begin; b0 < c.end; b0 += db) {
-      const int32_t nb = int32_t(min(int64_t(db), c.end - b0));
-      const int64_t *vp = VEC ? vpre : epre;
-      const int64_t e0 = vp[b0];
-      uint32_t selfs = 0;
-      for (int32_t i = tid; i <= nb; i += kAccThreads) {
-        const uint32_t vs = uint32_t(vp[b0 + i] - e0);
-        s_vst[i] = vs;
-        if (i < nb) {
-          const int64_t sg = seg[b0 + i];
-          selfs += uint32_t(sg < 0);
-          s_seg[i] = (sg & ~(int64_t(1) << 63)) - int64_t(vs);
-        }
-      }
-      const uint64_t bal = __ballot(selfs != 0u);
-      if (lane == 0 && bal) atomicAdd(&s_self, uint32_t(__popcll(bal)));
-      __syncthreads();
-      const uint32_t total = s_vst[nb];
-      if (!VEC) {
-        const uint32_t lo = uint32_t((uint64_t(total) * uint32_t(wave)) / kAccWaves);
-        const uint32_t hi = uint32_t((uint64_t(total) * uint32_t(wave + 1)) / kAccWaves);
-        uint32_t v = lo + lane;
-        if (v < hi) {
-          // cursor: the contribution holding virtual index v (upper_bound - 1 over s_vst[0..nb])
-          int32_t l = 0, r = nb;
-          while (r - l > 1) {
-            const int32_t m = (l + r) >> 1;
-            if (s_vst[m] <= v) l = m; else r = m;
-          }
-          int32_t cur = l;
-          uint32_t next = s_vst[cur + 1];
-          int64_t base = s_seg[cur];
-          for (; v < hi; v += 64u * U) {
-            int64_t a[U];
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-              const uint32_t vk = v + 64u * k;
-              a[k] = -1;
-              if (vk < hi) {
-                while (vk >= next) {
-                  cur++;
-                  next = s_vst[cur + 1];
-                  base = s_seg[cur];
-                }
-                a[k] = base + vk;
-              }
-            }
-            uint32_t it[U];
-#pragma unroll
-            for (int k = 0; k < U; k++) it[k] = a[k] >= 0 ? uint32_t(arena[a[k]]) : 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < U; k++)
-              if (it[k] != 0xFFFFFFFFu) atomicAdd(&acc[it[k]], 1u);
-          }
-        }
-      } else {
-        // groups of 8 ids; every segment boundary is a multiple of 8
-        const uint32_t groups = total >> 3;
-        const uint32_t lo = uint32_t((uint64_t(groups) * uint32_t(wave)) / kAccWaves);
-        const uint32_t hi = uint32_t((uint64_t(groups) * uint32_t(wave + 1)) / kAccWaves);
-        uint32_t g = lo + lane;
-        if (g < hi) {
-          int32_t l = 0, r = nb;
-          while (r - l > 1) {
-            const int32_t m = (l + r) >> 1;
-            if (s_vst[m] <= (g << 3)) l = m; else r = m;
-          }
-          int32_t cur = l;
-          uint32_t next = s_vst[cur + 1];
-          int64_t base = s_seg[cur];
-          for (; g < hi; g += 64u * U) {
-            int64_t a[U];
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-              const uint32_t gk = g + 64u * k;
-              a[k] = -1;
-              if (gk < hi) {
-                while ((gk << 3) >= next) {
-                  cur++;
-                  next = s_vst[cur + 1];
-                  base = s_seg[cur];
-                }
-                a[k] = base + (int64_t(gk) << 3);
-              }
-            }
-            uint4 q[U];
-#pragma unroll
-            for (int k = 0; k < U; k++)
-              q[k] = a[k] >= 0 ? *reinterpret_cast<const uint4 *>(arena + a[k]) : make_uint4(~0u, ~0u, ~0u, ~0u);
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-              const uint32_t w4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
-#pragma unroll
-              for (int h = 0; h < 4; h++) {
-                const uint32_t lo16 = w4[h] & 0xFFFFu, hi16 = w4[h] >> 16;
-                if (lo16 != 0xFFFFu) atomicAdd(&acc[lo16], 1u);
-                if (hi16 != 0xFFFFu) atomicAdd(&acc[hi16], 1u);
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-    // the -1 at x_p for every new position applies to column x_p = row
-    const uint32_t self_total = s_self;
-    const int64_t chunk_rowsum = chunk_work - int64_t(self_total);
-    if (tid == 0) {
-      acc[c.row] -= self_total;
-      atomicAdd(reinterpret_cast<unsigned long long *>(rowsum + c.row), (unsigned long long)chunk_rowsum);
-      if (c.split >= 0)
-        atomicAdd(reinterpret_cast<unsigned long long *>(split_sum + c.split), (unsigned long long)chunk_rowsum);
-    }
-    __syncthreads();
-    if (c.split < 0) {
-      uint64_t sum;
-      int64_t used;
-      const uint32_t nnz = compact_row_ranges(acc, M, 0, col_out, cnt_out, Place{row_base[c.row], nullptr, 0}, &used,
-                                              &sum, s_wave, &s_base);
-      const uint64_t total = block_sum_u64(sum, s_red);
-      if (tid == 0) {
-        row_nnz[c.row] = int32_t(nnz);
-        if (total != uint64_t(chunk_rowsum)) atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
-      }
-    } else {
-      uint32_t *srow = staging + int64_t(c.split) * M;
-      for (int32_t b = tid; b < M; b += kAccThreads) {
-        const uint32_t v = acc[b];
-        if (v) {
-          atomicAdd(srow + b, v);
-          acc[b] = 0;
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ---- 8. split rows: compact the staging rows ------------------------------------------------------
 // bump == nullptr: rows go to their padded place row_base[a]; else to an exact-size bump region
 // (row_base[a] is set).
@@ -663,16 +319,6 @@ __global__ void k_pack(const int64_t *__restrict__ row_base, const int64_t *__re
       pk_col[dst + i] = col[src + i];
       pk_cnt[dst + i] = cnt[src + i];
     }
-  }
-}
-
-__global__ void k_iota_users(int64_t n, const int64_t *__restrict__ user_ptr, int64_t *__restrict__ off,
-                             int32_t *__restrict__ len, int32_t *__restrict__ old) {
-  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) {
-    off[j] = user_ptr[j];
-    len[j] = int32_t(user_ptr[j + 1] - user_ptr[j]);
-    old[j] = 0;
   }
 }
 
@@ -1423,12 +1069,6 @@ __global__ __launch_bounds__(kAccThreads) void k_pack_dense(const uint32_t *__re
 
 inline unsigned blocks_for(int64_t n, int t) { return unsigned((n + t - 1) / t); }
 
-int key_bits(int32_t M) {
-  int b = 1;
-  while ((int64_t(1) << b) < M) b++;
-  return b;
-}
-
 }  // namespace
 
 Status DevBuf::reserve(size_t bytes) {
@@ -1452,13 +1092,6 @@ void DevBuf::release() {
   cap = 0;
 }
 
-Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr, int64_t *off, int32_t *len,
-                         int32_t *old) {
-  if (n_users > 0) k_iota_users<<<blocks_for(n_users, 256), 256, 0, s>>>(n_users, user_ptr, off, len, old);
-  COOC_HIP_TRY(hipGetLastError());
-  return Status::Ok();
-}
-
 Status Counter::init(int32_t n_items) {
   if (n_items <= 0) return Status{1, "n_items must be positive"};
   M_ = n_items;
@@ -1466,16 +1099,8 @@ Status Counter::init(int32_t n_items) {
   int dev = 0;
   COOC_HIP_TRY(hipGetDevice(&dev));
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu_, hipDeviceAttributeMultiprocessorCount, dev));
-  // run_sparse (cooc_sparse.hip) sets its own attributes; the general planner (streaming windows) keeps
-  // one LDS row over all items plus the descriptor batch, up to kMaxGeneralItems
-  if (n_items > kMaxGeneralItems) return Status::Ok();
-  const size_t lds = size_t(n_items) * 4;
-  db_ = std::min(1024, int((kLdsBudget - lds - 4) / 12));
-  if (db_ < 32) return Status{1, "n_items too large for the LDS row plus descriptors"};
-  const size_t lds2 = size_t(db_) * 12 + 4 + lds;
-  for (const void *k : {reinterpret_cast<const void *>(k_accumulate2<16, false>),
-                        reinterpret_cast<const void *>(k_accumulate2<4, true>)})
-    COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2)));
+  // run_sparse (cooc_sparse.hip) sets its own attributes; the batch planner keeps one LDS row
+  if (n_items >= kBatchMaxItems) return Status::Ok();
   for (const void *k : {reinterpret_cast<const void *>(k_acc_batch<4, 16, true>),
                         reinterpret_cast<const void *>(k_acc_batch<4, 8, false>)})
     COOC_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsBudget));
@@ -1488,229 +1113,12 @@ void Counter::release() {
   DevBuf *all[] = {&dense_, &bh_, &uidx_, &long_, &rcnt_, &desc_, &keys_in_, &vals_in_, &keys_out_, &vals_out_,
                    &sort_tmp_, &epre_, &row_ptr_, &row_work_, &row_nch_, &row_cap_, &row_split_, &order_keys_,
                    &order_, &ord_nch_, &ord_cbase_, &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_,
-                   &col_, &cnt_, &staging_, &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_, &seg_,
-                   &split_sum_, &tarena_, &bump_, &seg_off_, &plen_, &poff_, &vpre_, &send_, &witems_, &sp_arena_, &sp_tb_,
+                   &col_, &cnt_, &staging_, &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_,
+                   &split_sum_, &tarena_, &bump_, &seg_off_, &plen_, &poff_, &send_, &witems_, &sp_arena_, &sp_tb_,
                    &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_, &sp_pbase_, &sp_scr_, &sp_hz_, &sp_spre_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
-}
-
-// Plan, accumulate and compact given the per-contribution work prefix (epre) and segment starts
-// (seg) of a window (general planner, one LDS row per chunk).
-Status Counter::run_tile(const uint16_t *arena, int64_t n, hipStream_t s, KernelTimer *timer) {
-  const int32_t M = M_;
-  int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
-  PlanTotals *tot = tot_.as<PlanTotals>();
-  uint64_t *okeys = order_keys_.as<uint64_t>();
-  int32_t *order = order_.as<int32_t>();
-  k_plan_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_work_.as<uint64_t>(), order + M,
-                                                 row_nch_.as<int32_t>(), row_split_.as<int32_t>());
-  COOC_HIP_TRY(hipGetLastError());
-  size_t b = sort_tmp_.cap;
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, row_work_.as<uint64_t>(), okeys,
-                                                            order + M, order, M, 0, 64, s));
-  k_gather_i32<<<blocks_for(M, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), M, ord_nch_.as<int32_t>());
-  COOC_HIP_TRY(hipMemsetAsync(ord_cbase_.p, 0, sizeof(int32_t), s));
-  COOC_HIP_TRY(hipMemsetAsync(split_slot_.p, 0, sizeof(int32_t), s));
-  b = sort_tmp_.cap;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
-                                                M, s));
-  b = sort_tmp_.cap;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
-                                                split_slot_.as<int32_t>() + 1, M, s));
-  k_split_rows<<<blocks_for(M, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), M,
-                                                  split_row_.as<int32_t>());
-  k_totals<<<1, 1, 0, s>>>(ord_cbase_.as<int32_t>(), split_slot_.as<int32_t>(), M, tot, queue_.as<int32_t>());
-  COOC_HIP_TRY(hipGetLastError());
-  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
-  COOC_HIP_TRY(hipStreamSynchronize(s));
-  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
-  const int64_t n_chunks = h_tot_->n_chunks, n_split = h_tot_->n_split;
-  if (n_chunks == 0) return Status::Ok();
-  COOC_TRY(chunks_.reserve(sizeof(Chunk) * (n_chunks + 1)));
-  COOC_TRY(split_sum_.reserve(sizeof(int64_t) * (n_split + 1)));
-  COOC_HIP_TRY(hipMemsetAsync(split_sum_.p, 0, sizeof(int64_t) * (n_split + 1), s));
-  if (n_split > 0) {
-    const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(M);
-    COOC_TRY(staging_.reserve(need));
-    COOC_HIP_TRY(hipMemsetAsync(staging_.p, 0, need, s));
-  }
-  k_make_chunks<<<blocks_for(M, 256), 256, 0, s>>>(order, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), row_ptr,
-                                                   epre, split_slot_.as<int32_t>(), M, chunks_.as<Chunk>());
-  COOC_HIP_TRY(hipGetLastError());
-  // ★ accumulate
-  const int64_t grid = std::min<int64_t>(n_chunks, n_cu_);
-  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-  auto kern = vec_ ? k_accumulate2<4, true> : k_accumulate2<16, false>;
-  kern<<<unsigned(grid), kAccThreads, size_t(db_) * 12 + 4 + size_t(M) * 4, s>>>(
-      chunks_.as<Chunk>(), tot, queue_.as<int32_t>(), seg_.as<int64_t>(), arena, epre, vpre_.as<int64_t>(), M, db_,
-      row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(), cnt_.as<uint32_t>(),
-      staging_.as<uint32_t>(), split_sum_.as<int64_t>(), rowsum_.as<int64_t>(), reinterpret_cast<int64_t *>(&tot->err));
-  COOC_HIP_TRY(hipGetLastError());
-  if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
-  if (n_split > 0) {
-    const int64_t g2 = std::min<int64_t>(n_split, 4 * int64_t(n_cu_));
-    k_finalize_split<<<unsigned(g2), kAccThreads, 0, s>>>(tot, split_row_.as<int32_t>(), M, staging_.as<uint32_t>(),
-                                                          row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-                                                          col_.as<int32_t>(), cnt_.as<uint32_t>(),
-                                                          split_sum_.as<int64_t>(),
-                                                          reinterpret_cast<int64_t *>(&tot->err), nullptr, 0);
-    COOC_HIP_TRY(hipGetLastError());
-  }
-  return Status::Ok();
-}
-
-Status Counter::run(const ActiveUsers &au, hipStream_t s, CountResult *out, KernelTimer *timer) {
-  const int32_t M = M_;
-  dense_mode_ = false;
-  last_rows_ = M;
-  const int64_t n = au.n_contrib;
-  if (M > kMaxGeneralItems || db_ < 32)
-    return Status{1, "n_items > " + std::to_string(kMaxGeneralItems) +
-                         " is supported for one-window batches (cooc_count_device), not for streaming windows"};
-  if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
-  // ---- workspace
-  COOC_TRY(keys_in_.reserve(sizeof(uint32_t) * (n + 1)));
-  COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n + 1)));
-  COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n + 1)));
-  COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n + 1)));
-  COOC_TRY(epre_.reserve(sizeof(int64_t) * (n + 1)));
-  COOC_TRY(seg_.reserve(sizeof(int64_t) * (n + 1)));
-  COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
-  COOC_TRY(row_work_.reserve(sizeof(uint64_t) * M));
-  COOC_TRY(order_keys_.reserve(sizeof(uint64_t) * M));
-  COOC_TRY(order_.reserve(sizeof(int32_t) * M * 2));
-  COOC_TRY(row_nch_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(row_cap_.reserve(sizeof(int64_t) * M));
-  COOC_TRY(row_split_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(ord_nch_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(ord_cbase_.reserve(sizeof(int32_t) * (M + 1)));
-  COOC_TRY(row_base_.reserve(sizeof(int64_t) * (M + 1)));
-  COOC_TRY(split_slot_.reserve(sizeof(int32_t) * (M + 1)));
-  COOC_TRY(split_row_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
-  COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));
-  COOC_TRY(row_nnz_.reserve(sizeof(int32_t) * M));
-  COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
-
-  uint32_t *keys_in = keys_in_.as<uint32_t>(), *vals_in = vals_in_.as<uint32_t>();
-  uint32_t *keys = keys_out_.as<uint32_t>(), *vals = vals_out_.as<uint32_t>();
-  int64_t *epre = epre_.as<int64_t>(), *row_ptr = row_ptr_.as<int64_t>();
-  PlanTotals *tot = tot_.as<PlanTotals>();
-
-  COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
-  COOC_HIP_TRY(hipMemsetAsync(rowsum_.p, 0, sizeof(int64_t) * M, s));
-  COOC_HIP_TRY(hipMemsetAsync(row_nnz_.p, 0, sizeof(int32_t) * M, s));
-  COOC_HIP_TRY(hipMemsetAsync(epre, 0, sizeof(int64_t), s));
-
-  // 1. contributions
-  if (au.n_active > 0) {
-    const int64_t waves = au.n_active < 65536 ? au.n_active : 65536;
-    k_build_contribs<<<blocks_for(waves * 64, 256), 256, 0, s>>>(au.n_active, au.off, au.len, au.old, au.cbase,
-                                                                  au.arena, M, keys_in, vals_in,
-                                                                  reinterpret_cast<int64_t *>(&tot->err));
-    COOC_HIP_TRY(hipGetLastError());
-  }
-  // temp storage for every hipCUB call of the run
-  size_t tmp_bytes = 0, q = 0;
-  const int nb = key_bits(M);
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
-  tmp_bytes = std::max(tmp_bytes, q);
-  hipcub::TransformInputIterator<int64_t, WorkOp, const uint32_t *> work_it(vals, WorkOp{au.len, au.old});
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, work_it, epre + 1, int(n), s));
-  tmp_bytes = std::max(tmp_bytes, q);
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, row_work_.as<uint64_t>(),
-                                                            order_keys_.as<uint64_t>(), order_.as<int32_t>() + M,
-                                                            order_.as<int32_t>(), M, 0, 64, s));
-  tmp_bytes = std::max(tmp_bytes, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_cap_.as<int64_t>(), row_base_.as<int64_t>() + 1, M, s));
-  tmp_bytes = std::max(tmp_bytes, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, M, s));
-  tmp_bytes = std::max(tmp_bytes, q);
-  COOC_TRY(sort_tmp_.reserve(tmp_bytes));
-
-  // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152); 4. pair-work prefix
-  if (n > 0) {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, nb, s));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, work_it, epre + 1, int(n), s));
-  }
-  // 3. row pointer; output capacity per row (padded CSR)
-  k_row_ptr<<<blocks_for(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
-  k_row_cap<<<blocks_for(M, 256), 256, 0, s>>>(row_ptr, epre, M, row_cap_.as<int64_t>());
-  COOC_HIP_TRY(hipMemsetAsync(row_base_.p, 0, sizeof(int64_t), s));
-  {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_cap_.as<int64_t>(),
-                                                  row_base_.as<int64_t>() + 1, M, s));
-  }
-  k_cap_total<<<1, 1, 0, s>>>(row_base_.as<int64_t>(), epre, M, n, tot);
-  COOC_HIP_TRY(hipGetLastError());
-  COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
-  COOC_HIP_TRY(hipStreamSynchronize(s));
-  if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
-  const int64_t cap = h_tot_->cap_total, work_total = h_tot_->work_total;
-  COOC_TRY(col_.reserve(sizeof(int32_t) * (cap + 1)));
-  COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap + 1)));
-
-  vec_ = au.n_new == au.n_contrib && n > 0;  // one-window batch: all kind 0
-  if (vec_) {
-    const int64_t U = au.n_active;
-    COOC_TRY(plen_.reserve(sizeof(int64_t) * (U + 1)));
-    COOC_TRY(poff_.reserve(sizeof(int64_t) * (U + 1)));
-    COOC_TRY(vpre_.reserve(sizeof(int64_t) * (n + 1)));
-    k_pad_lens<<<blocks_for(U, 256), 256, 0, s>>>(U, au.len, plen_.as<int64_t>());
-    COOC_HIP_TRY(hipMemsetAsync(poff_.p, 0, sizeof(int64_t), s));
-    COOC_HIP_TRY(hipMemsetAsync(vpre_.p, 0, sizeof(int64_t), s));
-    hipcub::TransformInputIterator<int64_t, PadLenOp, const uint32_t *> pad_it(vals, PadLenOp{plen_.as<int64_t>()});
-    size_t b1 = 0, b2 = 0;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b1, plen_.as<int64_t>(), poff_.as<int64_t>() + 1, int(U), s));
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, pad_it, vpre_.as<int64_t>() + 1, int(n), s));
-    COOC_TRY(sort_tmp_.reserve(std::max(b1, b2)));
-    b1 = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b1, plen_.as<int64_t>(), poff_.as<int64_t>() + 1, int(U), s));
-    b2 = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b2, pad_it, vpre_.as<int64_t>() + 1, int(n), s));
-    int64_t padded = 0;
-    COOC_HIP_TRY(hipMemcpyAsync(&padded, poff_.as<int64_t>() + U, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    COOC_HIP_TRY(hipStreamSynchronize(s));
-    COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (padded + 16)));
-    k_narrow_pad<<<std::min<unsigned>(blocks_for(U * 64, 256), 16384), 256, 0, s>>>(
-        U, au.off, au.len, poff_.as<int64_t>(), au.arena, tarena_.as<uint16_t>());
-    k_seg_start_pad<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, poff_.as<int64_t>(), seg_.as<int64_t>());
-    COOC_HIP_TRY(hipGetLastError());
-    COOC_TRY(run_tile(tarena_.as<uint16_t>(), n, s, timer));
-  } else {
-    if (n > 0) {
-      k_seg_start<<<blocks_for(n, 256), 256, 0, s>>>(vals, n, au.off, au.old, seg_.as<int64_t>());
-      COOC_HIP_TRY(hipGetLastError());
-    }
-    const uint16_t *a16 = au.arena16;
-    if (!a16) {  // narrow the arena range the contributions reference
-      const int64_t span = au.arena_span;
-      COOC_TRY(tarena_.reserve(sizeof(uint16_t) * (span + 8)));
-      if (span > 0) {
-        k_narrow<<<blocks_for((span + 3) / 4, 256), 256, 0, s>>>(au.arena, span, tarena_.as<uint16_t>());
-        COOC_HIP_TRY(hipGetLastError());
-      }
-      a16 = tarena_.as<uint16_t>();
-    }
-    COOC_TRY(run_tile(a16, n, s, timer));
-  }
-  k_nnz_total<<<std::min<unsigned>(blocks_for(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
-  COOC_HIP_TRY(hipGetLastError());
-
-  out->row_base = row_base_.as<int64_t>();
-  out->row_nnz = row_nnz_.as<int32_t>();
-  out->col = col_.as<int32_t>();
-  out->cnt = cnt_.as<uint32_t>();
-  out->rowsum = rowsum_.as<int64_t>();
-  out->work = work_total;
-  out->observed = work_total - au.n_new;
-  out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
-  return Status::Ok();
 }
 
 Status Counter::read_totals(PlanTotals *t) {

@@ -37,6 +37,7 @@ Status cooc_ctx::init(const cooc_config &c) {
   COOC_TRY(counter.init(c.n_items));
   counter.set_output_layout((c.flags & COOC_FLAG_OUTPUT_DENSE) ? 2 : (c.flags & COOC_FLAG_OUTPUT_CSR) ? 1 : 0);
   counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0);
+  counter.set_sort_rows((c.flags & COOC_FLAG_SORT_ROWS) != 0);
   return Status::Ok();
 }
 
@@ -46,7 +47,7 @@ cooc_ctx::~cooc_ctx() {
   stream_state.release();
   sharder.release();
   counter.release();
-  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_off, &b_len, &b_old, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
+  cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
                           &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms, &b_verify};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
@@ -64,10 +65,8 @@ Status cooc_ctx::count_device(int64_t n_users, const int64_t *d_user_ptr, const 
   cooc::CountResult r;
   if (counter.batch_ok()) {
     COOC_TRY(counter.run_batch(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
-  } else if (counter.sparse()) {
-    COOC_TRY(counter.run_sparse(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
   } else {
-    COOC_TRY(count_general(n_users, d_user_ptr, d_items, n_interactions, s, &r));
+    COOC_TRY(counter.run_sparse(n_users, d_user_ptr, d_items, n_interactions, s, &r, timer.enabled ? &timer : nullptr));
   }
   return finish_batch(r, s, out);
 }
@@ -105,27 +104,6 @@ Status cooc_ctx::apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, con
   *d_items = b_cut_items.as<int32_t>();
   *n_interactions = n_cut;
   return Status::Ok();
-}
-
-cooc::Status cooc_ctx::count_general(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
-                                     int64_t n_interactions, hipStream_t s, cooc::CountResult *r) {
-  const int64_t n_act = std::max<int64_t>(n_users, 1);
-  COOC_TRY(b_off.reserve(sizeof(int64_t) * n_act));
-  COOC_TRY(b_len.reserve(sizeof(int32_t) * n_act));
-  COOC_TRY(b_old.reserve(sizeof(int32_t) * n_act));
-  COOC_TRY(cooc::launch_iota_users(s, n_users, d_user_ptr, b_off.as<int64_t>(), b_len.as<int32_t>(),
-                                   b_old.as<int32_t>()));
-  cooc::ActiveUsers au;
-  au.n_active = n_users;
-  au.off = b_off.as<int64_t>();
-  au.len = b_len.as<int32_t>();
-  au.old = b_old.as<int32_t>();
-  au.cbase = d_user_ptr;  // contributions are the interactions themselves (user_ptr[0] == 0)
-  au.n_contrib = n_interactions;
-  au.n_new = n_interactions;
-  au.arena = d_items;
-  au.arena_span = n_interactions;
-  return counter.run(au, s, r, timer.enabled ? &timer : nullptr);
 }
 
 cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, cooc_device_result *out) {

@@ -124,8 +124,6 @@ struct cooc_ctx {
   // user_cut > 0: replaces the CSR by its capped copy (b_cut_*); no-op otherwise
   cooc::Status apply_user_cut(int64_t n_users, const int64_t **d_user_ptr, const int32_t **d_items,
                               int64_t *n_interactions, hipStream_t s);
-  cooc::Status count_general(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
-                             int64_t n_interactions, hipStream_t s, cooc::CountResult *r);
   cooc::Status finish_batch(const cooc::CountResult &r, hipStream_t s, cooc_device_result *out);
   cooc::Status count_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_window_info *info);
   cooc::Status copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
@@ -156,7 +154,7 @@ struct cooc_ctx {
   cooc::Operator op;
 
   // stateless batch buffers
-  cooc::DevBuf b_user_ptr, b_items, b_off, b_len, b_old, b_tk_size, b_tk_val, b_tk_score, b_obs3, b_llr_terms;
+  cooc::DevBuf b_user_ptr, b_items, b_tk_size, b_tk_val, b_tk_score, b_obs3, b_llr_terms;
   // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
   cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
   cooc::DevBuf b_verify;  // cooc_verify_batch totals

@@ -100,6 +100,7 @@ struct PlanTotals {
   int64_t n_gather;       // bucket-start slots handed out by the queue builder
   int64_t bad_row;        // a row whose counts failed the row-sum check (err bit 1), for the message
   int64_t self_total;     // contributions whose walk includes their own position (pairs p == p removed)
+  int64_t n_deferred;     // whole rows handed to the sort + segmented-reduce path (hash table overflow)
 };
 
 // One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR
@@ -138,10 +139,6 @@ class Counter {
   void release();
   ~Counter() { release(); }
 
-  // Expand + reduce the given contributions; returns the padded CSR.  Synchronises `stream`
-  // once (to size the output).
-  Status run(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
-
   // One window over empty histories straight from a device CSR (user_ptr int64[U+1], items
   // int32[N]): the batch planner (per-block item histograms -> transpose of A by counting sort) and
   // k_acc_batch.  Needs n_items < kBatchMaxItems (one LDS row + pad sink + descriptors); returns the same padded
@@ -149,6 +146,7 @@ class Counter {
   Status run_batch(int64_t n_users, const int64_t *user_ptr, const int32_t *items, int64_t n, hipStream_t stream,
                    CountResult *out, KernelTimer *timer = nullptr);
   bool batch_ok() const { return M_ < kBatchMaxItems && !general_only_; }
+  // the large-universe planner: n_items >= kBatchMaxItems, or any n_items with COOC_FLAG_GENERAL_PLANNER
   // n_items >= kBatchMaxItems: one window over empty histories through the large-universe path
   // (cooc_sparse.hip: per-row workgroups, LDS hash / dense-tile chunks, split staging rows).  Same
   // padded CSR result as run().  Synchronises `stream` twice (plan totals, output-region check).
@@ -159,13 +157,11 @@ class Counter {
                     CountResult *out, KernelTimer *timer = nullptr, const int32_t *owner = nullptr,
                     int32_t part = 0, const int64_t *freq = nullptr, int64_t n_freq = 0,
                     const SparseWindow *win = nullptr);
-  bool sparse() const { return M_ >= kBatchMaxItems; }
-  // run() (the streaming general planner) keeps one LDS row per chunk: n_items <= kMaxGeneralItems
-  static constexpr int32_t kMaxGeneralItems = 40704;
+  bool sparse() const { return M_ >= kBatchMaxItems || general_only_; }
   // A streaming window (resident histories) through the batch planner and k_acc_batch; needs
   // batch_ok().  Same padded CSR result as run().  Synchronises `stream` once.
   Status run_window(const ActiveUsers &au, hipStream_t stream, CountResult *out, KernelTimer *timer = nullptr);
-  // COOC_FLAG_GENERAL_PLANNER: every window through run() (the sort-based general planner).
+  // COOC_FLAG_GENERAL_PLANNER: every window through the large-universe planner (run_sparse).
   void set_general_only(bool g) { general_only_ = g; }
 
   // Sharded records (W parts, owner(a) = a mod W).  shard_plan: this part's users -> its padded
@@ -181,6 +177,11 @@ class Counter {
                      const uint16_t *arena_all, int64_t arena_stride, hipStream_t stream, CountResult *out,
                      KernelTimer *timer = nullptr);
   int32_t last_rows() const { return last_rows_; }
+  // COOC_FLAG_SORT_ROWS: every whole row of the large-universe path through the sort + segmented-reduce
+  // path (otherwise only rows whose LDS hash table overflowed); rows and pairs it took in the last run
+  void set_sort_rows(bool on) { sort_rows_ = on; }
+  int64_t last_deferred_rows() const { return last_deferred_; }
+  int64_t last_deferred_pairs() const { return last_deferred_pairs_; }
   static constexpr int32_t kBatchMaxItems = 40320;
 
   // Output layout of run_batch: 0 = auto (dense when P >= M^2 / 2), 1 = sparse CSR, 2 = dense.
@@ -200,7 +201,6 @@ class Counter {
   int32_t n_items() const { return M_; }
 
  private:
-  Status run_tile(const uint16_t *arena, int64_t n, hipStream_t s, KernelTimer *timer);
   Status plan_local(int64_t U, const int64_t *up, const int32_t *items, int64_t n, int32_t W, hipStream_t s,
                     uint64_t *desc, uint16_t *arena, int64_t arena_cap, const int32_t *old = nullptr,
                     const int64_t *hoff = nullptr);
@@ -209,18 +209,16 @@ class Counter {
                          hipStream_t s, CountResult *out, KernelTimer *timer);
 
   int32_t M_ = 0;
-  int db_ = 0;       // segment descriptors staged per batch (general planner)
   int n_cu_ = 256;
   // workspace
   DevBuf keys_in_, vals_in_, keys_out_, vals_out_, sort_tmp_, epre_;
   DevBuf row_ptr_, row_work_, row_nch_, row_cap_, row_split_, order_keys_, order_;
   DevBuf ord_nch_, ord_cbase_, row_base_, split_slot_, split_row_, chunks_, tot_, queue_;
   DevBuf col_, cnt_, staging_, row_nnz_, rowsum_;
-  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, seg_, split_sum_, tarena_;
+  DevBuf pk_row_ptr_, pk_col_, pk_cnt_, split_sum_, tarena_;
   int64_t bump_cap_ = 0;    // k_acc_batch sparse output: entries in the bump region
   DevBuf bump_, seg_off_;  // seg_off_: sharded records, per (source, owned row) segment offsets
-  bool vec_ = false;        // general planner: 16-B partner-id loads over a padded arena (one-window batch)
-  DevBuf plen_, poff_, vpre_;
+  DevBuf plen_, poff_;
   DevBuf bh_, uidx_, long_, rcnt_, desc_;  // batch planner: block histograms, user of each interaction,
                                            // long lists, row counts, descriptors
   int output_pref_ = 0;               // set_output_layout
@@ -229,15 +227,17 @@ class Counter {
   // large-universe path: tile-grouped arena, tile starts, per-row work and plan, estimates, queue
   DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_, sp_pbase_, sp_scr_, sp_hz_;
   DevBuf sp_spre_;  // streaming windows: prefix of the contributions' self flags
+  // sort + segmented-reduce path of deferred rows: the deferred list, keys (x2), runs, per-batch tables
+  DevBuf sp_defer_, sr_keys_, sr_ukeys_, sr_ucnt_, sr_aux_;
+  int64_t last_deferred_ = 0, last_deferred_pairs_ = 0;
+  bool sort_rows_ = false;  // COOC_FLAG_SORT_ROWS
+  Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
+                      const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;
   int32_t last_rows_ = 0;             // rows of the last batch result (n_items, or the owned rows)
   static constexpr int64_t chunk_work_ = int64_t(1) << 22;  // pairs per chunk of the batch planner
   PlanTotals *h_tot_ = nullptr;  // pinned
 };
-
-// Launch wrappers for the streaming state (cooc_stream.hip).
-Status launch_iota_users(hipStream_t s, int64_t n_users, const int64_t *user_ptr, int64_t *off, int32_t *len,
-                         int32_t *old);
 
 // Item frequencies of a device item array into counts int64[M] (zeroed first); ids outside [0, M) are
 // not counted.

@@ -137,6 +137,8 @@ struct SpArgs {
   int64_t scr_cap;          // 0: gather mode off
   const int64_t *rowsum;    // [M] closed-form row sums W_a - c_a (k_sp_plan): every whole row is checked
   const int64_t *spre;      // streaming window: [n_contrib + 1] prefix of the kSelfBit flags; NULL: all set
+  int32_t *deferred;        // [M] whole rows left to the sort + segmented-reduce path (k_sr_*), in tot->n_deferred
+  int32_t sort_all;         // COOC_FLAG_SORT_ROWS: every whole row goes to that path (A/B and tests)
 };
 
 #ifdef COOC_SP_TRACE
@@ -644,7 +646,7 @@ struct SpStatic {
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
   unsigned long long rsum;          // the current whole row's compacted counts, summed (row-sum check)
 #ifdef COOC_SP_STATS
-  unsigned long long st[28];
+  unsigned long long st[48];
 #endif
 };
 
@@ -1124,7 +1126,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
   }
   const int64_t n_work = A.tot->n_chunks;
 #ifdef COOC_SP_STATS
-  if (threadIdx.x < 28) S_.st[threadIdx.x] = 0ull;
+  if (threadIdx.x < 48) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -1190,8 +1192,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     }
     __syncthreads();
     gather = gather && uni(S_.bstart[A.T]) <= uint32_t(A.scr_cap);
-    int dense_until = split ? t_end : -1;  // tiles below it go dense (split items; hash overflow fallback)
-    int32_t H = 0;                         // 0: table size from the estimate
+    const int dense_until = split ? t_end : -1;  // tiles below it go dense (split items)
+    int32_t H = 0;                               // 0: table size from the estimate
+    // a whole row whose hash table overflows (more distinct keys than the planner expected) is handed to
+    // the sort + segmented-reduce path (k_sr_*, after this kernel) whole: its entries so far are dropped
+    bool deferred = !split && A.sort_all;
+    if (deferred) t = t_end;
     while (t < t_end) {
       // ---- this chunk: tiles [t, t1), dense or hash
       const bool dense = t < dense_until || ((dn >> t) & 1ull);
@@ -1235,23 +1241,29 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       }
       const unsigned long long c_walked = STAT_CLOCK();
       STAT_ADD(split ? 4 : dense ? 0 : 1, c_walked - c_walk);
+#ifdef COOC_SP_STATS
+      // hash chunk classes: 0 = a light row (one hash chunk over every tile), 1 = a gathered tile range
+      // (buckets), 2 = any other (walks the lists over its tile range)
+      const int hcls = (!split && t == 0 && t1 == t_end) ? 0 : (gather && t > 0) ? 1 : 2;
+      if (!dense && !split) {
+        STAT_ADD(28 + 6 * hcls, 1);
+        STAT_ADD(29 + 6 * hcls, c_walked - c_walk);
+        STAT_ADD(31 + 6 * hcls, walked);
+        STAT_ADD(33 + 6 * hcls, k1 - k0);
+      }
+#endif
       STAT_ADD(dense ? 9 : 10, walked);
       STAT_ADD(dense ? 5 : 6, 1);
       if (!dense && uni(S_.flag)) {
-        STAT_ADD(H < kHashMax ? 7 : 8, 1);
-        // overflow: clear the table; retry with a 4x table, at the largest size as dense tiles
+        STAT_ADD(7, 1);
+        // overflow: clear the table (and the gather walk's state is this item's only); the row is deferred
         for (int32_t j = tid; j < H; j += kSpThreads) {
           L.R[j] = 0u;
           L.R[kHashMax + j] = 0u;
         }
-        if (H < kHashMax) {
-          H = min(kHashMax, H * 4);
-        } else {
-          dense_until = t1;
-          H = 0;
-        }
-        __syncthreads();  // every wave has read the flag before the retry resets it
-        continue;
+        deferred = true;
+        __syncthreads();  // every wave has read the flag and cleared its slots
+        break;
       }
       // the -1 at column a per contribution whose walk includes its own position (whole rows)
       const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
@@ -1284,12 +1296,24 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
         __syncthreads();
         sp_hash_compact(A, L, S_, H, c0, c1, rsum);
         STAT_ADD(3, STAT_CLOCK() - c_walked);
+#ifdef COOC_SP_STATS
+        STAT_ADD(30 + 6 * hcls, STAT_CLOCK() - c_walked);
+        STAT_ADD(32 + 6 * hcls, uni(S_.row_n));
+#endif
         STAT_ADD(14, H);
       }
       t = t1;
       H = 0;
     }
     STAT_ADD(split ? 12 : 11, 1);
+    if (deferred) {
+      STAT_ADD(8, 1);
+      rsum = 0;
+      if (tid == 0) {
+        A.deferred[atomicAdd(reinterpret_cast<unsigned long long *>(&A.tot->n_deferred), 1ull)] = a;
+        S_.row_n = 0;  // (the row's rows so far are abandoned; its region space is not reused)
+      }
+    }
     if (!split) {  // the row-sum check: every count of the row, summed exactly (u64), == W_a - c_a
       for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
       if ((tid & 63) == 0 && rsum) atomicAdd(&S_.rsum, (unsigned long long)rsum);
@@ -1306,7 +1330,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     if (tid == 0) S_.work = next;
     __syncthreads();
     // a uint32 counter that wrapped, or any id lost or counted twice, breaks the sum
-    if (!split && tid == 0 && S_.rsum != (unsigned long long)rs_expect) {
+    if (!split && !deferred && tid == 0 && S_.rsum != (unsigned long long)rs_expect) {
       atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
       A.tot->bad_row = a;
     }
@@ -1314,7 +1338,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
 #ifdef COOC_SP_STATS
   if (tid == 0) {
     S_.st[13] = STAT_CLOCK() - t_start;
-    for (int k = 0; k < 28; k++) atomicAdd(A.stats + k, S_.st[k]);
+    for (int k = 0; k < 48; k++) atomicAdd(A.stats + k, S_.st[k]);
   }
 #endif
 }
@@ -1440,8 +1464,135 @@ __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict
                                unsigned long long *__restrict__ bump) {
   tot->err &= ~int64_t(6);  // the region (4) and row-sum (2) checks of the previous attempt
   tot->nnz_total = 0;
+  tot->n_deferred = 0;
   qctr[0] = 0;
   bump[0] = 0;
+}
+
+// ---- the sort + segmented-reduce path (rows whose LDS hash table overflowed; COOC_FLAG_SORT_ROWS: all) ----
+// The north star's overflow fallback for the per-row Int2ShortOpenHashMap (ItemRowAggregator.java:21-31):
+// every pair of the deferred rows becomes one packed 64-bit key (row slot << 32 | partner id), the keys
+// are radix-sorted (hipCUB onesweep: wave-level digit ranking in LDS), runs of equal keys are counted
+// (DeviceRunLengthEncode: the segmented reduce of the +1 increments) and each row's runs are written as
+// its padded-CSR slice, in column order, with the same row-sum check as k_sp_main.  Deferred rows are
+// processed in batches of at most kSrBatchPairs pairs.
+constexpr int kSrThreads = 256;
+
+// One workgroup per deferred row of the batch: every contribution's list (the whole tile-grouped list,
+// sinks skipped) appended to the row's key range at kbase[j] + (epre[k] - epre[k0]), in list order.
+__global__ __launch_bounds__(kSrThreads) void k_sr_expand(const int32_t *__restrict__ rows, const int64_t *__restrict__ kbase,
+                                                          const int64_t *__restrict__ row_ptr,
+                                                          const int64_t *__restrict__ epre,
+                                                          const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb,
+                                                          const uint4 *__restrict__ tarena, int32_t T,
+                                                          uint64_t *__restrict__ keys) {
+  const int j = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int32_t a = rows[j];
+  const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1], e0 = epre[k0];
+  const uint64_t tag = uint64_t(j) << 32;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int64_t k = k0 + wave; k < k1; k += kSrThreads / 64) {
+    const uint32_t u = vals[k] & kListMask;
+    const int32_t g0 = tb[int64_t(u) * (T + 1)], g1 = tb[int64_t(u) * (T + 1) + T];
+    uint64_t *o = keys + kbase[j] + (epre[k] - e0);
+    int64_t pos = 0;
+    for (int32_t g = g0; g < g1; g += 64) {
+      uint4 v = make_uint4(kSink, kSink, kSink, kSink);
+      if (g + lane < g1) v = tarena[g + lane];
+      const uint32_t id[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t c = (v.x != kSink) + (v.y != kSink) + (v.z != kSink) + (v.w != kSink);
+      const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
+      int64_t q = pos + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (id[i] != kSink) o[q++] = tag | id[i];
+      pos += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2);
+    }
+  }
+}
+
+// First run of every row slot j of the batch (runs are sorted by (slot, column)): rstart[j] = lower bound
+// of j << 32 in the run keys; rstart[nb] = the run count.
+__global__ void k_sr_bounds(const uint64_t *__restrict__ ukeys, const int64_t *__restrict__ n_runs_p, int32_t nb,
+                            int64_t *__restrict__ rstart) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > nb) return;
+  const int64_t n = *n_runs_p;
+  int64_t lo = 0, hi = n;
+  const uint64_t key = uint64_t(j) << 32;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (ukeys[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  rstart[j] = lo;
+}
+
+// One workgroup per row slot: the row's runs -> (column, count) entries in column order at an exactly
+// sized bump reservation; the diagonal run loses the row's self term (and is dropped at zero); the counts
+// must add up to the closed-form row sum (err bit 1 with bad_row otherwise, as in k_sp_main).
+__global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restrict__ rows, const int64_t *__restrict__ rstart,
+                                                        const uint64_t *__restrict__ ukeys,
+                                                        const uint32_t *__restrict__ ucnt,
+                                                        const int64_t *__restrict__ row_ptr,
+                                                        const int64_t *__restrict__ spre,
+                                                        const int64_t *__restrict__ rowsum,
+                                                        int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
+                                                        unsigned long long *__restrict__ bump, int64_t cap,
+                                                        int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+                                                        PlanTotals *__restrict__ tot) {
+  __shared__ int64_t s_diag, s_base;
+  __shared__ unsigned long long s_sum;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int32_t a = rows[j];
+  const int64_t r0 = rstart[j], r1 = rstart[j + 1];
+  const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1];
+  const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
+  if (tid == 0) {
+    s_diag = -1;
+    s_sum = 0ull;
+  }
+  __syncthreads();
+  uint64_t sum = 0;
+  for (int64_t r = r0 + tid; r < r1; r += kSrThreads) {
+    sum += ucnt[r];
+    if (uint32_t(ukeys[r]) == uint32_t(a)) s_diag = r;
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if ((tid & 63) == 0) atomicAdd(&s_sum, (unsigned long long)sum);
+  __syncthreads();
+  const int64_t diag = s_diag;
+  const bool drop = diag >= 0 && ucnt[diag] == self;
+  const int64_t n = (r1 - r0) - (drop ? 1 : 0);
+  if (tid == 0) {
+    int64_t b = n > 0 ? int64_t(atomicAdd(bump, (unsigned long long)n)) : 0;
+    if (b + n > cap) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 4ull);
+      b = -1;
+    }
+    s_base = b;
+    row_base[a] = b < 0 ? 0 : b;
+    row_nnz[a] = b < 0 ? 0 : int32_t(n);
+    // self pairs are part of the sums of the runs; a diagonal run below the self term is an error too
+    if (s_sum != (unsigned long long)(rowsum[a] + self) || (self && (diag < 0 || ucnt[diag] < self))) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+      tot->bad_row = a;
+    }
+  }
+  __syncthreads();
+  const int64_t base = s_base;
+  if (base < 0) return;
+  for (int64_t r = r0 + tid; r < r1; r += kSrThreads) {
+    if (drop && r == diag) continue;
+    const int64_t q = base + (r - r0) - (drop && r > diag ? 1 : 0);
+    col_out[q] = int32_t(uint32_t(ukeys[r]));
+    cnt_out[q] = ucnt[r] - (r == diag ? self : 0u);
+  }
+}
+
+__global__ void k_sr_pair_work(const int32_t *__restrict__ rows, int64_t n, const int64_t *__restrict__ row_w,
+                               int64_t *__restrict__ out) {
+  const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) out[j] = row_w[rows[j]];
 }
 
 inline unsigned nblocks(int64_t n, int t) { return unsigned((n + t - 1) / t); }
@@ -1713,7 +1864,6 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
   cap = std::max<int64_t>(1, std::min(cap, budget));
-  vec_ = false;
   dense_mode_ = false;
   last_rows_ = M;
   COOC_TRY(bump_.reserve(sizeof(uint64_t) * 2));
@@ -1740,6 +1890,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   proto.rowsum = rowsum_.as<int64_t>();
   proto.spre = spre;
+  COOC_TRY(sp_defer_.reserve(sizeof(int32_t) * size_t(M)));
+  proto.deferred = sp_defer_.as<int32_t>();
+  proto.sort_all = sort_rows_ ? 1 : 0;
   int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
@@ -1765,8 +1918,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
 #ifdef COOC_SP_STATS
     static unsigned long long *d_stats = nullptr;
-    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 28 * 8);
-    hipMemsetAsync(d_stats, 0, 28 * 8, s);
+    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 48 * 8);
+    hipMemsetAsync(d_stats, 0, 48 * 8, s);
     A.stats = d_stats;
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
@@ -1806,18 +1959,27 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       COOC_HIP_TRY(hipGetLastError());
     }
   SPT("finalize");
+    COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+    int64_t err = h_tot_->err;
+    const int64_t n_def = h_tot_->n_deferred;
+    last_deferred_ = n_def;
+    last_deferred_pairs_ = 0;
+    if (n_def > 0 && !(err & 4)) {  // rows whose hash table overflowed (all whole rows: COOC_FLAG_SORT_ROWS)
+      COOC_TRY(run_deferred(n_def, T, row_ptr, epre, vals, spre, cap, s));
+      COOC_HIP_TRY(hipMemcpyAsync(&err, &tot->err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      COOC_HIP_TRY(hipStreamSynchronize(s));
+    }
+  SPT("deferred");
     k_sp_nnz_total<<<std::min<unsigned>(nblocks(M, 256), 64), 256, 0, s>>>(row_nnz_.as<int32_t>(), M, tot);
     COOC_HIP_TRY(hipGetLastError());
-    int64_t err = 0;
-    COOC_HIP_TRY(hipMemcpyAsync(&err, &tot->err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    COOC_HIP_TRY(hipStreamSynchronize(s));
 #ifdef COOC_SP_STATS
     {
-      unsigned long long h[28];
+      unsigned long long h[48];
       hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
       const double g = double(grid);
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
-              "compact hash %.0f | chunks dense %llu hash %llu retries %llu fallbacks %llu | pairs dense %.3g hash %.3g | "
+              "compact hash %.0f | chunks dense %llu hash %llu overflows %llu deferred rows %llu | pairs dense %.3g hash %.3g | "
               "rows %llu split items %llu | mean H %.0f | tail sizes %.0f\n",
               h[13] / 100.0 / g, h[0] / 100.0 / g, h[1] / 100.0 / g, h[4] / 100.0 / g, h[2] / 100.0 / g, h[3] / 100.0 / g,
               h[5], h[6], h[7], h[8], double(h[9]), double(h[10]), h[11], h[12], h[6] ? double(h[14]) / h[6] : 0.0,
@@ -1827,6 +1989,14 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
               double(h[18]), h[19], h[20] / 100.0 / g, h[21] / 100.0 / g, h[22] / 100.0 / g, double(h[23]));
       fprintf(stderr, "[sp stats] thread-0 sample: ids inserted %llu, probe rounds %llu (%.2f per group call)\n", h[24], h[25],
               h[24] ? double(h[25]) / double(h[24]) * 4.0 : 0.0);
+      for (int c = 0; c < 3; c++) {
+        const unsigned long long *q = h + 28 + 6 * c;
+        fprintf(stderr, "[sp stats] hash class %s: chunks %llu, walk %.0f us/WG (%.2f us/chunk), compact %.0f us/WG "
+                "(%.2f us/chunk), groups/chunk %.0f, row entries so far/chunk %.0f, contributions/chunk %.0f\n",
+                c == 0 ? "light-row" : c == 1 ? "gathered" : "list-walk", q[0], q[1] / 100.0 / g,
+                q[0] ? q[1] / 100.0 / double(q[0]) : 0.0, q[2] / 100.0 / g, q[0] ? q[2] / 100.0 / double(q[0]) : 0.0,
+                q[0] ? double(q[3]) / q[0] : 0.0, q[0] ? double(q[4]) / q[0] : 0.0, q[0] ? double(q[5]) / q[0] : 0.0);
+      }
       fprintf(stderr, "[sp stats] attempt %d: cap %lld slab %lld grid %lld err %lld scr_cap %lld n_gather %lld\n", attempt,
               (long long)cap, (long long)slab, (long long)grid, (long long)err, (long long)A.scr_cap, (long long)n_gather);
     }
@@ -1851,6 +2021,84 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   out->work = work_total;
   out->observed = work_total - self_total;  // ordered pairs of the counted rows
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
+  return Status::Ok();
+}
+
+// The deferred rows (k_sp_main: hash table overflow; COOC_FLAG_SORT_ROWS: every whole row) through the sort +
+// segmented-reduce path, in batches of at most kSrBatchPairs pairs (a whole row has <= kSplitWork).
+Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre,
+                             const uint32_t *vals, const int64_t *spre, int64_t cap, hipStream_t s) {
+  const int32_t *rows = sp_defer_.as<int32_t>();
+  // the rows' pair work (sp_roww_), to the host in deferral order
+  COOC_TRY(sr_aux_.reserve(sizeof(int64_t) * size_t(3 * n_def + 4)));
+  int64_t *d_w = sr_aux_.as<int64_t>();
+  k_sr_pair_work<<<nblocks(n_def, 256), 256, 0, s>>>(rows, n_def, sp_roww_.as<int64_t>(), d_w);
+  COOC_HIP_TRY(hipGetLastError());
+  std::vector<int64_t> w(size_t(n_def), 0);
+  COOC_HIP_TRY(hipMemcpyAsync(w.data(), d_w, sizeof(int64_t) * size_t(n_def), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  size_t f0 = 0, t0 = 0;
+  COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
+  // 28 B per pair (two key buffers, run keys, run counts); a batch holds any whole row
+  int64_t budget = std::min<int64_t>(int64_t(1) << 27, int64_t(f0 / 4 / 28));
+  budget = std::max<int64_t>(budget, kSplitWork);
+  int64_t max_batch = 0;
+  for (int64_t j0 = 0, acc = 0, j = 0; j <= n_def; j++) {  // the largest batch, for the buffers
+    if (j == n_def || (acc + w[size_t(j)] > budget && j > j0)) {
+      max_batch = std::max(max_batch, acc);
+      if (j == n_def) break;
+      j0 = j;
+      acc = 0;
+    }
+    acc += w[size_t(j)];
+  }
+  const int64_t nk = std::max<int64_t>(max_batch, 1);
+  COOC_TRY(sr_keys_.reserve(sizeof(uint64_t) * size_t(2 * nk)));
+  COOC_TRY(sr_ukeys_.reserve(sizeof(uint64_t) * size_t(nk)));
+  COOC_TRY(sr_ucnt_.reserve(sizeof(uint32_t) * size_t(nk)));
+  uint64_t *keys = sr_keys_.as<uint64_t>(), *keys2 = keys + nk, *ukeys = sr_ukeys_.as<uint64_t>();
+  uint32_t *ucnt = sr_ucnt_.as<uint32_t>();
+  int64_t *n_runs = d_w + n_def;  // [1]; then kbase [nb + 1], rstart [nb + 1] after it
+  int64_t *kbase = n_runs + 2;
+  size_t tmp = 0, q = 0;
+  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, q, keys, keys2, int(nk), 0, 64, s));
+  tmp = std::max(tmp, q);
+  COOC_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, q, keys2, ukeys, ucnt, n_runs, int(nk), s));
+  tmp = std::max(tmp, q);
+  COOC_TRY(sort_tmp_.reserve(tmp));
+  std::vector<int64_t> kb;
+  int64_t j0 = 0;
+  while (j0 < n_def) {
+    int64_t j1 = j0, acc = 0;
+    kb.assign(1, 0);
+    while (j1 < n_def && (j1 == j0 || acc + w[size_t(j1)] <= budget)) {
+      acc += w[size_t(j1)];
+      kb.push_back(acc);
+      j1++;
+    }
+    const int32_t nb = int32_t(j1 - j0);
+    last_deferred_pairs_ += acc;
+    if (acc > 0) {
+      int64_t *rstart = kbase + (nb + 1);
+      COOC_HIP_TRY(hipMemcpyAsync(kbase, kb.data(), sizeof(int64_t) * size_t(nb + 1), hipMemcpyHostToDevice, s));
+      k_sr_expand<<<unsigned(nb), kSrThreads, 0, s>>>(rows + j0, kbase, row_ptr, epre, vals, sp_tb_.as<int32_t>(),
+                                                      sp_arena_.as<uint4>(), T, keys);
+      COOC_HIP_TRY(hipGetLastError());
+      size_t b = sort_tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(sort_tmp_.p, b, keys, keys2, int(acc), 0, 32 + bits_for(nb + 1), s));
+      b = sort_tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(sort_tmp_.p, b, keys2, ukeys, ucnt, n_runs, int(acc), s));
+      k_sr_bounds<<<nblocks(nb + 1, 256), 256, 0, s>>>(ukeys, n_runs, nb, rstart);
+      k_sr_emit<<<unsigned(nb), kSrThreads, 0, s>>>(rows + j0, rstart, ukeys, ucnt, row_ptr, spre, rowsum_.as<int64_t>(),
+                                                    col_.as<int32_t>(), cnt_.as<uint32_t>(), bump_.as<unsigned long long>(),
+                                                    cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
+                                                    tot_.as<PlanTotals>());
+      COOC_HIP_TRY(hipGetLastError());
+      // kb (host) is reused by the next batch's upload: the copy must have been consumed
+      COOC_HIP_TRY(hipStreamSynchronize(s));
+    }
+    j0 = j1;
+  }
   return Status::Ok();
 }
 

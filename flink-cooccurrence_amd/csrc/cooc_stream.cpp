@@ -272,9 +272,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   tr.mark("upload_append", s);
   if (ctx.counter.batch_ok())  // n_items < 40,320: the batch planner + k_acc_batch
     COOC_TRY(ctx.counter.run_window(au, s, &r));
-  else if (!ctx.counter.sparse())  // COOC_FLAG_GENERAL_PLANNER (A/B of the batch planner)
-    COOC_TRY(ctx.counter.run(au, s, &r));
-  else  // n_items >= 40,320: the large-universe planner, old / new positions in one pass
+  else  // n_items >= 40,320 (or COOC_FLAG_GENERAL_PLANNER): the large-universe planner, old / new positions in one pass
     COOC_TRY(count_large_window(ctx, s, n_act, act_off, act_len, act_old, cbase[n_act], &r));
   tr.mark("count", s);
 

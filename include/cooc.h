@@ -76,9 +76,13 @@ enum cooc_status {
  * least half of the n_items^2 matrix and it fits in HBM, else the padded CSR). */
 #define COOC_FLAG_OUTPUT_CSR 2   /* always the padded CSR (row_base, row_nnz, col, cnt) */
 #define COOC_FLAG_OUTPUT_DENSE 4 /* always the dense matrix (dense, row_nnz) */
-/* Route every window through the sort-based general planner (the path for n_items >= 40,320) even
- * when the batch planner applies; same results (A/B and tests). */
+/* Route every window through the large-universe planner (the path for n_items >= 40,320: per-row LDS
+ * hash / dense-tile chunks) even when the batch planner applies; same results (A/B and tests). */
 #define COOC_FLAG_GENERAL_PLANNER 8
+/* Large universes: every whole row through the sort + segmented-reduce path (packed 64-bit (row, column)
+ * pair keys, radix-sorted, runs counted) instead of the LDS hash / dense-tile chunks.  That path always
+ * takes the rows whose LDS hash table overflows; the flag sends all of them (A/B and tests). */
+#define COOC_FLAG_SORT_ROWS 16
 
 typedef struct cooc_ctx cooc_ctx;
 
@@ -353,6 +357,9 @@ COOC_API int cooc_verify_batch(cooc_ctx *ctx, int32_t flags, uint64_t *d_row_che
  * stream it is launched on; read back after a call that ran it. */
 COOC_API int cooc_set_kernel_timing(cooc_ctx *ctx, int32_t enable);
 COOC_API int cooc_last_kernel_ms(cooc_ctx *ctx, float *accumulate_ms);
+/* Rows (and their ordered pairs) that the last large-universe count sent through the sort +
+ * segmented-reduce path (hash table overflow, or COOC_FLAG_SORT_ROWS). */
+COOC_API int cooc_last_sort_rows(cooc_ctx *ctx, int64_t *rows, int64_t *pairs);
 
 #ifdef __cplusplus
 }

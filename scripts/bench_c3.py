@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--shards", type=int, default=8, help="C3 users / this many are counted (8: one GPU's share)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lib", default=None, help="another build of libcooc_hip.so (e.g. the statistics build)")
+    ap.add_argument("--planner", default="auto", help='CooccurrenceCore planner ("sort": every whole row through '
+                    'the sort + segmented-reduce path)')
     args = ap.parse_args()
     import torch
 
@@ -43,7 +45,7 @@ def main():
     t_gen = time.perf_counter() - t0
     P = datagen.c3_ordered_pairs(0, U)
     M = datagen.C3_ITEMS
-    core = pkg.CooccurrenceCore(n_items=M, device=0)
+    core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner)
     core.set_kernel_timing(True)
     res = core.count_device(up, it)  # warm-up (allocations)
     torch.cuda.synchronize()
@@ -76,6 +78,9 @@ def main():
         "check_observed_eq_P": int(res.observed) == P,
         "check_sum_rowsum_eq_P": rs_total == P,
         "gen_s": t_gen,
+        "planner": args.planner,
+        "sort_path_rows_pairs": core.last_sort_rows(),
+        "verify": core.verify_batch(),
     }
     print(json.dumps(out), flush=True)
     core.close()

@@ -48,7 +48,7 @@ def _batch_layout_vs_closed_form(pkg, oracle, up, it, M, output):
     (1, 500, 97, 12.0, True),
     (2, 3000, 1000, 20.0, True),      # C1 shape, scaled
     (3, 2000, 4096, 40.0, False),     # rating-log shape
-    (4, 300, 40704, 60.0, True),      # the largest single-tile LDS row (general planner)
+    (4, 300, 40704, 60.0, True),      # just above the batch planner: the large-universe planner
     (6, 300, 40319, 60.0, True),     # the largest batch-planner row (+ pad sink + descriptors)
     (7, 5000, 2000, 150.0, False),    # long lists, many batches per chunk
 ])
@@ -128,11 +128,12 @@ def test_micro_logs_batch(pkg, oracle, torch_cuda, log):
     assert got.observed == w["observed"]
 
 
-@pytest.mark.parametrize("planner", ["auto", "general"])
+@pytest.mark.parametrize("planner", ["auto", "large", "sort"])
 @pytest.mark.parametrize("log", [l for l in micro_logs() if not l.get("closed_form_only")], ids=lambda l: l["name"])
 def test_micro_logs_operator(pkg, oracle, torch_cuda, log, planner):
     """The operator mirror (processElement / watermark firing / late drop) on the micro-logs, through
-    the batch planner (streaming windows over resident histories) and the general planner."""
+    the batch planner (streaming windows over resident histories), the large-universe planner (per-row LDS
+    hash / dense-tile chunks) and its sort + segmented-reduce path (planner="sort")."""
     ev = micro_events(log)
     M = 1 + max(e[2] for e in ev if e[0] == "e")
     op = pkg.NonSampledUserInteractionCounterOneInputStreamOperator(log["window_ms"], n_items=M, top_k=3,
@@ -212,7 +213,7 @@ def test_count_device_padded_layout(pkg, oracle, torch_cuda):
         assert np.array_equal(nnz, np.diff(rp))
 
 
-@pytest.mark.parametrize("planner", ["auto", "general"])
+@pytest.mark.parametrize("planner", ["auto", "large", "sort"])
 def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda, planner):
     """C1-shaped click log over 1 s windows: every window's delta rows, row sums, observed, the
     rescorer's top-k, and the final global state."""
@@ -249,7 +250,7 @@ def test_streaming_windows_vs_oracle(pkg, oracle, torch_cuda, planner):
     op.close()
 
 
-@pytest.mark.parametrize("planner", ["auto", "general"])
+@pytest.mark.parametrize("planner", ["auto", "large", "sort"])
 def test_streaming_long_histories_vs_closed_form(pkg, oracle, torch_cuda, planner):
     """Windows over resident histories longer than one fill thread's share (2,048 ids), with
     repeats, users absent from some windows, and a row (item 0) split over several chunks: every

@@ -96,11 +96,13 @@ def _check_rows(rows, brute, sample):
         assert int(gn.sum()) == int(rows.rowsum[a])
 
 
-def test_gather_and_split_rows_vs_brute(pkg, torch_cuda):
+@pytest.mark.parametrize("planner", ["auto", "sort"])
+def test_gather_and_split_rows_vs_brute(pkg, torch_cuda, planner):
+    """planner="sort": the split rows as usual, every whole row through the sort + segmented-reduce path."""
     torch = torch_cuda
     up, it, M = _structured_log()
     dev = torch.device("cuda")
-    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+    with pkg.CooccurrenceCore(n_items=M, device=0, planner=planner) as core:
         res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
         torch.cuda.current_stream().synchronize()
         lens = np.diff(up)
@@ -114,16 +116,22 @@ def test_gather_and_split_rows_vs_brute(pkg, torch_cuda):
         sample = np.concatenate([[0, 1, 57, 199], [200, 201, 250, 299], rng.choice(tail, 40, replace=False),
                                  [300, 32767]])
         _check_rows(rows, brute, sample)
+        if planner == "sort":
+            assert core.last_sort_rows()[0] == int(np.count_nonzero(rows.nnz)) - 200  # all but the 200 split rows
 
 
-def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda):
-    """The first 1,500 users of the shard-invariant C3 log (1e6 items): the whole CSR vs scipy."""
+@pytest.mark.parametrize("planner", ["auto", "sort"])
+def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda, planner):
+    """The first 1,500 users of the shard-invariant C3 log (1e6 items): the whole CSR vs scipy, through the
+    LDS hash / dense-tile chunks and through the sort + segmented-reduce path."""
     from flink_cooccurrence_amd import datagen
 
     up, it = datagen.c3_users(0, 1500)
     M = datagen.C3_ITEMS
-    with pkg.CooccurrenceCore(n_items=M) as core:
+    with pkg.CooccurrenceCore(n_items=M, planner=planner) as core:
         got = core.count(up, it)
+        if planner == "sort":
+            assert core.last_sort_rows()[0] == len(np.unique(it))
     rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
     assert got.observed == observed
     assert np.array_equal(got.row_ptr, rp)
@@ -278,8 +286,9 @@ def test_c5_topk_owned_parts_vs_whole(pkg, torch_cuda):
 
 def test_underestimated_row_table_overflow_retries(pkg, torch_cuda):
     """A row whose partners are far more diverse than the global item frequencies predict: the planner
-    sizes its hash chunk from the estimate, the LDS table overflows, and the chunk is redone with a 4x
-    table (then as dense tiles).  Rows must still be exact."""
+    sizes its hash chunk from the estimate, the LDS table overflows, and k_sp_main hands the whole row to
+    the sort + segmented-reduce path (packed 64-bit (row, column) keys, radix sort, run counts: the north
+    star's overflow fallback).  The path must have run, and the rows must be exact."""
     torch = torch_cuda
     rng = np.random.default_rng(21)
     M = 300_000
@@ -294,6 +303,8 @@ def test_underestimated_row_table_overflow_retries(pkg, torch_cuda):
         torch.cuda.current_stream().synchronize()
         lens = np.diff(up)
         assert res.observed == int(np.sum(lens * (lens - 1)))
+        n_sorted, pairs_sorted = core.last_sort_rows()
+        assert n_sorted >= 1 and pairs_sorted >= 3 * 2500, (n_sorted, pairs_sorted)
         rows = _Rows(res, M)
         assert int(rows.rowsum.sum()) == res.observed
         _check_rows(rows, _Brute(up, it, M), [5, 7, 8192, 8195, 8201] + list(np.unique(it[it >= 20_000])[:20]))
