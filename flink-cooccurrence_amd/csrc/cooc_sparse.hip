@@ -86,7 +86,7 @@ constexpr int kEstK = 84;                              // estimate table: W_k = 
 #endif
 constexpr int64_t kSplitWork = int64_t(1) << COOC_SP_SPLIT_LG;  // rows above this pair work are split
 constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
-constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups)
+constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups of 4 ids)
 constexpr int kGatherMinChunks = COOC_SP_GATHER_MIN;   // rows with this many chunks gather their tails
 #ifndef COOC_SP_FILL
 #define COOC_SP_FILL 0.375f  // A/B at C3: 0.375 with 4x tables 4.5% faster than 0.5 with 3x
@@ -96,7 +96,7 @@ constexpr int kGatherMinChunks = COOC_SP_GATHER_MIN;   // rows with this many ch
 #endif
 constexpr float kHashFill = COOC_SP_FILL * kHashMax;     // expected distinct keys per hash chunk
 constexpr float kDensePairs = COOC_SP_DENSE * kTW;       // a tile with more expected pairs is dense
-constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + kSpThreads;
+constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + kSpThreads;  // (gb + info: 8 B per descriptor)
 
 // One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
 struct SpWork {
@@ -221,15 +221,17 @@ __device__ inline float est_distinct(const float *est, int t, int64_t W) {
 // tile 0, mass 1 - g0) fit a gather scratch.
 __device__ inline int32_t sp_split_shares(int64_t W, float g0) {
   const float tail = float(W) * fmaxf(0.f, 1.f - g0);
-  return max(int32_t((W + kSubWork - 1) / kSubWork), int32_t(ceilf(tail / float(kScrGroups))));
+  return max(int32_t((W + kSubWork - 1) / kSubWork), int32_t(ceilf(tail / float(3 * kScrGroups))));
 }
 
 // ---- planner kernels ------------------------------------------------------------------------------
 // One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
 // item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and regroups the list by
-// column tile: every (user, tile) segment is padded to a multiple of 4 ids (16 B) with the sink id,
-// tb[u][t] = offset of tile t's segment from the user's padded base, tb[u][T] = plen[u] = the user's
-// padded length (the bases are its prefix; k_sp_scatter fills the arena and makes tb absolute).
+// column tile: the list is reordered tile by tile (ids of one tile contiguous, no padding between
+// tiles), tb[u][t] = offset of tile t's first id from the user's base, tb[u][T] = n_u; plen[u] = n_u
+// rounded up to 4 ids (16 B, sink ids at the end: the bases are its prefix, 16-B aligned; k_sp_scatter
+// fills the arena and makes tb absolute).  A chunk reads a tile range of a list as the 16-B groups
+// covering [tb[u][t0], tb[u][t1]) and masks the ids outside it by position.
 __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
                                                       const int32_t *__restrict__ items, int32_t M, int32_t T,
                                                       int64_t *__restrict__ plen, int32_t *__restrict__ tb,
@@ -271,20 +273,20 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (T < 64) {  // exclusive prefix of the padded tile counts: one wave scan (lane t = tile t)
-      const uint32_t x = lane <= T ? uint32_t((c[lane] + 3) & ~3) : 0u;
+    if (T < 64) {  // exclusive prefix of the tile counts: one wave scan (lane t = tile t)
+      const uint32_t x = lane <= T ? uint32_t(c[lane]) : 0u;
       const uint32_t inc = wave_incl_scan(x);
       if (lane <= T) tb[j * (T + 1) + lane] = int32_t(inc - x);
-      if (lane == T) plen[j] = int64_t(inc);  // (tile T is empty: inc = the padded length)
+      if (lane == T) plen[j] = int64_t((inc + 3) & ~3u);  // (tile T is empty: inc = n)
     } else {
       if (lane == 0) {
         int32_t run = 0;
         for (int32_t t = 0; t <= T; t++) {
           const int32_t x = c[t];
           c[t] = run;
-          run += (x + 3) & ~3;
+          run += x;
         }
-        plen[j] = run;
+        plen[j] = (run + 3) & ~3;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -296,10 +298,10 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
   if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
 }
 
-// The padded tile arena: user j's list tile by tile at pbase[j] (a multiple of 4 ids), each tile's
-// segment padded with kSink to a multiple of 4.  One wave per user, tile cursors in LDS.  Leaves
-// tb[j][t] = the absolute 16-B group index of tile t's segment (tb[j][T] = the end of j's list), so
-// that a walk needs one descriptor line per user.
+// The tile arena: user j's list tile by tile at pbase[j] (a multiple of 4 ids), sink ids after its
+// end up to the next multiple of 4.  One wave per user, tile cursors in LDS.  Leaves tb[j][t] = the
+// absolute position (in ids) of tile t's first id (tb[j][T] = the end of j's list), so that a walk
+// needs one descriptor line per user.
 constexpr uint32_t kSink = 0xFFFFFFFFu;
 // A contribution's value: the index of the list its row walks; in a streaming window (spre != NULL) with
 // kSelfBit when the walk includes the contribution's own position (a new position walks its user's whole
@@ -330,12 +332,12 @@ __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (int32_t t = lane; t < T; t += 64)  // pads: from the tile's last id to the next segment
-      for (int32_t q = c[t]; q < tbj[t + 1]; q++) o[q] = kSink;
+    const int32_t pend = int32_t(pbase[j + 1] - pbase[j]);
+    if (lane < pend - n) o[n + lane] = kSink;  // (<= 3 pads)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     int32_t *tbw = tb + j * (T + 1);
-    for (int32_t t = lane; t <= T; t += 64) tbw[t] = int32_t((pbase[j] + tbw[t]) >> 2);
+    for (int32_t t = lane; t <= T; t += 64) tbw[t] = int32_t(pbase[j] + tbw[t]);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
@@ -628,7 +630,8 @@ struct SpShared {
   uint32_t *R;       // [kTW] dense counters | hash keys [0, H) + counts [kHashMax, kHashMax + H)
   uint32_t *L1;      // [kL1Words] hash compaction: one bit per 32-column block
   uint32_t *L1pre;   // [kL1Words] its exclusive popcount prefix
-  int64_t *seg;      // [kSpDb] segment start - virtual start
+  int32_t *gb;       // [kSpDb] a segment's first 16-B group - its virtual start
+  uint32_t *info;    // [kSpDb] (its end - its first group's first position) << 2 | its first id's lane
   uint32_t *vst;     // [kSpDb + 1] virtual starts
   int32_t *qstart;   // [256] first segment of every walker
 };
@@ -692,56 +695,61 @@ __device__ inline void sp_hash_insert4(uint32_t *keys, uint32_t *cnts, const uin
 struct WalkOp {
   int mode;  // 0: dense counters R[id - c0]; 1: hash insert; 2: gather (tile 0 dense, other tiles to buckets)
   uint32_t c0, hshift, hmask;
-  int64_t sbase;  // gather: the workgroup's scratch
+  int64_t sbase;  // gather: the workgroup's scratch (16-B groups)
 };
 
-// One 16-B group of partner ids (one tile's; kSink pads).  Gather mode: a group of tile 0 is counted
-// in the dense tile, any other is appended to its tile's bucket in the workgroup's scratch.
+// One 16-B group of partner ids; m = the lanes (bits 0..3) inside the walked segment, the others are
+// ids of a neighbouring tile range or list (or end-of-list sinks) and are skipped.  Gather mode: an id
+// of tile 0 is counted in the dense tile, any other is appended to its tile's bucket (4-B ids, packed).
 __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStatic &S_, const WalkOp &op,
-                                      const uint4 &v) {
-  if (v.x == kSink) return;  // (the first id of a group is never a pad)
+                                      const uint4 &v, uint32_t m) {
+  uint4 w = v;
+  if (!(m & 1u)) w.x = kSink;
+  if (!(m & 2u)) w.y = kSink;
+  if (!(m & 4u)) w.z = kSink;
+  if (!(m & 8u)) w.w = kSink;
 #ifdef COOC_SP_STATS
   if (A.exp == 1 && op.mode == 1) {  // timing experiment: hash chunks load their groups but insert nothing
-    if (v.y == 0xFFFFFFFEu) S_.flag = 1u;
+    if (w.y == 0xFFFFFFFEu) S_.flag = 1u;
     return;
   }
 #endif
+  if (op.mode == 1) {
+    sp_hash_insert4(L.R, L.R + kHashMax, w, op.hshift, op.hmask, S_);
+    return;
+  }
+  const uint32_t x[4] = {w.x, w.y, w.z, w.w};
   if (op.mode == 2) {
-    const uint32_t t = v.x >> kTShift;
-    if (t == 0) {
-      atomicAdd(&L.R[v.x], 1u);
-      if (v.y != kSink) atomicAdd(&L.R[v.y], 1u);
-      if (v.z != kSink) atomicAdd(&L.R[v.z], 1u);
-      if (v.w != kSink) atomicAdd(&L.R[v.w], 1u);
-    } else {
-      const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
-      if (slot < S_.bstart[t + 1] - S_.bstart[t]) A.scratch[op.sbase + S_.bstart[t] + slot] = v;  // else overflow
+    uint32_t *scr = reinterpret_cast<uint32_t *>(A.scratch + op.sbase);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (x[i] == kSink) continue;
+      const uint32_t t = x[i] >> kTShift;
+      if (t == 0) {
+        atomicAdd(&L.R[x[i]], 1u);
+      } else {
+        const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
+        if (slot < S_.bstart[t + 1] - S_.bstart[t]) scr[S_.bstart[t] + slot] = x[i];  // else the bucket overflowed
+      }
     }
     return;
   }
-  if (op.mode == 1) {
-    sp_hash_insert4(L.R, L.R + kHashMax, v, op.hshift, op.hmask, S_);
-    return;
-  }
-  atomicAdd(&L.R[v.x - op.c0], 1u);
-  if (v.y != kSink) atomicAdd(&L.R[v.y - op.c0], 1u);
-  if (v.z != kSink) atomicAdd(&L.R[v.z - op.c0], 1u);
-  if (v.w != kSink) atomicAdd(&L.R[v.w - op.c0], 1u);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (x[i] != kSink) atomicAdd(&L.R[x[i] - op.c0], 1u);
 }
 
-// Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
-// applying op to every id (dense: one LDS counter add; hash: one table insert).  Batches of kSpDb descriptors are block-scanned into virtual starts;
-// walkers of S lanes (S from the mean segment length) own equal contiguous shares of the batch's
-// virtual range and step S ids at a time, kSpU loads in flight per lane.  Returns early (uniformly)
-// when *flag is raised.
-// One batch of segments: this thread's segment (tid < nb) is len 16-B groups at src[start ..).  The
-// lengths are block-scanned into virtual starts; walkers of S lanes (S from the mean segment length)
-// own equal contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight
-// per lane, applying op to every id.  Returns the batch's groups (uniform); ends with a barrier.
+// One batch of segments: this thread's segment (tid < nb) is the ids at positions [s, e) of ar (16-B
+// groups; a segment starts and ends anywhere inside a group).  The segments' group counts are
+// block-scanned into virtual starts; walkers of S lanes (S from the mean segment length) own equal
+// contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight per lane,
+// applying op to every id of the segment (lanes outside it masked).  Returns the batch's groups
+// (uniform); ends with a barrier.
 __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
-                                         int64_t nsrc, int nb, uint32_t len, int64_t start, const WalkOp &op) {
+                                         int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op) {
   const int tid = threadIdx.x;
   const unsigned long long c_b0 = STAT_CLOCK();
+  const uint32_t len = (tid < nb && e > s) ? ((e + 3u) >> 2) - (s >> 2) : 0u;
   uint32_t total;
   const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
   if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
@@ -750,7 +758,8 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   const uint32_t nW = kSpThreads / S;
   if (tid < nb) {
     L.vst[tid] = ex;
-    L.seg[tid] = start - int64_t(ex);
+    L.gb[tid] = int32_t(s >> 2) - int32_t(ex);
+    L.info[tid] = ((e - (s & ~3u)) << 2) | (s & 3u);
     if (len) {
       const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
       const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
@@ -767,47 +776,49 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   uint32_t g = lo + ql;
   if (g < hi) {
     int32_t cur = L.qstart[q];
-    uint32_t next = L.vst[cur + 1];
-    int64_t base = L.seg[cur];
+    uint32_t vs = L.vst[cur], next = L.vst[cur + 1], inf = L.info[cur];
+    int32_t gb = L.gb[cur];
+    // the group at virtual index gk of the current segment, and its in-segment lanes
+    auto fetch = [&](uint32_t gk, uint4 &v, uint32_t &m) {
+      while (gk >= next) {
+        cur++;
+        vs = next;
+        next = L.vst[cur + 1];
+        gb = L.gb[cur];
+        inf = L.info[cur];
+      }
+      const int64_t gi = int64_t(gb) + int64_t(gk);
+      const uint32_t qq = gk - vs;
+      const uint32_t lo_l = qq ? 0u : (inf & 3u);
+      const int32_t hi_l = min(4, int32_t(inf >> 2) - 4 * int32_t(qq));
+      m = ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);
+      v = BCHK(A, gi >= 0 && gi < nsrc, 8) ? ar[gi] : make_uint4(kSink, kSink, kSink, kSink);
+    };
     uint4 v[kSpU] = {};
-    bool ok[kSpU];
+    uint32_t m = 0;  // 4 lane bits per group in flight
 #pragma unroll
     for (int k = 0; k < kSpU; k++) {
       const uint32_t gk = g + S * k;
-      ok[k] = gk < hi;
-      if (ok[k]) {
-        while (gk >= next) {
-          cur++;
-          next = L.vst[cur + 1];
-          base = L.seg[cur];
-        }
-        v[k] = BCHK(A, base + gk >= 0 && base + gk < nsrc, 8) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
-      }
+      uint32_t mk = 0;
+      if (gk < hi) fetch(gk, v[k], mk);
+      m |= mk << (4 * k);
     }
     for (; g < hi; g += S * kSpU) {
       uint4 vn[kSpU] = {};
-      bool okn[kSpU];
+      uint32_t mn = 0;
 #pragma unroll
       for (int k = 0; k < kSpU; k++) {
         const uint32_t gk = g + S * (kSpU + k);
-        okn[k] = gk < hi;
-        if (okn[k]) {
-          while (gk >= next) {
-            cur++;
-            next = L.vst[cur + 1];
-            base = L.seg[cur];
-          }
-          vn[k] = BCHK(A, base + gk >= 0 && base + gk < nsrc, 16) ? ar[base + gk] : make_uint4(kSink, kSink, kSink, kSink);
-        }
+        uint32_t mk = 0;
+        if (gk < hi) fetch(gk, vn[k], mk);
+        mn |= mk << (4 * k);
       }
 #pragma unroll
       for (int k = 0; k < kSpU; k++)
-        if (ok[k]) sp_apply_group(A, L, S_, op, v[k]);
+        if ((m >> (4 * k)) & 15u) sp_apply_group(A, L, S_, op, v[k], (m >> (4 * k)) & 15u);
 #pragma unroll
-      for (int k = 0; k < kSpU; k++) {
-        v[k] = vn[k];
-        ok[k] = okn[k];
-      }
+      for (int k = 0; k < kSpU; k++) v[k] = vn[k];
+      m = mn;
     }
   }
   __syncthreads();
@@ -821,18 +832,16 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
   const int tid = threadIdx.x;
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
-    uint32_t len = 0;
-    int64_t start = 0;
+    uint32_t s0 = 0, e0 = 0;
     STAT_ADD(19, op.mode == 1 ? 1 : 0);
-    if (tid < nb) {  // the segment of tiles [t0, t1) (full: the whole list) in 16-B groups
+    if (tid < nb) {  // the ids of tiles [t0, t1) (full: the whole list) of the contribution's list
       const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] & kListMask : 0u;
       const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
       const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
-      const int32_t s0 = okt ? tbu[full ? 0 : t0] : 0;
-      len = okt ? uint32_t(tbu[full ? A.T : t1] - s0) : 0u;
-      start = s0;
+      s0 = okt ? uint32_t(tbu[full ? 0 : t0]) : 0u;
+      e0 = okt ? uint32_t(tbu[full ? A.T : t1]) : 0u;
     }
-    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, len, start, op);
+    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, s0, e0, op);
     if (uni(S_.flag)) break;
   }
   return walked;
@@ -1108,15 +1117,16 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
 // The workgroup loop.  A work item is a whole row (its chunks in column order, appended to the row's
 // contiguous output) or a split row's (tile, contribution share), added into the staging row.  One
 // code path for every chunk kind, so that the walk and the two compactions exist once.
-__global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
+__global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_main(SpArgs A) {  // 2 workgroups per CU: <= 128 VGPRs
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ SpStatic S_;
   SpShared L;
   L.R = lds;
   L.L1 = L.R + kTW;
   L.L1pre = L.L1 + kL1Words;
-  L.seg = reinterpret_cast<int64_t *>(L.L1pre + kL1Words);
-  L.vst = reinterpret_cast<uint32_t *>(L.seg + kSpDb);
+  L.gb = reinterpret_cast<int32_t *>(L.L1pre + kL1Words);
+  L.info = reinterpret_cast<uint32_t *>(L.gb + kSpDb);
+  L.vst = L.info + kSpDb;
   L.qstart = reinterpret_cast<int32_t *>(L.vst + kSpDb + 4);
   const int tid = threadIdx.x;
   for (int32_t i = tid; i < kTW + kL1Words; i += kSpThreads) L.R[i] = 0u;
@@ -1172,17 +1182,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
     // the closed-form row sum this row's counts must add up to (read now, compared at the end)
     const int64_t rs_expect = (!split && tid == 0) ? A.rowsum[a] : 0;
     if (gather && tid < 64) {
-      // bucket capacity of tile t >= 1 from the item's pair work Wi and contributions ci: a user
-      // holds lambda = Wi g_t / ci of its ids on average, a (user, tile) segment of x ids takes
-      // ceil(x / 4) groups, ~ P(x > 0) + (lambda - 1)^+ / 4 for Poisson x (an upper bound for a
-      // mixture of users); 10% + 32 groups of slack.  A bucket that still overflows only sends its
-      // tile's chunk back to walking the lists.
-      const float Wi = float(A.epre[k1] - A.epre[k0]), ci = float(max<int64_t>(1, k1 - k0));
+      // bucket capacity of tile t >= 1 (in ids): the item's expected ids in tile t, Wi g_t, + 10% + 64.
+      // A bucket that still overflows only sends its tile's chunk back to walking the lists.
+      const float Wi = float(A.epre[k1] - A.epre[k0]);
       uint32_t cap = 0;
-      if (tid >= 1 && tid < A.T) {
-        const float lam = Wi * A.gmass[tid] / ci;
-        cap = uint32_t(1.1f * ci * ((1.f - __expf(-lam)) + 0.25f * fmaxf(0.f, lam - 1.f))) + 32u;
-      }
+      if (tid >= 1 && tid < A.T) cap = (uint32_t(1.1f * Wi * A.gmass[tid]) + 64u + 3u) & ~3u;  // ids, 16-B aligned
       const uint32_t inc = wave_incl_scan(cap);
       if (tid < A.T) {
         S_.bstart[tid] = inc - cap;
@@ -1191,7 +1195,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       if (tid == A.T - 1) S_.bstart[A.T] = inc;
     }
     __syncthreads();
-    gather = gather && uni(S_.bstart[A.T]) <= uint32_t(A.scr_cap);
+    gather = gather && uni(S_.bstart[A.T]) <= uint32_t(A.scr_cap) * 4u;
     const int dense_until = split ? t_end : -1;  // tiles below it go dense (split items)
     int32_t H = 0;                               // 0: table size from the estimate
     // a whole row whose hash table overflows (more distinct keys than the planner expected) is handed to
@@ -1233,9 +1237,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_main(SpArgs A) {
       } else if (gather && !(uint64_t(uni(int64_t(S_.ovf))) & (((t1 < 64 ? (1ull << t1) : 0ull) - 1ull) & ~((1ull << t) - 1ull)))) {
         // a gathered tile range: the filled parts of its tiles' buckets, walked as one batch
         const int nb = t1 - t;
-        const uint32_t len = tid < nb ? S_.bcur[t + tid] : 0u;
-        const int64_t start = tid < nb ? op.sbase + S_.bstart[t + tid] : 0;
-        walked = sp_walk_batch(A, L, S_, A.scratch, int64_t(gridDim.x) * A.scr_cap, nb, len, start, op);
+        const uint32_t bs = tid < nb ? S_.bstart[t + tid] : 0u;
+        const uint32_t be = tid < nb ? bs + S_.bcur[t + tid] : 0u;
+        walked = sp_walk_batch(A, L, S_, A.scratch + op.sbase, A.scr_cap, nb, bs, be, op);
       } else {  // (also a gathered chunk whose bucket overflowed)
         walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
       }
@@ -1493,7 +1497,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_expand(const int32_t *__restr
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int64_t k = k0 + wave; k < k1; k += kSrThreads / 64) {
     const uint32_t u = vals[k] & kListMask;
-    const int32_t g0 = tb[int64_t(u) * (T + 1)], g1 = tb[int64_t(u) * (T + 1) + T];
+    const int32_t g0 = tb[int64_t(u) * (T + 1)] >> 2, g1 = (tb[int64_t(u) * (T + 1) + T] + 3) >> 2;
     uint64_t *o = keys + kbase[j] + (epre[k] - e0);
     int64_t pos = 0;
     for (int32_t g = g0; g < g1; g += 64) {
@@ -1659,7 +1663,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
-  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(4 * n1 + 16)));  // padded: <= 4 ids per id
+  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(n1 + 3 * U1 + 16)));  // lists padded to 4 ids
   COOC_TRY(sp_pbase_.reserve(sizeof(int64_t) * size_t(2 * U1 + 2)));    // plen [U], pbase [U + 1]
   COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 1)));
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
@@ -1849,7 +1853,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_work, 1), int64_t(n_cu_) * std::max(1, per_cu));
   int64_t scr_cap = 0;
   if (h_tot_->max_tail > 0 && T < 64) {
-    scr_cap = std::min<int64_t>(kScrGroups, h_tot_->max_tail + h_tot_->max_tail / 4 + 4096);
+    scr_cap = std::min<int64_t>(kScrGroups, (h_tot_->max_tail + h_tot_->max_tail / 4 + 64 * T + 4096) / 4 + 1);
     const size_t need = sizeof(uint4) * size_t(grid) * size_t(scr_cap);
     size_t f0 = 0, t0 = 0;
     COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
@@ -1885,7 +1889,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.T = T;
   proto.n_contrib = n_c;
   proto.n_users = U;
-  proto.n_groups = n1 + 4;
+  proto.n_groups = (n1 + 3 * U1) / 4 + 4;
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   proto.rowsum = rowsum_.as<int64_t>();
