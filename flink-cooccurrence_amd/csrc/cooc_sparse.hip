@@ -85,7 +85,10 @@ constexpr int kEstK = 84;                              // estimate table: W_k = 
 #define COOC_SP_GATHER_MIN 3
 #endif
 constexpr int64_t kSplitWork = int64_t(1) << COOC_SP_SPLIT_LG;  // rows above this pair work are split
-constexpr int64_t kSubWork = int64_t(1) << 23;         // pairs per split work item (expected)
+#ifndef COOC_SP_SUB_LG
+#define COOC_SP_SUB_LG 24  // 2^24-pair shares: 1.4% faster than 2^23 on the 1/8 C3 shard (profiles/r03/sub_ab)
+#endif
+constexpr int64_t kSubWork = int64_t(1) << COOC_SP_SUB_LG;  // pairs per split work item (expected)
 constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups of 4 ids)
 constexpr int kGatherMinChunks = COOC_SP_GATHER_MIN;   // rows with this many chunks gather their tails
 #ifndef COOC_SP_FILL
@@ -1281,6 +1284,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
           }
         }
         __syncthreads();
+        STAT_ADD(26, STAT_CLOCK() - c_walked);  // the share's flush of this tile into the staging row
       } else if (dense) {
         if (tid == 0 && a >= c0 && a < c1) L.R[a - c0] -= self;
         __syncthreads();
@@ -1991,6 +1995,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       fprintf(stderr, "[sp stats] hash detail per WG (us): walk scan %.0f walk loop %.0f | groups %.3g batches %llu | "
               "compact rank %.0f reserve %.0f write %.0f | entries %.3g\n", h[16] / 100.0 / g, h[17] / 100.0 / g,
               double(h[18]), h[19], h[20] / 100.0 / g, h[21] / 100.0 / g, h[22] / 100.0 / g, double(h[23]));
+      fprintf(stderr, "[sp stats] split flush (staging atomics) per WG (us): %.0f\n", h[26] / 100.0 / g);
       fprintf(stderr, "[sp stats] thread-0 sample: ids inserted %llu, probe rounds %llu (%.2f per group call)\n", h[24], h[25],
               h[24] ? double(h[25]) / double(h[24]) * 4.0 : 0.0);
       for (int c = 0; c < 3; c++) {
