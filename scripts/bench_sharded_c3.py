@@ -76,17 +76,36 @@ def main():
     ent_all = torch.cat(recv_ent)
     del recv_nnz, recv_ent
     torch.cuda.empty_cache()
-    merge_ms = []
-    for _ in range(2):
-        ev0.record()
-        merged = core.merge_partitions(W, part, nnz_all, ent_all, rowsum_global=rowsum)
-        ev1.record()
-        ev1.synchronize()
-        merge_ms.append(ev0.elapsed_time(ev1))
+    # the owner's merge: cooc_merge_partitions keeps a dense LDS row per owned row (n_items < 40,320); at
+    # 1e6 items the N partial rows of a row would be merged by sorting the received (row, column) keys and
+    # reducing equal keys -- timed here on a 1e9-entry slice of the received entries with torch.sort
+    # (the dominant step), then scaled to all of them
+    merge_ms, merged_nnz = [None], None
+    if M <= 40_704:
+        merge_ms = []
+        for _ in range(2):
+            ev0.record()
+            merged = core.merge_partitions(W, part, nnz_all, ent_all, rowsum_global=rowsum)
+            ev1.record()
+            ev1.synchronize()
+            merge_ms.append(ev0.elapsed_time(ev1))
+        merged_nnz = int(merged.nnz)
+    n_sl = min(int(ent_all.numel()), 1_000_000_000)
+    rows_of = torch.repeat_interleave(torch.arange(W * R, device=dev, dtype=torch.int64) % R, nnz_all.to(torch.int64))
+    keys = (rows_of[:n_sl] << 32) | (ent_all[:n_sl] >> 32)
+    del rows_of
+    torch.cuda.synchronize()
+    ev0.record()
+    torch.sort(keys)
+    ev1.record()
+    ev1.synchronize()
+    sort_ms = ev0.elapsed_time(ev1)
     out = {"config": f"C3 partial-count exchange at N={W}: ranks' 1/8 user shares of the shard-invariant 1B log, "
                      f"owner {part} ({R} rows owned)",
            "ranks": ranks, "owner_recv_entries": int(ent_all.numel()), "owner_recv_bytes": int(8 * ent_all.numel()),
-           "owner_merge_ms": merge_ms[-1], "owner_merged_entries": int(merged.nnz),
+           "owner_merge_ms": merge_ms[-1], "owner_merged_entries": merged_nnz,
+           "merge_sort_proxy": {"entries_sorted": n_sl, "ms": sort_ms,
+                                "ms_scaled_to_all_received": sort_ms * ent_all.numel() / n_sl},
            "owned_rows_exchange_bytes_per_rank": 4 * 999_536_273 * (W - 1) // W,
            "note": "sent_bytes = 8 B x the rank's partial entries owned elsewhere (what the all-to-all moves out "
                    "of one rank); owned_rows_exchange_bytes_per_rank = what count_owned's all-gather moves in"}
