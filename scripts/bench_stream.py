@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--copy", action="store_true", help="also copy every window's outputs to the host")
     ap.add_argument("--users", type=int, default=138_493)
-    ap.add_argument("--planner", default="auto", choices=["auto", "general"])
+    ap.add_argument("--planner", default="auto", choices=["auto", "large", "general", "sort"])
     ap.add_argument("--c3-shard", type=int, default=0,
                     help="stream users [0, 1e7 / this) of the C3 log (1e6 items) instead of the C2 log")
     args = ap.parse_args()
