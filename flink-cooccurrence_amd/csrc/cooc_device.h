@@ -101,6 +101,8 @@ struct PlanTotals {
   int64_t bad_row;        // a row whose counts failed the row-sum check (err bit 1), for the message
   int64_t self_total;     // contributions whose walk includes their own position (pairs p == p removed)
   int64_t n_deferred;     // whole rows handed to the sort + segmented-reduce path (hash table overflow)
+  int64_t n_tiny;         // whole rows of <= kTinyW pairs (the queue's tail): one wave each (k_sp_tiny)
+  int64_t tiny_ctr;       // k_sp_tiny's work counter
 };
 
 // One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR

@@ -78,6 +78,7 @@ constexpr int kSpDb = 512;                             // contribution descripto
 constexpr int kMaxProbe = 64;                          // linear probes before an insert gives up
 constexpr int kSpU = 4;                                // partner loads in flight per lane
 constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
+constexpr int kTinyW = 256;                            // rows of at most this many pairs: one wave each (k_sp_tiny)
 #ifndef COOC_SP_SPLIT_LG
 #define COOC_SP_SPLIT_LG 23
 #endif
@@ -464,10 +465,11 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
                                                  uint64_t *__restrict__ skey,
                                                  int32_t *__restrict__ order, int32_t *__restrict__ nwork,
                                                  int32_t *__restrict__ row_nnz, int64_t *__restrict__ row_base,
-                                                 PlanTotals *__restrict__ tot, const int64_t *__restrict__ spre) {
+                                                 PlanTotals *__restrict__ tot, const int64_t *__restrict__ spre,
+                                                 int32_t tiny_on) {
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0;
+  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0, n_tiny = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -482,6 +484,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     int32_t nw = 0;
     if (c > 0) {
       n_active = 1;
+      n_tiny = (tiny_on && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
       bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
@@ -549,6 +552,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   uint64_t act = n_active;
   for (int o = 32; o > 0; o >>= 1) {
     act += __shfl_xor(act, o, 64);
+    n_tiny += __shfl_xor(n_tiny, o, 64);
     n_gather += __shfl_xor(n_gather, o, 64);
     max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
   }
@@ -563,6 +567,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     if (r[3]) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_split_work), (unsigned long long)r[3]);
   }
   if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
+  if (lane == 0 && n_tiny) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_tiny), (unsigned long long)n_tiny);
   if (lane == 0 && n_gather)
     atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_gather_rows), (unsigned long long)n_gather);
 }
@@ -1137,7 +1142,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
     S_.slab_cur = S_.slab_end = 0;
     S_.flag = 0u;
   }
-  const int64_t n_work = A.tot->n_chunks;
+  const int64_t n_work = A.tot->n_chunks - A.tot->n_tiny;  // (the tiny rows at the queue's tail: k_sp_tiny)
 #ifdef COOC_SP_STATS
   if (threadIdx.x < 48) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
@@ -1473,6 +1478,7 @@ __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict
   tot->err &= ~int64_t(6);  // the region (4) and row-sum (2) checks of the previous attempt
   tot->nnz_total = 0;
   tot->n_deferred = 0;
+  tot->tiny_ctr = 0;
   qctr[0] = 0;
   bump[0] = 0;
 }
@@ -1594,6 +1600,152 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
     const int64_t q = base + (r - r0) - (drop && r > diag ? 1 : 0);
     col_out[q] = int32_t(uint32_t(ukeys[r]));
     cnt_out[q] = ucnt[r] - (r == diag ? self : 0u);
+  }
+}
+
+// ---- tiny rows: one wave per row ------------------------------------------------------------------
+// A whole row of at most kTinyW pairs (a streaming window's rows are mostly a few pairs each): its
+// contributions' lists are gathered into a per-wave LDS buffer, sorted (bitonic, wave-synchronous),
+// equal columns counted (the segmented reduce of the +1 increments), the diagonal's self term removed,
+// and the entries written in column order from a per-wave output slab.  No workgroup barrier.
+constexpr int kTinyThreads = 256, kTinyWaves = kTinyThreads / 64;
+constexpr int64_t kTinySlab = 4096;  // output entries reserved per wave at a time
+
+__device__ inline void tiny_sync() {  // the wave's LDS writes visible to its other lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
+  __shared__ uint32_t buf[kTinyWaves][kTinyW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t *b = buf[wave];
+  const int64_t first = A.tot->n_chunks - A.tot->n_tiny, n_tiny = A.tot->n_tiny;
+  const uint32_t *ar = reinterpret_cast<const uint32_t *>(A.tarena);
+  int64_t slab_cur = 0, slab_end = 0;  // (wave-uniform)
+  for (;;) {
+    int64_t i = 0;
+    if (lane == 0) i = int64_t(atomicAdd(reinterpret_cast<unsigned long long *>(&A.tot->tiny_ctr), 1ull));
+    i = __shfl(i, 0, 64);
+    if (i >= n_tiny) break;
+    const SpWork it = A.queue[first + i];
+    const int32_t a = it.row;
+    const int64_t k0 = it.k0, k1 = it.k1;
+    // 1. the contributions' lists (whole lists), 64 at a time, into b in list order
+    uint32_t W = 0;
+    for (int64_t c0 = k0; c0 < k1; c0 += 64) {
+      uint32_t s0 = 0, e0 = 0;
+      if (c0 + lane < k1) {
+        const uint32_t u = A.vals[c0 + lane] & kListMask;
+        const int32_t *tbu = A.tb + int64_t(u) * (A.T + 1);
+        s0 = uint32_t(tbu[0]);
+        e0 = uint32_t(tbu[A.T]);
+      }
+      const uint32_t len = e0 - s0, inc = wave_incl_scan(len);
+      const uint32_t tot = __shfl(inc, 63, 64);
+      if (W + tot > uint32_t(kTinyW)) {  // (cannot happen: the planner's W bounds it)
+        if (lane == 0) atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
+        W = 0;
+        break;
+      }
+      for (uint32_t q = 0; q < len; q++) b[W + inc - len + q] = ar[s0 + q];
+      W += tot;
+    }
+    // 2. bitonic sort of b[0, n2), padded with kSink
+    uint32_t n2 = 1;
+    while (n2 < W) n2 <<= 1;
+    for (uint32_t q = W + lane; q < n2; q += 64) b[q] = kSink;
+    tiny_sync();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t q = lane; q < n2 / 2; q += 64) {
+          const uint32_t lo = 2 * q - (q & (j - 1)), hi = lo + j;  // pairs (lo, lo + j) with bit j of lo clear
+          const uint32_t x = b[lo], y = b[hi];
+          const bool up = (lo & k) == 0;
+          if ((x > y) == up) {
+            b[lo] = y;
+            b[hi] = x;
+          }
+        }
+        tiny_sync();
+      }
+    }
+    // 3. run heads (a 256-bit mask in four ballots), counts, the diagonal's self term
+    const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
+    uint64_t hm[kTinyW / 64];
+#pragma unroll
+    for (int g = 0; g < kTinyW / 64; g++) {
+      const uint32_t q = uint32_t(g * 64 + lane);
+      const bool h = q < W && (q == 0 || b[q] != b[q - 1]);
+      hm[g] = __ballot(h);
+    }
+    uint32_t my_cnt[kTinyW / 64], n_keep = 0;
+    uint64_t keep[kTinyW / 64];
+#pragma unroll
+    for (int g = 0; g < kTinyW / 64; g++) {
+      const uint32_t q = uint32_t(g * 64 + lane);
+      uint32_t cnt = 0;
+      if ((hm[g] >> lane) & 1ull) {
+        uint32_t nx = W;  // the next head after q
+        const uint64_t rest = lane < 63 ? hm[g] >> (lane + 1) << (lane + 1) : 0ull;
+        if (rest) {
+          nx = uint32_t(g * 64 + __ffsll((long long)rest) - 1);
+        } else {
+#pragma unroll
+          for (int g2 = g + 1; g2 < kTinyW / 64; g2++)
+            if (nx == W && hm[g2]) nx = uint32_t(g2 * 64 + __ffsll((long long)hm[g2]) - 1);
+        }
+        cnt = nx - q;
+        if (b[q] == uint32_t(a)) cnt -= self;
+      }
+      my_cnt[g] = cnt;
+      keep[g] = __ballot(cnt != 0u);
+      n_keep += uint32_t(__popcll(keep[g]));
+    }
+    // 4. output: the wave's slab; row sum check (counts add up to W - self)
+    if (slab_cur + n_keep > slab_end) {
+      int64_t nb = 0;
+      if (lane == 0) {
+        const int64_t take = max<int64_t>(kTinySlab, n_keep);
+        nb = int64_t(atomicAdd(A.bump, (unsigned long long)take));
+        if (nb + take > A.cap) {
+          atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 4ull);
+          nb = -1;
+        } else {
+          nb = nb | (take << 40);  // (take <= 2^23, positions < 2^40)
+        }
+      }
+      nb = __shfl(nb, 0, 64);
+      if (nb < 0) break;
+      slab_cur = nb & ((int64_t(1) << 40) - 1);
+      slab_end = slab_cur + (nb >> 40);
+    }
+    const int64_t base = slab_cur;
+    slab_cur += n_keep;
+    uint64_t rsum = 0;
+    uint32_t before = 0;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+    for (int g = 0; g < kTinyW / 64; g++) {
+      if (my_cnt[g]) {
+        const int64_t pos = base + before + uint32_t(__popcll(keep[g] & lt));
+        A.col_out[pos] = int32_t(b[g * 64 + lane]);
+        A.cnt_out[pos] = my_cnt[g];
+        rsum += my_cnt[g];
+      }
+      before += uint32_t(__popcll(keep[g]));
+    }
+    for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
+    if (lane == 0) {
+      A.row_base[a] = n_keep ? base : 0;
+      A.row_nnz[a] = int32_t(n_keep);
+      if (rsum != uint64_t(A.rowsum[a])) {
+        atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
+        A.tot->bad_row = a;
+      }
+    }
+    tiny_sync();  // (b is rewritten by the next row)
   }
 }
 
@@ -1793,7 +1945,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                             sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
                                             order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
-                                            row_base_.as<int64_t>(), tot, spre);
+                                            row_base_.as<int64_t>(), tot, spre, sort_rows_ ? 0 : 1);
   k_sp_totals<<<1, 1, 0, s>>>(tot, epre, spre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
@@ -1868,7 +2020,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * grid)));
-  const int64_t slack = 2 * grid * slab + M;
+  const int64_t n_tiny = h_tot_->n_tiny;
+  const int64_t grid_tiny = std::min<int64_t>((n_tiny + kTinyWaves - 1) / kTinyWaves, int64_t(n_cu_) * 8);
+  const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0);
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
   cap = std::max<int64_t>(1, std::min(cap, budget));
@@ -1932,7 +2086,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-    if (n_work > 0) {
+    if (n_work > n_tiny) {
       k_sp_main<<<unsigned(grid), kSpThreads, kSpLds, s>>>(A);
       COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_TRACE
@@ -1958,6 +2112,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
     }
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+    if (n_tiny > 0) {
+      k_sp_tiny<<<unsigned(grid_tiny), kTinyThreads, 0, s>>>(A);
+      COOC_HIP_TRY(hipGetLastError());
+    }
   SPT("main");
     if (n_split > 0) {
       k_sp_split_finalize<<<unsigned(n_split), kFinThreads, 0, s>>>(

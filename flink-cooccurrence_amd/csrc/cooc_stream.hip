@@ -390,12 +390,18 @@ __global__ void k_gs_alloc(int32_t M, const int64_t *__restrict__ drp, const int
     nbase[a] = -1;
     return;
   }
-  const int64_t need = int64_t(glen[a]) + (newpre[d1] - newpre[d0]);
+  const int64_t added = newpre[d1] - newpre[d0];
+  if (added == 0) {  // no new column: the counts are added in place (the slab stays)
+    nbase[a] = -2;
+    return;
+  }
+  const int64_t need = int64_t(glen[a]) + added;
   nbase[a] = int64_t(atomicAdd(bump, (unsigned long long)need));
 }
 
 // the merge: old entries shift right by the new columns before them (and take a matching delta's
-// count), new delta entries go after the old columns below them.  One wave per touched row.
+// count), new delta entries go after the old columns below them; a row without new columns takes its
+// delta counts in place.  One wave per touched row.
 __global__ __launch_bounds__(256) void k_gs_merge(int32_t M, const int64_t *__restrict__ drp,
                                                   const int32_t *__restrict__ dcol, const uint32_t *__restrict__ dcnt,
                                                   const int64_t *__restrict__ newpre, const int32_t *__restrict__ flag,
@@ -406,8 +412,15 @@ __global__ __launch_bounds__(256) void k_gs_merge(int32_t M, const int64_t *__re
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
     const int64_t nb = nbase[a];
-    if (nb < 0) continue;
+    if (nb == -1) continue;
     const int64_t d0 = drp[a], d = drp[a + 1] - d0, ob = gbase[a], n_old = glen[a];
+    if (nb == -2) {  // every delta column is already in the row: add its count where it sits
+      for (int64_t e = lane; e < d; e += 64) {
+        const int32_t c = dcol[d0 + e];
+        gcnt[ob + lower_bound_col(gcol + ob, n_old, c)] += dcnt[d0 + e];
+      }
+      continue;
+    }
     for (int64_t i = lane; i < n_old; i += 64) {
       const int32_t c = gcol[ob + i];
       const int64_t p = lower_bound_col(dcol + d0, d, c);
