@@ -255,10 +255,10 @@ Status launch_verify(hipStream_t s, int32_t M, const CountResult &r, bool symmet
 // ItemRowRescorer...java:35,171-177): row a = len[a] (column, count) entries in ascending column order
 // at base[a] of the arena (col, cnt); kernels in cooc_stream.hip.
 struct GlobalSparse {
-  DevBuf base, len, col, cnt, flag, newpre, nbase, bump_dev;
+  DevBuf base, len, col, cnt, flag, newpre, nbase, bump_dev, opos, chunk_pre;
   int64_t cap = 0, bump = 0, live = 0;
   void release() {
-    DevBuf *all[] = {&base, &len, &col, &cnt, &flag, &newpre, &nbase, &bump_dev};
+    DevBuf *all[] = {&base, &len, &col, &cnt, &flag, &newpre, &nbase, &bump_dev, &opos, &chunk_pre};
     for (DevBuf *b : all) b->release();
     cap = bump = live = 0;
   }

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *
     const int32_t n = row_nnz[a];
     if (n == 0) continue;
     const int64_t b = row_base[a];
-    if (G) {  // dense global rows (sparse ones are merged by k_gs_merge)
+    if (G) {  // dense global rows (sparse ones are merged by k_gs_flags / k_gs_move_all / k_gs_insert)
       uint32_t *g = G + a * int64_t(M);
       for (int32_t i = lane; i < n; i += 64) g[col[b + i]] += cnt[b + i];  // unique (a, col) per window
     }
@@ -360,32 +360,42 @@ __device__ inline int64_t lower_bound_col(const int32_t *__restrict__ c, int64_t
   return lo;
 }
 
-// flag[e] = 1 when delta entry e's column is not yet in its row (one wave per row)
-__global__ __launch_bounds__(256) void k_gs_flags(int32_t M, const int64_t *__restrict__ drp,
-                                                  const int32_t *__restrict__ dcol, const int64_t *__restrict__ gbase,
-                                                  const int32_t *__restrict__ glen, const int32_t *__restrict__ gcol,
-                                                  int32_t *__restrict__ flag) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
-    const int64_t d0 = drp[a], d1 = drp[a + 1];
-    if (d0 == d1) continue;
-    const int32_t *old = gcol + gbase[a];
-    const int64_t n_old = glen[a];
-    for (int64_t e = d0 + lane; e < d1; e += 64) {
-      const int64_t p = lower_bound_col(old, n_old, dcol[e]);
-      flag[e] = (p < n_old && old[p] == dcol[e]) ? 0 : 1;
-    }
+// The row of packed delta entry e: the last a with drp[a] <= e (drp ascending, drp[M] = nnz).
+__device__ inline int32_t gs_row_of(const int64_t *__restrict__ drp, int32_t M, int64_t e) {
+  int32_t lo = 0, hi = M;  // invariant: drp[lo] <= e < drp[hi]
+  while (hi - lo > 1) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (drp[mid] <= e) lo = mid; else hi = mid;
   }
+  return lo;
 }
 
-// new slab of every touched row: need = old + new columns, bump-allocated; live += new columns
+// Per delta entry (flat over the window's entries, whatever the row lengths): its column's position
+// in the row's old slab (opos) and flag[e] = 1 when the column is new to the row.
+__global__ __launch_bounds__(256) void k_gs_flags(int32_t M, int64_t nnz, const int64_t *__restrict__ drp,
+                                                  const int32_t *__restrict__ dcol, const int64_t *__restrict__ gbase,
+                                                  const int32_t *__restrict__ glen, const int32_t *__restrict__ gcol,
+                                                  int32_t *__restrict__ flag, int64_t *__restrict__ opos) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  const int32_t a = gs_row_of(drp, M, e);
+  const int32_t *old = gcol + gbase[a];
+  const int64_t n_old = glen[a], c = dcol[e];
+  const int64_t p = lower_bound_col(old, n_old, int32_t(c));
+  opos[e] = p;
+  flag[e] = (p < n_old && old[p] == c) ? 0 : 1;
+}
+
+// new slab of every touched row with new columns: old + new entries, bump-allocated; a row without new
+// columns keeps its slab (-2: counts added in place); chunks[a] = its old entries in kGsChunk pieces
+constexpr int64_t kGsChunk = 2048;
 __global__ void k_gs_alloc(int32_t M, const int64_t *__restrict__ drp, const int64_t *__restrict__ newpre,
                            const int32_t *__restrict__ glen, int64_t *__restrict__ nbase,
-                           unsigned long long *__restrict__ bump) {
+                           unsigned long long *__restrict__ bump, int32_t *__restrict__ chunks) {
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= M) return;
   const int64_t d0 = drp[a], d1 = drp[a + 1];
+  chunks[a] = 0;
   if (d0 == d1) {
     nbase[a] = -1;
     return;
@@ -397,31 +407,28 @@ __global__ void k_gs_alloc(int32_t M, const int64_t *__restrict__ drp, const int
   }
   const int64_t need = int64_t(glen[a]) + added;
   nbase[a] = int64_t(atomicAdd(bump, (unsigned long long)need));
+  chunks[a] = int32_t((glen[a] + kGsChunk - 1) / kGsChunk);
 }
 
-// the merge: old entries shift right by the new columns before them (and take a matching delta's
-// count), new delta entries go after the old columns below them; a row without new columns takes its
-// delta counts in place.  One wave per touched row.
-__global__ __launch_bounds__(256) void k_gs_merge(int32_t M, const int64_t *__restrict__ drp,
-                                                  const int32_t *__restrict__ dcol, const uint32_t *__restrict__ dcnt,
-                                                  const int64_t *__restrict__ newpre, const int32_t *__restrict__ flag,
-                                                  const int64_t *__restrict__ nbase, const int64_t *__restrict__ gbase,
-                                                  const int32_t *__restrict__ glen, int32_t *__restrict__ gcol,
-                                                  uint32_t *__restrict__ gcnt) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
-    const int64_t nb = nbase[a];
-    if (nb == -1) continue;
-    const int64_t d0 = drp[a], d = drp[a + 1] - d0, ob = gbase[a], n_old = glen[a];
-    if (nb == -2) {  // every delta column is already in the row: add its count where it sits
-      for (int64_t e = lane; e < d; e += 64) {
-        const int32_t c = dcol[d0 + e];
-        gcnt[ob + lower_bound_col(gcol + ob, n_old, c)] += dcnt[d0 + e];
-      }
-      continue;
+// The moved rows' old entries, kGsChunk per block (flat over the rows, so a long row is spread over
+// many blocks): an old entry shifts right by the new columns below it and takes a matching delta's count.
+__global__ __launch_bounds__(256) void k_gs_move_all(int32_t M, const int64_t *__restrict__ chunk_pre,
+                                                 const int64_t *__restrict__ drp, const int32_t *__restrict__ dcol,
+                                                 const uint32_t *__restrict__ dcnt, const int64_t *__restrict__ newpre,
+                                                 const int64_t *__restrict__ nbase, const int64_t *__restrict__ gbase,
+                                                 const int32_t *__restrict__ glen, int32_t *__restrict__ gcol,
+                                                 uint32_t *__restrict__ gcnt) {
+  const int64_t n_chunks = chunk_pre[M];
+  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+    int32_t lo = 0, hi = M;  // the row: last a with chunk_pre[a] <= ch
+    while (hi - lo > 1) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (chunk_pre[mid] <= ch) lo = mid; else hi = mid;
     }
-    for (int64_t i = lane; i < n_old; i += 64) {
+    const int32_t a = lo;
+    const int64_t i0 = (ch - chunk_pre[a]) * kGsChunk, n_old = glen[a], i1 = min(n_old, i0 + kGsChunk);
+    const int64_t nb = nbase[a], d0 = drp[a], d = drp[a + 1] - d0, ob = gbase[a];
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
       const int32_t c = gcol[ob + i];
       const int64_t p = lower_bound_col(dcol + d0, d, c);
       const uint32_t add = (p < d && dcol[d0 + p] == c) ? dcnt[d0 + p] : 0u;
@@ -429,13 +436,27 @@ __global__ __launch_bounds__(256) void k_gs_merge(int32_t M, const int64_t *__re
       gcol[pos] = c;
       gcnt[pos] = gcnt[ob + i] + add;
     }
-    for (int64_t e = lane; e < d; e += 64) {
-      if (!flag[d0 + e]) continue;
-      const int32_t c = dcol[d0 + e];
-      const int64_t pos = nb + (newpre[d0 + e] - newpre[d0]) + lower_bound_col(gcol + ob, n_old, c);
-      gcol[pos] = c;
-      gcnt[pos] = dcnt[d0 + e];
-    }
+  }
+}
+
+// Per delta entry: a new column lands after the old columns below it in the row's new slab; in a row
+// without new columns the count is added where the column sits.
+__global__ __launch_bounds__(256) void k_gs_insert(int32_t M, int64_t nnz, const int64_t *__restrict__ drp,
+                                                   const int32_t *__restrict__ dcol, const uint32_t *__restrict__ dcnt,
+                                                   const int64_t *__restrict__ newpre, const int32_t *__restrict__ flag,
+                                                   const int64_t *__restrict__ opos, const int64_t *__restrict__ nbase,
+                                                   const int64_t *__restrict__ gbase, int32_t *__restrict__ gcol,
+                                                   uint32_t *__restrict__ gcnt) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  const int32_t a = gs_row_of(drp, M, e);
+  const int64_t nb = nbase[a];
+  if (nb == -2) {
+    gcnt[gbase[a] + opos[e]] += dcnt[e];
+  } else if (flag[e]) {
+    const int64_t pos = nb + (newpre[e] - newpre[drp[a]]) + opos[e];
+    gcol[pos] = dcol[e];
+    gcnt[pos] = dcnt[e];
   }
 }
 
@@ -609,16 +630,21 @@ Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, c
 
 Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32_t *dcol, const uint32_t *dcnt,
                        int64_t nnz, GlobalSparse &g, DevBuf &tmp, int64_t *new_cols) {
-  // 1. new-column flags, their exclusive prefix (newpre[nnz] = the window's new columns)
+  // 1. per delta entry: its old-slab position and whether its column is new; the flags' prefix
+  //    (newpre[nnz] = the window's new columns)
   COOC_TRY(g.flag.reserve(sizeof(int32_t) * size_t(std::max<int64_t>(nnz, 1))));
+  COOC_TRY(g.opos.reserve(sizeof(int64_t) * size_t(std::max<int64_t>(nnz, 1))));
   COOC_TRY(g.newpre.reserve(sizeof(int64_t) * size_t(nnz + 1)));
   COOC_TRY(g.nbase.reserve(sizeof(int64_t) * size_t(M)));
+  COOC_TRY(g.chunk_pre.reserve(sizeof(int64_t) * size_t(M + 1) + sizeof(int32_t) * size_t(M)));
   int32_t *flag = g.flag.as<int32_t>();
-  int64_t *newpre = g.newpre.as<int64_t>();
+  int64_t *newpre = g.newpre.as<int64_t>(), *opos = g.opos.as<int64_t>();
+  int64_t *chunk_pre = g.chunk_pre.as<int64_t>();
+  int32_t *chunks = reinterpret_cast<int32_t *>(chunk_pre + M + 1);
   COOC_HIP_TRY(hipMemsetAsync(newpre, 0, sizeof(int64_t), s));
-  const unsigned gw = std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192);
   if (nnz > 0) {
-    k_gs_flags<<<gw, 256, 0, s>>>(M, drp, dcol, g.base.as<int64_t>(), g.len.as<int32_t>(), g.col.as<int32_t>(), flag);
+    k_gs_flags<<<blocks_for(nnz, 256), 256, 0, s>>>(M, nnz, drp, dcol, g.base.as<int64_t>(), g.len.as<int32_t>(),
+                                                  g.col.as<int32_t>(), flag, opos);
     hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> f64(flag, WidenLen{});
     size_t b = 0;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, f64, newpre + 1, int(nnz), s));
@@ -628,7 +654,7 @@ Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32
   }
   COOC_HIP_TRY(hipMemcpyAsync(new_cols, newpre + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
-  // 2. room for the touched rows' new slabs (at most live + nnz entries): compact, then grow
+  // 2. room for the moved rows' new slabs (at most live + nnz entries): compact, then grow
   const int64_t need = g.live + nnz;
   if (g.bump + need > g.cap) {
     COOC_TRY(compact_global(s, M, g, tmp, std::max<int64_t>(2 * (g.live + need), int64_t(1) << 12)));
@@ -636,9 +662,23 @@ Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32
   COOC_TRY(g.bump_dev.reserve(sizeof(uint64_t)));
   COOC_HIP_TRY(hipMemcpyAsync(g.bump_dev.p, &g.bump, sizeof(int64_t), hipMemcpyHostToDevice, s));
   k_gs_alloc<<<blocks_for(M, 256), 256, 0, s>>>(M, drp, newpre, g.len.as<int32_t>(), g.nbase.as<int64_t>(),
-                                                g.bump_dev.as<unsigned long long>());
-  k_gs_merge<<<gw, 256, 0, s>>>(M, drp, dcol, dcnt, newpre, flag, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
-                                g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>());
+                                                g.bump_dev.as<unsigned long long>(), chunks);
+  // 3. the moved rows' old entries in kGsChunk pieces, then every delta entry
+  COOC_HIP_TRY(hipMemsetAsync(chunk_pre, 0, sizeof(int64_t), s));
+  {
+    hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> c64(chunks, WidenLen{});
+    size_t b = 0;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, c64, chunk_pre + 1, M, s));
+    COOC_TRY(tmp.reserve(b));
+    b = tmp.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, c64, chunk_pre + 1, M, s));
+  }
+  // (the chunk total is not read back: a fixed grid strides over chunk_pre[M] chunks)
+  k_gs_move_all<<<2048, 256, 0, s>>>(M, chunk_pre, drp, dcol, dcnt, newpre, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
+                                    g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>());
+  if (nnz > 0)
+    k_gs_insert<<<blocks_for(nnz, 256), 256, 0, s>>>(M, nnz, drp, dcol, dcnt, newpre, flag, opos, g.nbase.as<int64_t>(),
+                                                    g.base.as<int64_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>());
   k_gs_commit<<<blocks_for(M, 256), 256, 0, s>>>(M, drp, newpre, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
                                                  g.len.as<int32_t>());
   COOC_HIP_TRY(hipGetLastError());
