@@ -753,16 +753,30 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
 // contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight per lane,
 // applying op to every id of the segment (lanes outside it masked).  Returns the batch's groups
 // (uniform); ends with a barrier.
+struct NoHook {
+  __device__ void operator()() const {}
+};
+// hook(): called once per batch right after the scan of its segment lengths (before the group loads) --
+// the caller issues the next batch's descriptor loads there, so that they overlap this batch's walk.
+template <class Hook = NoHook>
 __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
-                                         int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op) {
+                                         int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op,
+                                         const Hook &hook = Hook()) {
   const int tid = threadIdx.x;
   const unsigned long long c_b0 = STAT_CLOCK();
   const uint32_t len = (tid < nb && e > s) ? ((e + 3u) >> 2) - (s >> 2) : 0u;
   uint32_t total;
   const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
+  hook();  // (also for a batch without groups: the caller's next descriptors depend on it)
   if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
   const uint32_t mean = total / uint32_t(nb);
-  const uint32_t S = mean >= 12 ? 16u : 4u;
+#ifndef COOC_SP_SLONG
+#define COOC_SP_SLONG 64u  // whole-wave walkers for long segments: 1.2% faster than 16 (profiles/r03/walker_ab)
+#endif
+#ifndef COOC_SP_SSHORT
+#define COOC_SP_SSHORT 4u
+#endif
+  const uint32_t S = mean >= 12 ? COOC_SP_SLONG : COOC_SP_SSHORT;
   const uint32_t nW = kSpThreads / S;
   if (tid < nb) {
     L.vst[tid] = ex;
@@ -853,18 +867,33 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
   const int tid = threadIdx.x;
+  const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
+  const int ts = full ? 0 : t0, te = full ? A.T : t1;
+  // the ids of tiles [t0, t1) (full: the whole list) of contribution k's list; the descriptors are
+  // software-pipelined over the batches: batch b + 1's list indices are loaded when batch b starts,
+  // their tile starts while batch b walks (sp_walk_batch's hook)
+  auto list_of = [&](int64_t k) -> uint32_t {
+    return BCHK(A, k < A.n_contrib, 1) ? A.vals[k] & kListMask : 0u;
+  };
+  auto seg_of = [&](uint32_t u, uint32_t &s0, uint32_t &e0) {
+    const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
+    s0 = okt ? uint32_t(tbu[ts]) : 0u;
+    e0 = okt ? uint32_t(tbu[te]) : 0u;
+  };
+  uint32_t s0 = 0, e0 = 0, nu = 0, ns = 0, ne = 0;
+  if (k0 + tid < k1 && tid < kSpDb) seg_of(list_of(k0 + tid), s0, e0);
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
-    uint32_t s0 = 0, e0 = 0;
+    const int64_t b1 = b0 + kSpDb;
+    const bool more = b1 + tid < k1 && tid < kSpDb;
     STAT_ADD(19, op.mode == 1 ? 1 : 0);
-    if (tid < nb) {  // the ids of tiles [t0, t1) (full: the whole list) of the contribution's list
-      const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] & kListMask : 0u;
-      const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
-      const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
-      s0 = okt ? uint32_t(tbu[full ? 0 : t0]) : 0u;
-      e0 = okt ? uint32_t(tbu[full ? A.T : t1]) : 0u;
-    }
-    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, s0, e0, op);
+    if (more) nu = list_of(b1 + tid);
+    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, tid < nb ? s0 : 0u, tid < nb ? e0 : 0u, op,
+                            [&]() {
+                              if (more) seg_of(nu, ns, ne);
+                            });
+    s0 = ns;
+    e0 = ne;
     if (uni(S_.flag)) break;
   }
   return walked;
