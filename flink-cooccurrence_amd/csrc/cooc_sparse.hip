@@ -118,8 +118,9 @@ struct SpArgs {
   PlanTotals *tot;
   int32_t *qctr;
   const uint32_t *vals;     // contributions: user index, item-sorted
-  const int32_t *tb;        // [U x (T + 1)] absolute 16-B group index of each tile segment of a user
-  const uint4 *tarena;      // tile-grouped, padded lists in 16-B groups
+  const int32_t *tb;        // [U x (T + 2)] a user's tile-0 range in arena0, its tile starts in arena1
+  const uint4 *tarena;      // arena1: the lists' ids of tiles >= 1 (u32), in 16-B groups
+  const uint4 *tarena0;     // arena0: the lists' tile-0 ids (u16), in 16-B groups
   const int64_t *epre;      // [n_contrib + 1] prefix of the contributions' list lengths (pair work)
   const float *gmass;       // [T] share of the interactions in each tile
   uint32_t *staging;        // [n_split x sstride]
@@ -136,7 +137,7 @@ struct SpArgs {
   unsigned long long *prog;   // COOC_SP_TRACE: per-workgroup progress in pinned host memory
   unsigned long long *stats;  // COOC_SP_STATS: per-phase clocks and counts
   int32_t exp;                // COOC_SP_STATS only: experiment selector (COOC_SP_EXP; results invalid when set)
-  int64_t n_contrib, n_users, n_groups;
+  int64_t n_contrib, n_users, n_groups, n_groups0;
   uint4 *scratch;           // gather mode: per-workgroup tail buckets, scr_cap groups each
   int64_t scr_cap;          // 0: gather mode off
   const int64_t *rowsum;    // [M] closed-form row sums W_a - c_a (k_sp_plan): every whole row is checked
@@ -229,16 +230,25 @@ __device__ inline int32_t sp_split_shares(int64_t W, float g0) {
 }
 
 // ---- planner kernels ------------------------------------------------------------------------------
+// Two arenas hold the users' lists, tile by tile: tile 0 (columns < 16,384: the Zipf head, ~70% of the
+// ids) as u16 ids in arena0 (8 ids per 16-B load; at C3 the 1/8 shard's tile-0 part is ~180 MB and stays
+// in the Infinity Cache), tiles >= 1 as u32 ids in arena1, ids of one tile contiguous, no padding between
+// tiles.  tb[u] has T + 2 entries: tb[u][0] / tb[u][T + 1] = start / end of u's tile-0 ids in arena0
+// (u16 positions), tb[u][t] (1 <= t <= T) = the arena1 position of tile t's first id (tb[u][T] = the end
+// of u's list there).  A chunk reads a tile range of a list as the 16-B groups covering it and masks the
+// ids outside it by position.
+constexpr uint32_t kSink = 0xFFFFFFFFu;
+constexpr uint32_t kSink16 = 0xFFFFu;  // (arena0 pads; never a tile-0 id)
+
 // One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
-// item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and regroups the list by
-// column tile: the list is reordered tile by tile (ids of one tile contiguous, no padding between
-// tiles), tb[u][t] = offset of tile t's first id from the user's base, tb[u][T] = n_u; plen[u] = n_u
-// rounded up to 4 ids (16 B, sink ids at the end: the bases are its prefix, 16-B aligned; k_sp_scatter
-// fills the arena and makes tb absolute).  A chunk reads a tile range of a list as the 16-B groups
-// covering [tb[u][t0], tb[u][t1]) and masks the ids outside it by position.
+// item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and counts the list by tile:
+// tb relative to the user's bases, plen0[u] = its tile-0 ids rounded up to 8 (16 B of u16), plen1[u] =
+// its other ids rounded up to 4 (the bases are their prefixes; k_sp_scatter fills the arenas and makes
+// tb absolute).
 __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
                                                       const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                      int64_t *__restrict__ plen, int32_t *__restrict__ tb,
+                                                      int64_t *__restrict__ plen0, int64_t *__restrict__ plen1,
+                                                      int32_t *__restrict__ tb,
                                                       uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                                                       const int32_t *__restrict__ owner, int32_t part,
                                                       int32_t *__restrict__ ownc, PlanTotals *__restrict__ tot) {
@@ -277,24 +287,27 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (T < 64) {  // exclusive prefix of the tile counts: one wave scan (lane t = tile t)
-      const uint32_t x = lane <= T ? uint32_t(c[lane]) : 0u;
+    int32_t *tbj = tb + j * (T + 2);
+    const int32_t n0 = c[0];
+    if (T < 64) {  // exclusive prefix of tiles 1..T's counts: one wave scan (lane t = tile t)
+      const uint32_t x = (lane >= 1 && lane <= T) ? uint32_t(c[lane]) : 0u;
       const uint32_t inc = wave_incl_scan(x);
-      if (lane <= T) tb[j * (T + 1) + lane] = int32_t(inc - x);
-      if (lane == T) plen[j] = int64_t((inc + 3) & ~3u);  // (tile T is empty: inc = n)
+      if (lane >= 1 && lane <= T) tbj[lane] = int32_t(inc - x);  // (tile T is empty: tbj[T] = n - n0)
     } else {
       if (lane == 0) {
         int32_t run = 0;
-        for (int32_t t = 0; t <= T; t++) {
+        for (int32_t t = 1; t <= T; t++) {
           const int32_t x = c[t];
-          c[t] = run;
+          tbj[t] = run;
           run += x;
         }
-        plen[j] = (run + 3) & ~3;
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (int32_t t = lane; t <= T; t += 64) tb[j * (T + 1) + t] = c[t];
+    }
+    if (lane == 0) {
+      tbj[0] = 0;
+      tbj[T + 1] = n0;
+      plen0[j] = (n0 + 7) & ~7;
+      plen1[j] = (n - n0 + 3) & ~3;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -302,11 +315,9 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
   if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
 }
 
-// The tile arena: user j's list tile by tile at pbase[j] (a multiple of 4 ids), sink ids after its
-// end up to the next multiple of 4.  One wave per user, tile cursors in LDS.  Leaves tb[j][t] = the
-// absolute position (in ids) of tile t's first id (tb[j][T] = the end of j's list), so that a walk
-// needs one descriptor line per user.
-constexpr uint32_t kSink = 0xFFFFFFFFu;
+// The arenas: user j's tile-0 ids at pbase0[j] of arena0 (u16; a multiple of 8; kSink16 pads after
+// them), its other ids tile by tile at pbase1[j] of arena1 (u32; a multiple of 4; kSink pads).  One wave
+// per user, tile cursors in LDS.  Leaves tb absolute, so that a walk needs one descriptor line per user.
 // A contribution's value: the index of the list its row walks; in a streaming window (spre != NULL) with
 // kSelfBit when the walk includes the contribution's own position (a new position walks its user's whole
 // history, an old one only the window's new items, see k_sp_window_contribs).  In a one-window batch every
@@ -314,8 +325,9 @@ constexpr uint32_t kSink = 0xFFFFFFFFu;
 constexpr uint32_t kSelfBit = 0x80000000u, kListMask = 0x7FFFFFFFu;
 __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__restrict__ up,
                                                     const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                    const int64_t *__restrict__ pbase, int32_t *__restrict__ tb,
-                                                    uint32_t *__restrict__ tarena) {
+                                                    const int64_t *__restrict__ pbase0,
+                                                    const int64_t *__restrict__ pbase1, int32_t *__restrict__ tb,
+                                                    uint16_t *__restrict__ arena0, uint32_t *__restrict__ arena1) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int32_t *c = cur[wave];
@@ -324,24 +336,32 @@ __global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__
   for (int64_t j = gw; j < U; j += n_waves) {
     const int64_t s = up[j];
     const int32_t n = int32_t(up[j + 1] - s);
-    const int32_t *tbj = tb + j * (T + 1);
-    uint32_t *o = tarena + pbase[j];
-    for (int32_t t = lane; t <= T; t += 64) c[t] = tbj[t];
+    int32_t *tbj = tb + j * (T + 2);
+    uint16_t *o0 = arena0 + pbase0[j];
+    uint32_t *o1 = arena1 + pbase1[j];
+    for (int32_t t = lane; t < T; t += 64) c[t] = tbj[t];  // (c[0] = 0: the arena0 cursor)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     for (int32_t p = lane; p < n; p += 64) {
       int32_t it = items[s + p];
       if (uint32_t(it) >= uint32_t(M)) it = 0;  // (reported by k_sp_partition)
-      o[atomicAdd(&c[it >> kTShift], 1)] = uint32_t(it);
+      const int32_t t = it >> kTShift;
+      const int32_t q = atomicAdd(&c[t], 1);
+      if (t == 0) o0[q] = uint16_t(it); else o1[q] = uint32_t(it);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const int32_t pend = int32_t(pbase[j + 1] - pbase[j]);
-    if (lane < pend - n) o[n + lane] = kSink;  // (<= 3 pads)
+    const int32_t n0 = tbj[T + 1], n1 = tbj[T];
+    const int32_t p0 = int32_t(pbase0[j + 1] - pbase0[j]), p1 = int32_t(pbase1[j + 1] - pbase1[j]);
+    if (lane < p0 - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
+    if (lane < p1 - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    int32_t *tbw = tb + j * (T + 1);
-    for (int32_t t = lane; t <= T; t += 64) tbw[t] = int32_t(pbase[j] + tbw[t]);
+    if (lane == 0) {
+      tbj[0] = int32_t(pbase0[j]);
+      tbj[T + 1] = int32_t(pbase0[j] + n0);
+    }
+    for (int32_t t = 1 + lane; t <= T; t += 64) tbj[t] = int32_t(pbase1[j] + tbj[t]);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
@@ -706,31 +726,46 @@ struct WalkOp {
   int64_t sbase;  // gather: the workgroup's scratch (16-B groups)
 };
 
-// One 16-B group of partner ids; m = the lanes (bits 0..3) inside the walked segment, the others are
-// ids of a neighbouring tile range or list (or end-of-list sinks) and are skipped.  Gather mode: an id
-// of tile 0 is counted in the dense tile, any other is appended to its tile's bucket (4-B ids, packed).
+// One 16-B group of kIds partner ids (kIds = 4: u32 ids of arena1 or a gather bucket; 8: u16 tile-0 ids
+// of arena0); m = the lanes (bits 0 .. kIds - 1) inside the walked segment, the others are ids of a
+// neighbouring tile range or list (or end-of-list sinks) and are skipped.  Gather mode: an id of tile 0
+// is counted in the dense tile, any other is appended to its tile's bucket (4-B ids, packed).
+template <int kIds>
 __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStatic &S_, const WalkOp &op,
                                       const uint4 &v, uint32_t m) {
-  uint4 w = v;
-  if (!(m & 1u)) w.x = kSink;
-  if (!(m & 2u)) w.y = kSink;
-  if (!(m & 4u)) w.z = kSink;
-  if (!(m & 8u)) w.w = kSink;
+  uint32_t x[kIds];
+  if (kIds == 4) {
+    x[0] = v.x;
+    x[1] = v.y;
+    x[2] = v.z;
+    x[3] = v.w;
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      x[2 * i] = w[i] & 0xFFFFu;
+      x[2 * i + 1] = w[i] >> 16;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kIds; i++)
+    if (!((m >> i) & 1u)) x[i] = kSink;
 #ifdef COOC_SP_STATS
   if (A.exp == 1 && op.mode == 1) {  // timing experiment: hash chunks load their groups but insert nothing
-    if (w.y == 0xFFFFFFFEu) S_.flag = 1u;
+    if (x[1] == 0xFFFFFFFEu) S_.flag = 1u;
     return;
   }
 #endif
   if (op.mode == 1) {
-    sp_hash_insert4(L.R, L.R + kHashMax, w, op.hshift, op.hmask, S_);
+#pragma unroll
+    for (int h = 0; h < kIds; h += 4)
+      sp_hash_insert4(L.R, L.R + kHashMax, make_uint4(x[h], x[h + 1], x[h + 2], x[h + 3]), op.hshift, op.hmask, S_);
     return;
   }
-  const uint32_t x[4] = {w.x, w.y, w.z, w.w};
   if (op.mode == 2) {
     uint32_t *scr = reinterpret_cast<uint32_t *>(A.scratch + op.sbase);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < kIds; i++) {
       if (x[i] == kSink) continue;
       const uint32_t t = x[i] >> kTShift;
       if (t == 0) {
@@ -743,31 +778,25 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
     return;
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < kIds; i++)
     if (x[i] != kSink) atomicAdd(&L.R[x[i] - op.c0], 1u);
 }
 
 // One batch of segments: this thread's segment (tid < nb) is the ids at positions [s, e) of ar (16-B
-// groups; a segment starts and ends anywhere inside a group).  The segments' group counts are
-// block-scanned into virtual starts; walkers of S lanes (S from the mean segment length) own equal
+// groups of kIds ids; a segment starts and ends anywhere inside a group).  The segments' group counts
+// are block-scanned into virtual starts; walkers of S lanes (S from the mean segment length) own equal
 // contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight per lane,
 // applying op to every id of the segment (lanes outside it masked).  Returns the batch's groups
 // (uniform); ends with a barrier.
-struct NoHook {
-  __device__ void operator()() const {}
-};
-// hook(): called once per batch right after the scan of its segment lengths (before the group loads) --
-// the caller issues the next batch's descriptor loads there, so that they overlap this batch's walk.
-template <class Hook = NoHook>
+template <int kIds>
 __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
-                                         int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op,
-                                         const Hook &hook = Hook()) {
+                                         int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op) {
+  constexpr uint32_t kSh = kIds == 8 ? 3u : 2u, kLo = kIds - 1;
   const int tid = threadIdx.x;
   const unsigned long long c_b0 = STAT_CLOCK();
-  const uint32_t len = (tid < nb && e > s) ? ((e + 3u) >> 2) - (s >> 2) : 0u;
+  const uint32_t len = (tid < nb && e > s) ? ((e + kLo) >> kSh) - (s >> kSh) : 0u;
   uint32_t total;
   const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
-  hook();  // (also for a batch without groups: the caller's next descriptors depend on it)
   if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
   const uint32_t mean = total / uint32_t(nb);
 #ifndef COOC_SP_SLONG
@@ -780,8 +809,8 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   const uint32_t nW = kSpThreads / S;
   if (tid < nb) {
     L.vst[tid] = ex;
-    L.gb[tid] = int32_t(s >> 2) - int32_t(ex);
-    L.info[tid] = ((e - (s & ~3u)) << 2) | (s & 3u);
+    L.gb[tid] = int32_t(s >> kSh) - int32_t(ex);
+    L.info[tid] = ((e - (s & ~kLo)) << 3) | (s & kLo);
     if (len) {
       const uint32_t q0 = uint32_t((uint64_t(ex) * nW + total - 1) / total);
       const uint32_t q1 = uint32_t((uint64_t(ex + len) * nW + total - 1) / total);
@@ -811,28 +840,29 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
       }
       int64_t gi = int64_t(gb) + int64_t(gk);
 #ifdef COOC_SP_STATS
-      if (A.exp == 2 && op.mode != 2 && (gk & 1u)) gi = -1;  // (the experiment above: no load)
+      if (A.exp == 2 && op.mode != 2 && (gk & 1u)) gi = -1;  // (the experiment below: no load)
 #endif
       const uint32_t qq = gk - vs;
-      const uint32_t lo_l = qq ? 0u : (inf & 3u);
-      const int32_t hi_l = min(4, int32_t(inf >> 2) - 4 * int32_t(qq));
+      const uint32_t lo_l = qq ? 0u : (inf & 7u);
+      const int32_t hi_l = min(int32_t(kIds), int32_t(inf >> 3) - int32_t(kIds) * int32_t(qq));
       m = ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);
 #ifdef COOC_SP_STATS
       if (gi < 0) {
         v = make_uint4(kSink, kSink, kSink, kSink);
+        m = 0;
         return;
       }
 #endif
       v = BCHK(A, gi >= 0 && gi < nsrc, 8) ? ar[gi] : make_uint4(kSink, kSink, kSink, kSink);
     };
     uint4 v[kSpU] = {};
-    uint32_t m = 0;  // 4 lane bits per group in flight
+    uint32_t m = 0;  // 8 lane bits per group in flight
 #pragma unroll
     for (int k = 0; k < kSpU; k++) {
       const uint32_t gk = g + S * k;
       uint32_t mk = 0;
       if (gk < hi) fetch(gk, v[k], mk);
-      m |= mk << (4 * k);
+      m |= mk << (8 * k);
     }
     for (; g < hi; g += S * kSpU) {
       uint4 vn[kSpU] = {};
@@ -842,16 +872,14 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
         const uint32_t gk = g + S * (kSpU + k);
         uint32_t mk = 0;
         if (gk < hi) fetch(gk, vn[k], mk);
-        mn |= mk << (4 * k);
+        mn |= mk << (8 * k);
       }
 #pragma unroll
       for (int k = 0; k < kSpU; k++) {
-#ifdef COOC_SP_STATS
-        // timing experiment (results invalid): every other group of dense / hash walks is not loaded or
-        // applied -- how much of a walk is the group delivery
-        if (A.exp == 2 && op.mode != 2 && ((g + S * k) & 1u)) continue;
-#endif
-        if ((m >> (4 * k)) & 15u) sp_apply_group(A, L, S_, op, v[k], (m >> (4 * k)) & 15u);
+        // (stats build, COOC_SP_EXP=2, results invalid: every other group of dense / hash walks is neither
+        // loaded nor applied -- how much of a walk is the group delivery)
+        const uint32_t mk = (m >> (8 * k)) & 255u;
+        if (mk) sp_apply_group<kIds>(A, L, S_, op, v[k], mk);
       }
 #pragma unroll
       for (int k = 0; k < kSpU; k++) v[k] = vn[k];
@@ -863,37 +891,35 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   return total;
 }
 
+// Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
+// applying op to every id: the tile-0 part of the lists from arena0 (u16, 8 ids per load), the rest from
+// arena1 (u32), a batch of kSpDb contributions at a time.  Returns the groups walked.
 __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0,
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
   const int tid = threadIdx.x;
   const bool okt = BCHK(A, t0 >= 0 && t1 <= A.T && t0 <= t1, 4);
-  const int ts = full ? 0 : t0, te = full ? A.T : t1;
-  // the ids of tiles [t0, t1) (full: the whole list) of contribution k's list; the descriptors are
-  // software-pipelined over the batches: batch b + 1's list indices are loaded when batch b starts,
-  // their tile starts while batch b walks (sp_walk_batch's hook)
-  auto list_of = [&](int64_t k) -> uint32_t {
-    return BCHK(A, k < A.n_contrib, 1) ? A.vals[k] & kListMask : 0u;
-  };
-  auto seg_of = [&](uint32_t u, uint32_t &s0, uint32_t &e0) {
-    const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 1);
-    s0 = okt ? uint32_t(tbu[ts]) : 0u;
-    e0 = okt ? uint32_t(tbu[te]) : 0u;
-  };
-  uint32_t s0 = 0, e0 = 0, nu = 0, ns = 0, ne = 0;
-  if (k0 + tid < k1 && tid < kSpDb) seg_of(list_of(k0 + tid), s0, e0);
+  const bool has0 = full || t0 == 0;                 // (uniform)
+  const int ta = full ? 1 : max(t0, 1), tz = full ? A.T : t1;
+  const bool has1 = tz > ta;
   for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
     const int nb = int(min<int64_t>(kSpDb, k1 - b0));
-    const int64_t b1 = b0 + kSpDb;
-    const bool more = b1 + tid < k1 && tid < kSpDb;
+    uint32_t s0 = 0, e0 = 0, s1 = 0, e1 = 0;
     STAT_ADD(19, op.mode == 1 ? 1 : 0);
-    if (more) nu = list_of(b1 + tid);
-    walked += sp_walk_batch(A, L, S_, A.tarena, A.n_groups, nb, tid < nb ? s0 : 0u, tid < nb ? e0 : 0u, op,
-                            [&]() {
-                              if (more) seg_of(nu, ns, ne);
-                            });
-    s0 = ns;
-    e0 = ne;
+    if (tid < nb && okt) {
+      const uint32_t u = BCHK(A, b0 + tid < A.n_contrib, 1) ? A.vals[b0 + tid] & kListMask : 0u;
+      const int32_t *tbu = A.tb + int64_t(BCHK(A, u < A.n_users, 2) ? u : 0u) * (A.T + 2);
+      if (has0) {
+        s0 = uint32_t(tbu[0]);
+        e0 = uint32_t(tbu[A.T + 1]);
+      }
+      if (has1) {
+        s1 = uint32_t(tbu[ta]);
+        e1 = uint32_t(tbu[tz]);
+      }
+    }
+    if (has0) walked += sp_walk_batch<8>(A, L, S_, A.tarena0, A.n_groups0, nb, s0, e0, op);
+    if (has1) walked += sp_walk_batch<4>(A, L, S_, A.tarena, A.n_groups, nb, s1, e1, op);
     if (uni(S_.flag)) break;
   }
   return walked;
@@ -1292,7 +1318,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const int nb = t1 - t;
         const uint32_t bs = tid < nb ? S_.bstart[t + tid] : 0u;
         const uint32_t be = tid < nb ? bs + S_.bcur[t + tid] : 0u;
-        walked = sp_walk_batch(A, L, S_, A.scratch + op.sbase, A.scr_cap, nb, bs, be, op);
+        walked = sp_walk_batch<4>(A, L, S_, A.scratch + op.sbase, A.scr_cap, nb, bs, be, op);
       } else {  // (also a gathered chunk whose bucket overflowed)
         walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
       }
@@ -1540,36 +1566,26 @@ __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict
 // processed in batches of at most kSrBatchPairs pairs.
 constexpr int kSrThreads = 256;
 
-// One workgroup per deferred row of the batch: every contribution's list (the whole tile-grouped list,
-// sinks skipped) appended to the row's key range at kbase[j] + (epre[k] - epre[k0]), in list order.
+// One workgroup per deferred row of the batch: every contribution's list (its tile-0 ids from arena0,
+// the rest from arena1) appended to the row's key range at kbase[j] + (epre[k] - epre[k0]).
 __global__ __launch_bounds__(kSrThreads) void k_sr_expand(const int32_t *__restrict__ rows, const int64_t *__restrict__ kbase,
                                                           const int64_t *__restrict__ row_ptr,
                                                           const int64_t *__restrict__ epre,
                                                           const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb,
-                                                          const uint4 *__restrict__ tarena, int32_t T,
+                                                          const uint16_t *__restrict__ arena0,
+                                                          const uint32_t *__restrict__ arena1, int32_t T,
                                                           uint64_t *__restrict__ keys) {
   const int j = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int32_t a = rows[j];
   const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1], e0 = epre[k0];
   const uint64_t tag = uint64_t(j) << 32;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int64_t k = k0 + wave; k < k1; k += kSrThreads / 64) {
     const uint32_t u = vals[k] & kListMask;
-    const int32_t g0 = tb[int64_t(u) * (T + 1)] >> 2, g1 = (tb[int64_t(u) * (T + 1) + T] + 3) >> 2;
+    const int32_t *tbu = tb + int64_t(u) * (T + 2);
+    const int32_t s0 = tbu[0], n0 = tbu[T + 1] - s0, s1 = tbu[1], n1 = tbu[T] - s1;
     uint64_t *o = keys + kbase[j] + (epre[k] - e0);
-    int64_t pos = 0;
-    for (int32_t g = g0; g < g1; g += 64) {
-      uint4 v = make_uint4(kSink, kSink, kSink, kSink);
-      if (g + lane < g1) v = tarena[g + lane];
-      const uint32_t id[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t c = (v.x != kSink) + (v.y != kSink) + (v.z != kSink) + (v.w != kSink);
-      const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
-      int64_t q = pos + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt);
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (id[i] != kSink) o[q++] = tag | id[i];
-      pos += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2);
-    }
+    for (int32_t q = lane; q < n0; q += 64) o[q] = tag | uint32_t(arena0[s0 + q]);
+    for (int32_t q = lane; q < n1; q += 64) o[n0 + q] = tag | arena1[s1 + q];
   }
 }
 
@@ -1670,7 +1686,8 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t *b = buf[wave];
   const int64_t first = A.tot->n_chunks - A.tot->n_tiny, n_tiny = A.tot->n_tiny;
-  const uint32_t *ar = reinterpret_cast<const uint32_t *>(A.tarena);
+  const uint16_t *a0 = reinterpret_cast<const uint16_t *>(A.tarena0);
+  const uint32_t *a1 = reinterpret_cast<const uint32_t *>(A.tarena);
   int64_t slab_cur = 0, slab_end = 0;  // (wave-uniform)
   for (;;) {
     int64_t i = 0;
@@ -1683,21 +1700,25 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
     // 1. the contributions' lists (whole lists), 64 at a time, into b in list order
     uint32_t W = 0;
     for (int64_t c0 = k0; c0 < k1; c0 += 64) {
-      uint32_t s0 = 0, e0 = 0;
+      uint32_t s0 = 0, n0 = 0, s1 = 0, n1 = 0;
       if (c0 + lane < k1) {
         const uint32_t u = A.vals[c0 + lane] & kListMask;
-        const int32_t *tbu = A.tb + int64_t(u) * (A.T + 1);
+        const int32_t *tbu = A.tb + int64_t(u) * (A.T + 2);
         s0 = uint32_t(tbu[0]);
-        e0 = uint32_t(tbu[A.T]);
+        n0 = uint32_t(tbu[A.T + 1]) - s0;
+        s1 = uint32_t(tbu[1]);
+        n1 = uint32_t(tbu[A.T]) - s1;
       }
-      const uint32_t len = e0 - s0, inc = wave_incl_scan(len);
+      const uint32_t len = n0 + n1, inc = wave_incl_scan(len);
       const uint32_t tot = __shfl(inc, 63, 64);
       if (W + tot > uint32_t(kTinyW)) {  // (cannot happen: the planner's W bounds it)
         if (lane == 0) atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
         W = 0;
         break;
       }
-      for (uint32_t q = 0; q < len; q++) b[W + inc - len + q] = ar[s0 + q];
+      uint32_t *d = b + W + inc - len;
+      for (uint32_t q = 0; q < n0; q++) d[q] = a0[s0 + q];
+      for (uint32_t q = 0; q < n1; q++) d[n0 + q] = a1[s1 + q];
       W += tot;
     }
     // 2. bitonic sort of b[0, n2), padded with kSink
@@ -1867,9 +1888,11 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
-  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(n1 + 3 * U1 + 16)));  // lists padded to 4 ids
-  COOC_TRY(sp_pbase_.reserve(sizeof(int64_t) * size_t(2 * U1 + 2)));    // plen [U], pbase [U + 1]
-  COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 1)));
+  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(n1 + 3 * U1 + 16)));   // arena1: lists padded to 4 ids
+  COOC_TRY(sp_arena0_.reserve(sizeof(uint16_t) * size_t(n1 + 7 * U1 + 16)));  // arena0: tile-0 ids padded to 8
+  COOC_TRY(sp_pbase_.reserve(sizeof(int64_t) * size_t(4 * U1 + 4)));    // plen0, pbase0, plen1, pbase1
+  COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 2)));
+  if (n1 + 7 * U1 + 16 > int64_t(INT32_MAX)) return Status{1, "more than 2^31 arena positions in one window"};
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
   COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
@@ -1908,7 +1931,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   tmp = std::max(tmp, q);
   COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, q, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), M, s));
   tmp = std::max(tmp, q);
-  int64_t *plen = sp_pbase_.as<int64_t>(), *pbase = plen + U1;
+  int64_t *plen = sp_pbase_.as<int64_t>(), *pbase = plen + U1;  // (tile-0 part; the rest after it)
+  int64_t *plen1 = pbase + U1 + 1, *pbase1 = plen1 + U1;
   COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, pbase + 1, int(U1), s));
   tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
@@ -1920,17 +1944,20 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
   }
   if (U > 0) {
-    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, sp_tb_.as<int32_t>(),
+    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, plen1, sp_tb_.as<int32_t>(),
                                                            win ? nullptr : keys_in, vals_in, owner, part,
                                                            sp_ownc_.as<int32_t>(), tot);
     COOC_HIP_TRY(hipGetLastError());
   }
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(pbase1, 0, sizeof(int64_t), s));
   if (U > 0) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
-    k_sp_scatter<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, pbase, sp_tb_.as<int32_t>(),
-                                                         sp_arena_.as<uint32_t>());
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen1, pbase1 + 1, int(U), s));
+    k_sp_scatter<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, pbase, pbase1, sp_tb_.as<int32_t>(),
+                                                         sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>());
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
@@ -2084,6 +2111,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.vals = vals;
   proto.tb = sp_tb_.as<int32_t>();
   proto.tarena = sp_arena_.as<uint4>();
+  proto.tarena0 = sp_arena0_.as<uint4>();
   proto.epre = epre;
   proto.gmass = gmass;
   proto.split_slot = split_slot_.as<int32_t>();
@@ -2096,6 +2124,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.n_contrib = n_c;
   proto.n_users = U;
   proto.n_groups = (n1 + 3 * U1) / 4 + 4;
+  proto.n_groups0 = (n1 + 7 * U1) / 8 + 4;
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   proto.rowsum = rowsum_.as<int64_t>();
@@ -2303,7 +2332,7 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
       int64_t *rstart = kbase + (nb + 1);
       COOC_HIP_TRY(hipMemcpyAsync(kbase, kb.data(), sizeof(int64_t) * size_t(nb + 1), hipMemcpyHostToDevice, s));
       k_sr_expand<<<unsigned(nb), kSrThreads, 0, s>>>(rows + j0, kbase, row_ptr, epre, vals, sp_tb_.as<int32_t>(),
-                                                      sp_arena_.as<uint4>(), T, keys);
+                                                      sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), T, keys);
       COOC_HIP_TRY(hipGetLastError());
       size_t b = sort_tmp_.cap;
       COOC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(sort_tmp_.p, b, keys, keys2, int(acc), 0, 32 + bits_for(nb + 1), s));
