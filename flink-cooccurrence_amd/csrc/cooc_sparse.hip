@@ -805,7 +805,10 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
 #ifndef COOC_SP_SSHORT
 #define COOC_SP_SSHORT 4u
 #endif
-  const uint32_t S = mean >= 12 ? COOC_SP_SLONG : COOC_SP_SSHORT;
+#ifndef COOC_SP_STIER
+#define COOC_SP_STIER 32  // segments of >= 32 groups: whole-wave walkers, >= 12: 16 lanes (profiles/r03/walker_ab)
+#endif
+  const uint32_t S = mean >= COOC_SP_STIER ? COOC_SP_SLONG : mean >= 12 ? 16u : COOC_SP_SSHORT;
   const uint32_t nW = kSpThreads / S;
   if (tid < nb) {
     L.vst[tid] = ex;
