@@ -1070,21 +1070,30 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   const int per = H / kSpThreads;
   const int32_t nL1 = (c1 - c0 + 1023) >> 10;
   uint32_t ek[kHashMax / kSpThreads], ec[kHashMax / kSpThreads], er[kHashMax / kSpThreads];
+  // the table swept 4 slots (16 B) per LDS access: thread tid takes slots 4 (tid + q kSpThreads) .. + 3
+  (void)per;
 #pragma unroll
-  for (int i = 0; i < kHashMax / kSpThreads; i++) {
-    ek[i] = ~0u;
-    ec[i] = 0u;
-    er[i] = 0u;
-    if (i < per) {
-      const int j = tid + i * kSpThreads;
-      const uint32_t k = keys[j], v = cnts[j];
-      keys[j] = 0u;
-      cnts[j] = 0u;
-      if (k && v) {
-        const uint32_t col = k - 1u - uint32_t(c0);
+  for (int q = 0; q < kHashMax / (4 * kSpThreads); q++) {
+    const int j = 4 * (tid + q * kSpThreads);
+    uint4 k4 = make_uint4(0u, 0u, 0u, 0u), v4 = k4;
+    if (j < H) {
+      k4 = *reinterpret_cast<const uint4 *>(keys + j);
+      v4 = *reinterpret_cast<const uint4 *>(cnts + j);
+      *reinterpret_cast<uint4 *>(keys + j) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4 *>(cnts + j) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint32_t kk[4] = {k4.x, k4.y, k4.z, k4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = 4 * q + u;
+      ek[i] = ~0u;
+      ec[i] = 0u;
+      er[i] = 0u;
+      if (kk[u] && vv[u]) {
+        const uint32_t col = kk[u] - 1u - uint32_t(c0);
         ek[i] = col;
-        ec[i] = v;
-        rsum += v;
+        ec[i] = vv[u];
+        rsum += vv[u];
         atomicOr(&L.L1[col >> 10], 1u << ((col >> 5) & 31u));
       }
     }
