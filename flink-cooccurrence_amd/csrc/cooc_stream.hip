@@ -149,7 +149,8 @@ __device__ inline double llr_terms(double all, double x_k11k12, double x_k21k22,
 // Per column b of the rescored rows (the int32 view of its row sum unless exact): rs = rowSum(b) and the
 // terms of an entry with k11 == 1 that depend on b only (ItemRowRescorer...java:230-240): k11 + k21 =
 // rs, k21 = rs - 1, k12 + k22 = observed + 2 - rs.  32 B per column, one line per gathered entry.
-constexpr int kRsR = 8;   // 64-entry steps scored before the heap is fed (per wave)
+constexpr int kRsR = 8;  // 64-entry steps scored before the heap is fed (per wave)
+constexpr int64_t kRsChunk = kRsR * 64;
 struct alignas(32) ColTerms {
   int64_t rs;
   double x_rs;   // xlogx(rs)
@@ -164,6 +165,17 @@ __global__ void k_col_terms(int32_t M, const int64_t *__restrict__ grs, const in
   const int64_t observed = exact ? obs[1] : obs[0];
   const int64_t rs = exact ? grs[b] : int64_t(int32_t(uint32_t(uint64_t(grs[b]))));
   out[b] = ColTerms{rs, xlogx(rs), xlogx(rs - 1), xlogx(observed + 2 - rs)};
+}
+
+// xlogx(k11) and xlogx(observed + 2 k11) for every int16 k11 (index k11 + 32768; the second table at
+// + 65536): the two terms of the full LLR that depend on the count alone.
+__global__ void k_k11_terms(const int64_t *__restrict__ obs, int32_t exact, double *__restrict__ out) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 65536) return;
+  const int64_t observed = exact ? obs[1] : obs[0];
+  const int64_t k11 = int64_t(i) - 32768;
+  out[i] = xlogx(k11);
+  out[i + 65536] = xlogx(observed + 2 * k11);
 }
 
 // ---- IntDoublePriorityQueue.java:132-205, every lane of the wave runs it on the same LDS heap ----
@@ -221,19 +233,97 @@ struct CsrRows {
   }
 };
 
-// One wave per rescored row, rows iterated in ascending column order (the tie contract).  The wave
-// scores kRsR steps of 64 entries, then feeds the lanes that can enter the heap to it step by step in
-// lane order, which is exactly the sequential loop of ItemRowRescorer...java:199-223.  Scoring is
-// split by count so that the wave's lanes do not diverge over the expensive case: an entry with
-// k11 == 1 (most of a sparse row) needs one log (every other term comes from the per-column table
-// and the row's constants); the others (hot pairs, wrapped or zero int16 views) are queued in LDS and
-// scored 64 at a time with the full formula (7 logs).  Both are LogLikelihood.java:41-57 in Java's operation order, bit for bit.
-// rows == nullptr: rescored row t is item t.  obs[0] = the rescorer's observed (sum of int
-// deltas), obs[1] = the exact pair count.
+// Per-row constants of the rescorer's LLR (ItemRowRescorer...java:199-205): k11k12 = k11 + k12 = rs_a;
+// with k11 == 1 also k11k12 + k21k22 = observed + 2, k21k22 = observed + 2 - rs_a, k12 = rs_a - 1.
+struct RowTerms {
+  int64_t observed, rs_a;
+  double x_a, x_all1, x_r1, x_a1;
+  __device__ RowTerms(int64_t obs, int64_t rs) : observed(obs), rs_a(rs) {
+    x_a = xlogx(rs);
+    x_all1 = xlogx(obs + 2);
+    x_r1 = xlogx(obs + 2 - rs);
+    x_a1 = xlogx(rs - 1);
+  }
+};
+
+// Scores the kRsR * 64 entries [i0, i0 + kRsR * 64) of row a into the wave's LDS ring: rscore[k] = the
+// entry's LLR, rcol[k] = its column (-1: no entry or a zero count).  Scoring is split by count so that
+// the wave's lanes do not diverge over the expensive case: an entry with k11 == 1 (most of a sparse
+// row) needs one log (every other term comes from the per-column table and the row's constants); the
+// others (hot pairs, wrapped or zero int16 views) are queued in LDS and scored 64 at a time with the
+// full formula (5 logs; the two terms that depend on k11 alone come from k_k11_terms' tables).  Both
+// are LogLikelihood.java:41-57 in Java's operation order, bit for bit.
+template <class Rows>
+__device__ inline void rs_score_chunk(const Rows &src, int32_t a, int64_t i0, int64_t n, const RowTerms &R,
+                                      int32_t exact, const ColTerms *__restrict__ cterm,
+                                      const double *__restrict__ k11t, double *rscore, int32_t *rcol, int32_t *rq) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t npend = 0;
+  int32_t cj[kRsR];
+  uint32_t vj[kRsR];
+#pragma unroll
+  for (int j = 0; j < kRsR; j++) {  // all kRsR steps' loads in flight at once
+    cj[j] = 0;
+    vj[j] = 0u;
+    if (i0 + j * 64 + lane < n) src.get(a, i0 + j * 64 + lane, cj[j], vj[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kRsR; j++) {
+    const int32_t c = cj[j];
+    const uint32_t v = vj[j];
+    const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+    const bool fast = v != 0u && k11 == 1;
+    double score = 0.0;
+    if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+      const ColTerms t = cterm[c];
+      const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (t.rs - k11);
+      score = llr_terms(R.x_all1, R.x_a, R.x_r1, t.x_rs, t.x_or2, 0.0, R.x_a1, t.x_rs1, xlogx(k22));
+    }
+    const bool slow = v != 0u && !fast;
+    const uint64_t sm = __ballot(slow);
+    if (slow) rq[npend + uint32_t(__popcll(sm & lt))] = j * 64 + lane;
+    npend += uint32_t(__popcll(sm));
+    rscore[j * 64 + lane] = slow ? __longlong_as_double(k11) : score;  // slow: k11 parked until scored
+    rcol[j * 64 + lane] = v != 0u ? c : -1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t p = lane; p < npend; p += 64) {  // LogLikelihood.java:41-57, k11k12 and k11 + k21 from tables
+    const int32_t idx = rq[p];
+    const int32_t c = rcol[idx];
+    const int64_t k11 = __double_as_longlong(rscore[idx]);
+    const ColTerms h = cterm[c];
+    const int64_t k12 = R.rs_a - k11;
+    const int64_t k21 = h.rs - k11;
+    const int64_t k22 = R.observed + k11 - k12 - k21;
+    // xlogx(k11) and xlogx(k11 + k12 + k21 + k22) = xlogx(observed + 2 k11) depend on k11 only: tables
+    // over the int16 range (the same function, so the same bits)
+    const bool in = k11 >= -32768 && k11 < 32768;
+    const double x_all = in ? k11t[k11 + 32768 + 65536] : xlogx(k11 + k12 + (k21 + k22));
+    const double x_11 = in ? k11t[k11 + 32768] : xlogx(k11);
+    rscore[idx] = llr_terms(x_all, R.x_a, xlogx(k21 + k22), h.x_rs, xlogx(k12 + k22), x_11, xlogx(k12), xlogx(k21),
+                            xlogx(k22));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline int64_t rs_row_sum(const int64_t *__restrict__ grs, int32_t a, int32_t exact) {
+  return exact ? grs[a] : int64_t(int32_t(uint32_t(uint64_t(grs[a]))));
+}
+
+// One wave per rescored row, taken from a counter (rows with long lists, the Zipf head, go first and
+// no wave is left with a static share of them), rows iterated in ascending column order (the tie
+// contract).  The wave scores kRsR steps of 64 entries (rs_score_chunk), then feeds the lanes that can
+// enter the heap to it step by step in lane order, which is exactly the sequential loop of
+// ItemRowRescorer...java:199-223.  rows == nullptr: rescored row t is item t.  obs[0] = the
+// rescorer's observed (sum of int deltas), obs[1] = the exact pair count.
 template <class Rows>
 __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__restrict__ n_rows_p, Rows src,
                           const int64_t *__restrict__ grs, const ColTerms *__restrict__ cterm,
-                          const int64_t *__restrict__ obs, int32_t exact,
+                          const double *__restrict__ k11t,
+                          const int64_t *__restrict__ obs, int32_t exact, unsigned long long *__restrict__ row_ctr,
                           int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
                           double *__restrict__ out_score) {
   extern __shared__ double smem[];
@@ -241,59 +331,20 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + int64_t(waves) * (topk + 1)) + int64_t(wave) * (topk + 1);
   double *ring = smem + int64_t(waves) * (topk + 1) + (int64_t(waves) * (topk + 1) + 1) / 2;
-  double *rscore = ring + int64_t(wave) * (kRsR * 64) * 2;
-  int32_t *rcol = reinterpret_cast<int32_t *>(rscore + kRsR * 64);
-  int32_t *rq = rcol + kRsR * 64;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  double *rscore = ring + int64_t(wave) * kRsChunk * 2;
+  int32_t *rcol = reinterpret_cast<int32_t *>(rscore + kRsChunk);
+  int32_t *rq = rcol + kRsChunk;
   const int64_t n_rows = n_rows_p[0];
   const int64_t observed = exact ? obs[1] : obs[0];
-  for (int64_t t = int64_t(blockIdx.x) * waves + wave; t < n_rows; t += int64_t(gridDim.x) * waves) {
+  for (int64_t t = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 1ull)) : 0ll, 0, 64); t < n_rows;
+       t = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 1ull)) : 0ll, 0, 64)) {
     const int32_t a = rows ? rows[t] : int32_t(t);
-    const int64_t rs_a = exact ? grs[a] : int64_t(int32_t(uint32_t(uint64_t(grs[a]))));
+    const RowTerms R(observed, rs_row_sum(grs, a, exact));
     const int64_t n = src.size(a);
-    // row terms: k11k12 = k11 + k12 = rs_a; with k11 == 1 also k11k12 + k21k22 = observed + 2,
-    // k21k22 = observed + 2 - rs_a, k12 = rs_a - 1
-    const double x_a = xlogx(rs_a), x_all1 = xlogx(observed + 2), x_r1 = xlogx(observed + 2 - rs_a),
-                 x_a1 = xlogx(rs_a - 1);
     int32_t size = 0;
     double least = 0.0;
-    for (int64_t i0 = 0; i0 < n; i0 += kRsR * 64) {
-      uint32_t npend = 0;
-#pragma unroll 2
-      for (int j = 0; j < kRsR; j++) {
-        int32_t c = 0;
-        uint32_t v = 0u;
-        if (i0 + j * 64 + lane < n) src.get(a, i0 + j * 64 + lane, c, v);
-        const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
-        const bool fast = v != 0u && k11 == 1;
-        double score = 0.0;
-        if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
-          const ColTerms t = cterm[c];
-          const int64_t k22 = observed + k11 - (rs_a - k11) - (t.rs - k11);
-          score = llr_terms(x_all1, x_a, x_r1, t.x_rs, t.x_or2, 0.0, x_a1, t.x_rs1, xlogx(k22));
-        }
-        const bool slow = v != 0u && !fast;
-        const uint64_t sm = __ballot(slow);
-        if (slow) rq[npend + uint32_t(__popcll(sm & lt))] = j * 64 + lane;
-        npend += uint32_t(__popcll(sm));
-        rscore[j * 64 + lane] = slow ? __longlong_as_double(k11) : score;  // slow: k11 parked until scored
-        rcol[j * 64 + lane] = v != 0u ? c : -1;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t p = lane; p < npend; p += 64) {  // LogLikelihood.java:41-57, k11k12 and k11 + k21 from tables
-        const int32_t idx = rq[p];
-        const int32_t c = rcol[idx];
-        const int64_t k11 = __double_as_longlong(rscore[idx]);
-        const ColTerms h = cterm[c];
-        const int64_t k12 = rs_a - k11;
-        const int64_t k21 = h.rs - k11;
-        const int64_t k22 = observed + k11 - k12 - k21;
-        rscore[idx] = llr_terms(xlogx(k11 + k12 + (k21 + k22)), x_a, xlogx(k21 + k22), h.x_rs, xlogx(k12 + k22),
-                                xlogx(k11), xlogx(k12), xlogx(k21), xlogx(k22));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+    for (int64_t i0 = 0; i0 < n; i0 += kRsChunk) {
+      rs_score_chunk(src, a, i0, n, R, exact, cterm, k11t, rscore, rcol, rq);
       for (int j = 0; j < kRsR && i0 + j * 64 < n; j++) {
         const int32_t c = rcol[j * 64 + lane];
         const double score = rscore[j * 64 + lane];
@@ -586,8 +637,14 @@ template <class Rows>
 Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_rows_dev, int64_t max_rows, Rows src,
                            int32_t M, const int64_t *grs, const int64_t *obs, bool exact, int32_t topk,
                            DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score) {
-  COOC_TRY(terms.reserve(sizeof(ColTerms) * size_t(std::max(M, 1))));
+  // terms: [ColTerms x M][the rows counter][k11 tables: 2 x 65536 doubles]
+  const size_t o_ctr = (sizeof(ColTerms) * size_t(std::max(M, 1)) + 255) & ~size_t(255);
+  COOC_TRY(terms.reserve(o_ctr + 256 + sizeof(double) * 2 * 65536));
+  auto *row_ctr = reinterpret_cast<unsigned long long *>(static_cast<char *>(terms.p) + o_ctr);
+  auto *k11t = reinterpret_cast<double *>(static_cast<char *>(terms.p) + o_ctr + 256);
+  COOC_HIP_TRY(hipMemsetAsync(row_ctr, 0, sizeof(unsigned long long), s));
   k_col_terms<<<blocks_for(M, 256), 256, 0, s>>>(M, grs, obs, exact ? 1 : 0, terms.as<ColTerms>());
+  k_k11_terms<<<256, 256, 0, s>>>(obs, exact ? 1 : 0, k11t);
   const int waves = rescore_waves_per_block(topk);
   const size_t lds = rescore_lds_bytes(topk);
   if (lds > 160 * 1024 - 256) return Status{1, "topk too large for the LDS heaps"};
@@ -599,8 +656,8 @@ Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   const int64_t want = (max_rows + waves - 1) / waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
-  k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), obs, exact ? 1 : 0, topk,
-                                                 out_size, out_val, out_score);
+  k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), k11t, obs, exact ? 1 : 0,
+                                                 row_ctr, topk, out_size, out_val, out_score);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }

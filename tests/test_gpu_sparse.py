@@ -387,3 +387,51 @@ def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda, M):
     ex, v32 = op.core.global_rowsums()
     assert np.array_equal(ex[gi], gex) and np.array_equal(v32[gi], gv32)
     op.close()
+
+
+def test_c5_topk_long_rows_vs_oracle(pkg, oracle, torch_cuda):
+    """Rows of >= 32,768 entries take the rescorer's long-row prepass (every 512-entry chunk scored in
+    parallel for its largest score; the row's wave skips the chunks that cannot enter its full heap).
+    Two hubs: item 0 with 45,000 partners of near-equal counts (ties everywhere: a chunk whose maximum
+    equals the heap's least must be skipped exactly like the sequential loop skips its entries), and
+    item 1 whose partners' counts grow with the column (every later chunk beats the heap).  Both heaps,
+    and short rows, against the oracle's rescorer (ItemRowRescorer...java:195-241), through the whole-
+    batch launch and the sampled-rows launch."""
+    torch = torch_cuda
+    from tests._helpers import assert_row_topk, oracle_row_topk
+
+    M, k = 50_000, 50
+    rng = np.random.default_rng(31)
+    users = []
+    for b in range(2, 45_002):
+        users.append([0, b])
+        if b % 997 == 0:
+            users.append([0, b])  # a few partners of hub 0 with count 2
+    for b in range(2, 40_002, 1):
+        for _ in range(1 + (b - 2) // 8_000):
+            users.append([1, b])  # hub 1: counts 1..5 rising with the column
+    for _ in range(20_000):
+        users.append(sorted(rng.choice(np.arange(2, M), 3, replace=False).tolist()))
+    lens = np.array([len(u) for u in users], np.int64)
+    up = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    it = np.concatenate([np.array(u, np.int32) for u in users])
+    dev = torch.device("cuda")
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        got = core.count(up, it)
+        rs32 = got.rowsum32.astype(np.int64)
+        observed = int(rs32.sum())
+        assert got.row_ptr[1] - got.row_ptr[0] >= 45_000 and got.row_ptr[2] - got.row_ptr[1] >= 40_000
+        sz = torch.empty(M, dtype=torch.int32, device=dev)
+        v = torch.empty((M, k), dtype=torch.int32, device=dev)
+        sc = torch.empty((M, k), dtype=torch.float64, device=dev)
+        core.topk_batch_device(k, sz, v, sc)
+        sz, v, sc = sz.cpu().numpy(), v.cpu().numpy(), sc.cpu().numpy()
+        sample = np.array([0, 1, 2, 500, 20_001, 44_999], np.int64)
+        s_sz, s_v, s_sc = core.topk_items(sample, k)
+    for i, a in enumerate(sample.tolist()):
+        s, e = got.row_ptr[a], got.row_ptr[a + 1]
+        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed)
+        assert_row_topk(sz[a], v[a], sc[a], want, where=f"batch row {a}")
+        assert_row_topk(s_sz[i], s_v[i], s_sc[i], want, where=f"sampled row {a}")
+        n = int(sz[a])
+        assert np.array_equal(v[a, :n], s_v[i, :n]) and np.array_equal(sc[a, :n], s_sc[i, :n], equal_nan=True)
