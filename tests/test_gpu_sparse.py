@@ -390,13 +390,12 @@ def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda, M):
 
 
 def test_c5_topk_long_rows_vs_oracle(pkg, oracle, torch_cuda):
-    """Rows of >= 32,768 entries take the rescorer's long-row prepass (every 512-entry chunk scored in
-    parallel for its largest score; the row's wave skips the chunks that cannot enter its full heap).
-    Two hubs: item 0 with 45,000 partners of near-equal counts (ties everywhere: a chunk whose maximum
-    equals the heap's least must be skipped exactly like the sequential loop skips its entries), and
-    item 1 whose partners' counts grow with the column (every later chunk beats the heap).  Both heaps,
-    and short rows, against the oracle's rescorer (ItemRowRescorer...java:195-241), through the whole-
-    batch launch and the sampled-rows launch."""
+    """Rows of tens of thousands of entries (88 chunks of 512 for one wave).  Two hubs: item 0 with
+    45,000 partners of near-equal counts (ties everywhere: an entry equal to the heap's least must not
+    enter, as in the sequential loop), and item 1 whose partners' counts grow with the column (later
+    entries keep replacing the heap's least).  Both heaps, and short rows, against the oracle's
+    rescorer (ItemRowRescorer...java:195-241), through the whole-batch launch and the sampled-rows
+    launch."""
     torch = torch_cuda
     from tests._helpers import assert_row_topk, oracle_row_topk
 
