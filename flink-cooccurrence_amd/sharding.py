@@ -205,6 +205,18 @@ class OwnedResult:
     gathered_bytes: int     # history bytes this rank received
 
 
+def _gather_parts(out, part, sizes, group=None):
+    """out = the ranks' parts concatenated in rank order (sizes[r] elements from rank r): an uneven
+    all_to_all_single whose input is this rank's part repeated once per destination."""
+    world = len(sizes)
+    if world == 1:
+        out.copy_(part)
+        return
+    n = int(part.numel())
+    dist.all_to_all_single(out, part.repeat(world) if n else part, output_split_sizes=list(sizes),
+                           input_split_sizes=[n] * world, group=group)
+
+
 def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     """One window over this rank's users; histories all-gathered, owned rows counted here."""
     world = dist.get_world_size(group)
@@ -216,8 +228,10 @@ def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     counts = core.item_counts(items, stream=stream)  # (torch.bincount: global atomics on Zipf-hot bins)
     dist.all_reduce(counts, group=group)
     owner = snake_owner(counts, world)
-    # all-gather the histories straight into one compact CSR: every rank's lengths and items are
-    # broadcast from it into their exact place (uneven parts: no padding, no compacting copy)
+    # all-gather the histories straight into one compact CSR: one uneven all-to-all per array, every
+    # rank sending its whole part to every rank, so that the parts land at their exact places (no
+    # padding, no compacting copy) and all the transfers of a collective run at once -- on xGMI's
+    # point-to-point links every peer pair moves its part over its own link
     sizes = torch.tensor([n_users, n], dtype=torch.int64, device=dev)
     all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(all_sizes, sizes, group=group)
@@ -227,17 +241,8 @@ def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
     up_all = torch.zeros(n_users_all + 1, dtype=torch.int64, device=dev)
     it_all = torch.empty(max(n_all, 1), dtype=torch.int32, device=dev)
     lens_all = up_all[1:]
-    uo = io = 0
-    for r in range(world):
-        ru, rn = sz[r]
-        if r == rank:
-            torch.sub(user_ptr[1:], user_ptr[:-1], out=lens_all[uo:uo + ru])
-            it_all[io:io + rn] = items
-        if ru:
-            dist.broadcast(lens_all[uo:uo + ru], src=dist.get_global_rank(group, r) if group else r, group=group)
-        if rn:
-            dist.broadcast(it_all[io:io + rn], src=dist.get_global_rank(group, r) if group else r, group=group)
-        uo, io = uo + ru, io + rn
+    _gather_parts(lens_all, torch.sub(user_ptr[1:], user_ptr[:-1]), [s_[0] for s_ in sz], group)
+    _gather_parts(it_all[:n_all], items, [s_[1] for s_ in sz], group)
     lens_all.cumsum_(0)  # lengths -> offsets, in place (up_all[0] == 0)
     res = core.count_device_owned(up_all, it_all, owner, rank, counts, n_all, stream)
     obs = torch.tensor([res.observed], dtype=torch.int64, device=dev)
