@@ -240,38 +240,85 @@ __device__ inline int32_t sp_split_shares(int64_t W, float g0) {
 constexpr uint32_t kSink = 0xFFFFFFFFu;
 constexpr uint32_t kSink16 = 0xFFFFu;  // (arena0 pads; never a tile-0 id)
 
-// One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the
-// item sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152), and counts the list by tile:
-// tb relative to the user's bases, plen0[u] = its tile-0 ids rounded up to 8 (16 B of u16), plen1[u] =
-// its other ids rounded up to 4 (the bases are their prefixes; k_sp_scatter fills the arenas and makes
-// tb absolute).
-__global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *__restrict__ up,
-                                                      const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                      int64_t *__restrict__ plen0, int64_t *__restrict__ plen1,
-                                                      int32_t *__restrict__ tb,
-                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                                                      const int32_t *__restrict__ owner, int32_t part,
-                                                      int32_t *__restrict__ ownc, PlanTotals *__restrict__ tot) {
+// The arenas' user regions, packed and dense: one wave per user counts its tile-0 ids (ballots) and
+// writes len[j] = round8(tile-0 ids) << 32 | round4(other ids); their inclusive prefix (one scan) gives
+// every user's base in arena0 (high half) and arena1 (low half).
+__global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t *__restrict__ up,
+                                                        const int32_t *__restrict__ items, int32_t M,
+                                                        uint64_t *__restrict__ len) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up[j];
+    const int32_t n = int32_t(up[j + 1] - s);
+    int32_t n0 = 0;
+    for (int32_t p0 = 0; p0 < n; p0 += 4 * 64) {
+      int32_t it[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) it[k] = p0 + 64 * k + lane < n ? items[s + p0 + 64 * k + lane] : -1;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {  // (an invalid id goes to tile 0 in k_sp_tile_lists, which reports it)
+        const bool in = p0 + 64 * k + lane < n;
+        n0 += int32_t(__popcll(__ballot(in && (uint32_t(it[k]) < uint32_t(kTW) || uint32_t(it[k]) >= uint32_t(M)))));
+      }
+    }
+    if (lane == 0) len[j] = (uint64_t((n0 + 7) & ~7) << 32) | uint64_t((n - n0 + 3) & ~3);
+  }
+}
+
+// One wave per user: validates the ids, emits the contributions (item, user) in CSR order for the item
+// sort (the keyBy(itemA) regrouping, FlinkCooccurrences.java:152; owner != NULL: only counts the owned
+// ones), counts the list by tile in LDS and writes the arenas: the user's tile-0 ids as u16 at its
+// arena0 base (kSink16 pads to a multiple of 8), its other ids tile by tile as u32 at its arena1 base
+// (kSink pads to a multiple of 4), bases from k_sp_tile_counts' prefix.  tb[j] gets the absolute
+// offsets: [0] = base0, [t] = base1 + the ids of tiles 1..t-1, [T + 1] = base0 + the tile-0 ids.
+constexpr int kTlR = 4;  // ids per lane held in registers across both passes (users of <= 256 ids)
+
+__global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t *__restrict__ up,
+                                                       const int32_t *__restrict__ items, int32_t M, int32_t T,
+                                                       int32_t *__restrict__ tb, uint16_t *__restrict__ arena0,
+                                                       uint32_t *__restrict__ arena1, const uint64_t *__restrict__ pbase,
+                                                       uint32_t *__restrict__ keys,
+                                                       uint32_t *__restrict__ vals, const int32_t *__restrict__ owner,
+                                                       int32_t part, int32_t *__restrict__ ownc,
+                                                       PlanTotals *__restrict__ tot) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int32_t *c = cur[wave];
   const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   bool bad = false;
+  int64_t s = 0, e = 0;
+  if (gw < U) {
+    s = up[gw];
+    e = up[gw + 1];
+  }
   for (int64_t j = gw; j < U; j += n_waves) {
-    const int64_t s = up[j];
-    const int32_t n = int32_t(up[j + 1] - s);
+    const int32_t n = int32_t(e - s);
+    // the next user's bounds and this user's first kTlR * 64 ids: all loads in flight together
+    int64_t sn = 0, en = 0;
+    if (j + n_waves < U) {
+      sn = up[j + n_waves];
+      en = up[j + n_waves + 1];
+    }
+    int32_t r[kTlR];
+#pragma unroll
+    for (int k = 0; k < kTlR; k++) {
+      const int32_t p = lane + 64 * k;
+      r[k] = p < n ? items[s + p] : 0;
+      if (uint32_t(r[k]) >= uint32_t(M)) {
+        bad = true;
+        r[k] = 0;
+      }
+    }
     for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    int32_t mine = 0;
-    for (int32_t p = lane; p < n; p += 64) {
-      int32_t it = items[s + p];
-      if (uint32_t(it) >= uint32_t(M)) {
-        bad = true;
-        it = 0;
-      }
-      atomicAdd(&c[it >> kTShift], 1);
+    int32_t mine = 0, n0 = 0;  // (tile-0 ids, the Zipf head, counted by ballot: no same-address LDS atomics)
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    auto count = [&](int32_t p, int32_t it) {
+      if (it >> kTShift) atomicAdd(&c[it >> kTShift], 1);
       if (!owner) {
         if (keys) {  // (NULL: the contributions come from elsewhere, k_sp_window_contribs)
           keys[s + p] = uint32_t(it);
@@ -280,6 +327,25 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
       } else {
         mine += owner[it] == part;
       }
+    };
+#pragma unroll
+    for (int k = 0; k < kTlR; k++) {
+      const bool in = lane + 64 * k < n;
+      n0 += __popcll(__ballot(in && (r[k] >> kTShift) == 0));
+      if (in) count(lane + 64 * k, r[k]);
+    }
+    for (int32_t p0 = 64 * kTlR; p0 < n; p0 += 64) {
+      const int32_t p = p0 + lane;
+      int32_t it = 0;
+      if (p < n) {
+        it = items[s + p];
+        if (uint32_t(it) >= uint32_t(M)) {
+          bad = true;
+          it = 0;
+        }
+      }
+      n0 += __popcll(__ballot(p < n && (it >> kTShift) == 0));
+      if (p < n) count(p, it);
     }
     if (owner) {
       for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
@@ -288,84 +354,67 @@ __global__ __launch_bounds__(256) void k_sp_partition(int64_t U, const int64_t *
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     int32_t *tbj = tb + j * (T + 2);
-    const int32_t n0 = c[0];
-    if (T < 64) {  // exclusive prefix of tiles 1..T's counts: one wave scan (lane t = tile t)
-      const uint32_t x = (lane >= 1 && lane <= T) ? uint32_t(c[lane]) : 0u;
-      const uint32_t inc = wave_incl_scan(x);
-      if (lane >= 1 && lane <= T) tbj[lane] = int32_t(inc - x);  // (tile T is empty: tbj[T] = n - n0)
-    } else {
-      if (lane == 0) {
-        int32_t run = 0;
-        for (int32_t t = 1; t <= T; t++) {
-          const int32_t x = c[t];
-          tbj[t] = run;
-          run += x;
-        }
+    const int32_t n1 = n - n0;
+    const uint64_t pb = pbase[j];
+    const int64_t b0 = int64_t(pb >> 32), b1 = int64_t(pb & 0xFFFFFFFFull);
+    // exclusive prefix of tiles 1..T's counts: tb and the tiles' cursors
+    if (T < 64) {  // one wave scan, lane t = tile t
+      const int32_t x = (lane >= 1 && lane <= T) ? c[lane] : 0;
+      const int32_t ex = int32_t(wave_incl_scan(uint32_t(x))) - x;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane >= 1 && lane <= T) {
+        tbj[lane] = int32_t(b1 + ex);  // (tile T is empty: tbj[T] = base1 + n1)
+        c[lane] = ex;
+      }
+    } else if (lane == 0) {
+      int32_t run = 0;
+      for (int32_t t = 1; t <= T; t++) {
+        const int32_t x = c[t];
+        tbj[t] = int32_t(b1 + run);
+        c[t] = run;
+        run += x;
       }
     }
     if (lane == 0) {
-      tbj[0] = 0;
-      tbj[T + 1] = n0;
-      plen0[j] = (n0 + 7) & ~7;
-      plen1[j] = (n - n0 + 3) & ~3;
+      tbj[0] = int32_t(b0);
+      tbj[T + 1] = int32_t(b0 + n0);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    uint16_t *o0 = arena0 + b0;
+    uint32_t *o1 = arena1 + b1;
+    int32_t q0 = 0;  // the tile-0 cursor (wave-uniform): ballot ranks, in lane order
+    auto place = [&](bool in, int32_t it) {
+      const bool t0 = in && (it >> kTShift) == 0;
+      const uint64_t b = __ballot(t0);
+      if (t0) o0[q0 + int32_t(__popcll(b & lt))] = uint16_t(it);
+      else if (in) o1[atomicAdd(&c[it >> kTShift], 1)] = uint32_t(it);
+      q0 += int32_t(__popcll(b));
+    };
+#pragma unroll
+    for (int k = 0; k < kTlR; k++) place(lane + 64 * k < n, r[k]);
+    for (int32_t p0 = 64 * kTlR; p0 < n; p0 += 64) {  // (long lists: L1 / L2 lines of the first pass)
+      const int32_t p = p0 + lane;
+      int32_t it = p < n ? items[s + p] : 0;
+      if (uint32_t(it) >= uint32_t(M)) it = 0;
+      place(p < n, it);
+    }
+    if (lane < ((n0 + 7) & ~7) - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
+    if (lane < ((n1 + 3) & ~3) - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    s = sn;
+    e = en;
   }
   if (bad) atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 1ull);
 }
 
-// The arenas: user j's tile-0 ids at pbase0[j] of arena0 (u16; a multiple of 8; kSink16 pads after
-// them), its other ids tile by tile at pbase1[j] of arena1 (u32; a multiple of 4; kSink pads).  One wave
-// per user, tile cursors in LDS.  Leaves tb absolute, so that a walk needs one descriptor line per user.
 // A contribution's value: the index of the list its row walks; in a streaming window (spre != NULL) with
 // kSelfBit when the walk includes the contribution's own position (a new position walks its user's whole
 // history, an old one only the window's new items, see k_sp_window_contribs).  In a one-window batch every
 // walk includes it (no bit: the self count of a row is its contribution count).
 constexpr uint32_t kSelfBit = 0x80000000u, kListMask = 0x7FFFFFFFu;
-__global__ __launch_bounds__(256) void k_sp_scatter(int64_t U, const int64_t *__restrict__ up,
-                                                    const int32_t *__restrict__ items, int32_t M, int32_t T,
-                                                    const int64_t *__restrict__ pbase0,
-                                                    const int64_t *__restrict__ pbase1, int32_t *__restrict__ tb,
-                                                    uint16_t *__restrict__ arena0, uint32_t *__restrict__ arena1) {
-  __shared__ int32_t cur[4][kSpMaxTiles + 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t *c = cur[wave];
-  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t j = gw; j < U; j += n_waves) {
-    const int64_t s = up[j];
-    const int32_t n = int32_t(up[j + 1] - s);
-    int32_t *tbj = tb + j * (T + 2);
-    uint16_t *o0 = arena0 + pbase0[j];
-    uint32_t *o1 = arena1 + pbase1[j];
-    for (int32_t t = lane; t < T; t += 64) c[t] = tbj[t];  // (c[0] = 0: the arena0 cursor)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int32_t p = lane; p < n; p += 64) {
-      int32_t it = items[s + p];
-      if (uint32_t(it) >= uint32_t(M)) it = 0;  // (reported by k_sp_partition)
-      const int32_t t = it >> kTShift;
-      const int32_t q = atomicAdd(&c[t], 1);
-      if (t == 0) o0[q] = uint16_t(it); else o1[q] = uint32_t(it);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int32_t n0 = tbj[T + 1], n1 = tbj[T];
-    const int32_t p0 = int32_t(pbase0[j + 1] - pbase0[j]), p1 = int32_t(pbase1[j + 1] - pbase1[j]);
-    if (lane < p0 - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
-    if (lane < p1 - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      tbj[0] = int32_t(pbase0[j]);
-      tbj[T + 1] = int32_t(pbase0[j] + n0);
-    }
-    for (int32_t t = 1 + lane; t <= T; t += 64) tbj[t] = int32_t(pbase1[j] + tbj[t]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
 
 // Owner-filtered contributions (multi-GPU: this part's rows only): user j's owned interactions at
 // ownoff[j] (exclusive prefix of the per-user counts), in list order.  One wave per user.
@@ -382,16 +431,25 @@ __global__ __launch_bounds__(256) void k_sp_owned_contribs(int64_t U, const int6
     const int64_t s = up[j];
     const int32_t n = int32_t(up[j + 1] - s);
     int64_t o = ownoff[j];
-    for (int32_t p0 = 0; p0 < n; p0 += 64) {
-      const int32_t p = p0 + lane;
-      int32_t it = p < n ? items[s + p] : -1;
-      const bool m = p < n && uint32_t(it) < uint32_t(M) && owner[it] == part;
-      const uint64_t bal = __ballot(m);
-      if (m) {
-        keys[o + __popcll(bal & lt)] = uint32_t(it);
-        vals[o + __popcll(bal & lt)] = uint32_t(j);
+    for (int32_t p0 = 0; p0 < n; p0 += 4 * 64) {  // 4 steps' id and owner loads in flight together
+      int32_t it[4];
+      bool m[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t p = p0 + 64 * k + lane;
+        it[k] = p < n ? items[s + p] : -1;
       }
-      o += __popcll(bal);
+#pragma unroll
+      for (int k = 0; k < 4; k++) m[k] = uint32_t(it[k]) < uint32_t(M) && owner[it[k]] == part;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint64_t bal = __ballot(m[k]);
+        if (m[k]) {
+          keys[o + __popcll(bal & lt)] = uint32_t(it[k]);
+          vals[o + __popcll(bal & lt)] = uint32_t(j);
+        }
+        o += __popcll(bal);
+      }
     }
   }
 }
@@ -1900,11 +1958,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(vals_in_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(keys_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
   COOC_TRY(vals_out_.reserve(sizeof(uint32_t) * (n1 + 1)));
-  COOC_TRY(sp_arena_.reserve(sizeof(uint32_t) * size_t(n1 + 3 * U1 + 16)));   // arena1: lists padded to 4 ids
-  COOC_TRY(sp_arena0_.reserve(sizeof(uint16_t) * size_t(n1 + 7 * U1 + 16)));  // arena0: tile-0 ids padded to 8
-  COOC_TRY(sp_pbase_.reserve(sizeof(int64_t) * size_t(4 * U1 + 4)));    // plen0, pbase0, plen1, pbase1
+  const int64_t n_groups0 = (n1 + 7 * U1) / 8 + 4, n_groups1 = (n1 + 3 * U1) / 4 + 4;
+  COOC_TRY(sp_arena_.reserve(sizeof(uint4) * size_t(n_groups1)));   // arena1: lists padded to 4 ids
+  COOC_TRY(sp_arena0_.reserve(sizeof(uint4) * size_t(n_groups0)));  // arena0: tile-0 ids padded to 8
+  COOC_TRY(sp_pbase_.reserve(sizeof(uint64_t) * size_t(2 * U1 + 1)));  // packed region lengths, their prefix
   COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 2)));
-  if (n1 + 7 * U1 + 16 > int64_t(INT32_MAX)) return Status{1, "more than 2^31 arena positions in one window"};
+  if (8 * n_groups0 > int64_t(INT32_MAX)) return Status{1, "more than 2^31 arena positions in one window"};
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
   COOC_TRY(row_ptr_.reserve(sizeof(int64_t) * (M + 1)));
   COOC_TRY(rowsum_.reserve(sizeof(int64_t) * M));
@@ -1943,8 +2002,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   tmp = std::max(tmp, q);
   COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, q, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), M, s));
   tmp = std::max(tmp, q);
-  int64_t *plen = sp_pbase_.as<int64_t>(), *pbase = plen + U1;  // (tile-0 part; the rest after it)
-  int64_t *plen1 = pbase + U1 + 1, *pbase1 = plen1 + U1;
+  uint64_t *plen = sp_pbase_.as<uint64_t>(), *pbase = plen + U1;
   COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, pbase + 1, int(U1), s));
   tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
@@ -1955,21 +2013,15 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
     COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
   }
+  COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(uint64_t), s));
   if (U > 0) {
-    k_sp_partition<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, plen, plen1, sp_tb_.as<int32_t>(),
-                                                           win ? nullptr : keys_in, vals_in, owner, part,
-                                                           sp_ownc_.as<int32_t>(), tot);
-    COOC_HIP_TRY(hipGetLastError());
-  }
-  COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipMemsetAsync(pbase1, 0, sizeof(int64_t), s));
-  if (U > 0) {
+    k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen);
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen1, pbase1 + 1, int(U), s));
-    k_sp_scatter<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, pbase, pbase1, sp_tb_.as<int32_t>(),
-                                                         sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>());
+    k_sp_tile_lists<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_tb_.as<int32_t>(),
+                                                            sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), pbase,
+                                                            win ? nullptr : keys_in, vals_in, owner, part,
+                                                            sp_ownc_.as<int32_t>(), tot);
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
@@ -2135,8 +2187,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.T = T;
   proto.n_contrib = n_c;
   proto.n_users = U;
-  proto.n_groups = (n1 + 3 * U1) / 4 + 4;
-  proto.n_groups0 = (n1 + 7 * U1) / 8 + 4;
+  proto.n_groups = n_groups1;
+  proto.n_groups0 = n_groups0;
   proto.scratch = scr_cap ? sp_scr_.as<uint4>() : nullptr;
   proto.scr_cap = (scr_cap && n_gather) ? scr_cap : 0;
   proto.rowsum = rowsum_.as<int64_t>();
