@@ -245,14 +245,15 @@ constexpr uint32_t kSink16 = 0xFFFFu;  // (arena0 pads; never a tile-0 id)
 // every user's base in arena0 (high half) and arena1 (low half).
 __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t *__restrict__ up,
                                                         const int32_t *__restrict__ items, int32_t M,
-                                                        uint64_t *__restrict__ len) {
+                                                        uint64_t *__restrict__ len, const int32_t *__restrict__ owner,
+                                                        int32_t part, int32_t *__restrict__ ownc) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   for (int64_t j = gw; j < U; j += n_waves) {
     const int64_t s = up[j];
     const int32_t n = int32_t(up[j + 1] - s);
-    int32_t n0 = 0;
+    int32_t n0 = 0, mine = 0;
     for (int32_t p0 = 0; p0 < n; p0 += 4 * 64) {
       int32_t it[4];
 #pragma unroll
@@ -261,9 +262,13 @@ __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t
       for (int k = 0; k < 4; k++) {  // (an invalid id goes to tile 0 in k_sp_tile_lists, which reports it)
         const bool in = p0 + 64 * k + lane < n;
         n0 += int32_t(__popcll(__ballot(in && (uint32_t(it[k]) < uint32_t(kTW) || uint32_t(it[k]) >= uint32_t(M)))));
+        if (owner) mine += int32_t(__popcll(__ballot(uint32_t(it[k]) < uint32_t(M) && owner[it[k]] == part)));
       }
     }
-    if (lane == 0) len[j] = (uint64_t((n0 + 7) & ~7) << 32) | uint64_t((n - n0 + 3) & ~3);
+    if (lane == 0) {
+      len[j] = (uint64_t((n0 + 7) & ~7) << 32) | uint64_t((n - n0 + 3) & ~3);
+      if (owner) ownc[j] = mine;
+    }
   }
 }
 
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
                                                        uint32_t *__restrict__ arena1, const uint64_t *__restrict__ pbase,
                                                        uint32_t *__restrict__ keys,
                                                        uint32_t *__restrict__ vals, const int32_t *__restrict__ owner,
-                                                       int32_t part, int32_t *__restrict__ ownc,
+                                                       int32_t part, const int64_t *__restrict__ ownoff,
                                                        PlanTotals *__restrict__ tot) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -307,49 +312,49 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
     for (int k = 0; k < kTlR; k++) {
       const int32_t p = lane + 64 * k;
       r[k] = p < n ? items[s + p] : 0;
-      if (uint32_t(r[k]) >= uint32_t(M)) {
-        bad = true;
-        r[k] = 0;
-      }
+      if (uint32_t(r[k]) >= uint32_t(M)) bad = true;
     }
     for (int32_t t = lane; t <= T; t += 64) c[t] = 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    int32_t mine = 0, n0 = 0;  // (tile-0 ids, the Zipf head, counted by ballot: no same-address LDS atomics)
+    int32_t n0 = 0;  // (tile-0 ids, the Zipf head, counted by ballot: no same-address LDS atomics)
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    auto count = [&](int32_t p, int32_t it) {
-      if (it >> kTShift) atomicAdd(&c[it >> kTShift], 1);
+    int64_t o = owner ? ownoff[j] : 0;  // (owned contributions: at ownoff[j], in list order)
+    auto count = [&](bool in, int32_t p, int32_t it, bool valid) {
+      n0 += __popcll(__ballot(in && (it >> kTShift) == 0));
+      if (in && (it >> kTShift)) atomicAdd(&c[it >> kTShift], 1);
       if (!owner) {
-        if (keys) {  // (NULL: the contributions come from elsewhere, k_sp_window_contribs)
+        if (keys && in) {  // (NULL: the contributions come from elsewhere, k_sp_window_contribs)
           keys[s + p] = uint32_t(it);
           vals[s + p] = uint32_t(j);
         }
       } else {
-        mine += owner[it] == part;
+        const bool m = in && valid && owner[it] == part;
+        const uint64_t bal = __ballot(m);
+        if (m && keys) {
+          keys[o + __popcll(bal & lt)] = uint32_t(it);
+          vals[o + __popcll(bal & lt)] = uint32_t(j);
+        }
+        o += __popcll(bal);
       }
     };
+    bool valid[kTlR];
 #pragma unroll
     for (int k = 0; k < kTlR; k++) {
-      const bool in = lane + 64 * k < n;
-      n0 += __popcll(__ballot(in && (r[k] >> kTShift) == 0));
-      if (in) count(lane + 64 * k, r[k]);
+      valid[k] = uint32_t(r[k]) < uint32_t(M);
+      if (!valid[k]) r[k] = 0;
     }
+#pragma unroll
+    for (int k = 0; k < kTlR; k++) count(lane + 64 * k < n, lane + 64 * k, r[k], valid[k]);
     for (int32_t p0 = 64 * kTlR; p0 < n; p0 += 64) {
       const int32_t p = p0 + lane;
-      int32_t it = 0;
-      if (p < n) {
-        it = items[s + p];
-        if (uint32_t(it) >= uint32_t(M)) {
-          bad = true;
-          it = 0;
-        }
+      int32_t it = p < n ? items[s + p] : 0;
+      const bool v = uint32_t(it) < uint32_t(M);
+      if (!v) {
+        bad = true;
+        it = 0;
       }
-      n0 += __popcll(__ballot(p < n && (it >> kTShift) == 0));
-      if (p < n) count(p, it);
-    }
-    if (owner) {
-      for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-      if (lane == 0) ownc[j] = mine;
+      count(p < n, p, it, v);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -415,44 +420,6 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
 // history, an old one only the window's new items, see k_sp_window_contribs).  In a one-window batch every
 // walk includes it (no bit: the self count of a row is its contribution count).
 constexpr uint32_t kSelfBit = 0x80000000u, kListMask = 0x7FFFFFFFu;
-
-// Owner-filtered contributions (multi-GPU: this part's rows only): user j's owned interactions at
-// ownoff[j] (exclusive prefix of the per-user counts), in list order.  One wave per user.
-__global__ __launch_bounds__(256) void k_sp_owned_contribs(int64_t U, const int64_t *__restrict__ up,
-                                                           const int32_t *__restrict__ items, int32_t M,
-                                                           const int32_t *__restrict__ owner, int32_t part,
-                                                           const int64_t *__restrict__ ownoff,
-                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int64_t j = gw; j < U; j += n_waves) {
-    const int64_t s = up[j];
-    const int32_t n = int32_t(up[j + 1] - s);
-    int64_t o = ownoff[j];
-    for (int32_t p0 = 0; p0 < n; p0 += 4 * 64) {  // 4 steps' id and owner loads in flight together
-      int32_t it[4];
-      bool m[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int32_t p = p0 + 64 * k + lane;
-        it[k] = p < n ? items[s + p] : -1;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) m[k] = uint32_t(it[k]) < uint32_t(M) && owner[it[k]] == part;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint64_t bal = __ballot(m[k]);
-        if (m[k]) {
-          keys[o + __popcll(bal & lt)] = uint32_t(it[k]);
-          vals[o + __popcll(bal & lt)] = uint32_t(j);
-        }
-        o += __popcll(bal);
-      }
-    }
-  }
-}
 
 // Streaming window (old / new positions, NonSampled...java:129-161): user j's two lists are A_j (the whole
 // history after the window, at up2[2j]) and B_j (its new items, positions >= old[j], at up2[2j + 1]).
@@ -2015,13 +1982,27 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   }
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(uint64_t), s));
   if (U > 0) {
-    k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen);
+    k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen, owner, part,
+                                                             sp_ownc_.as<int32_t>());
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
+  }
+  int64_t *ownoff = owner ? sp_ownoff_.as<int64_t>() : nullptr;
+  if (owner) {  // owned contributions per user -> their offsets
+    COOC_HIP_TRY(hipMemsetAsync(ownoff, 0, sizeof(int64_t), s));
+    if (U > 0) {
+      hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> oc(sp_ownc_.as<int32_t>(), WidenCount{});
+      size_t b = 0;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, oc, ownoff + 1, int(U), s));
+      COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
+      b = sort_tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, oc, ownoff + 1, int(U), s));
+    }
+  }
+  if (U > 0) {
     k_sp_tile_lists<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_tb_.as<int32_t>(),
                                                             sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), pbase,
-                                                            win ? nullptr : keys_in, vals_in, owner, part,
-                                                            sp_ownc_.as<int32_t>(), tot);
+                                                            win ? nullptr : keys_in, vals_in, owner, part, ownoff, tot);
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
@@ -2033,19 +2014,6 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipGetLastError());
   }
   if (owner) {
-    int64_t *ownoff = sp_ownoff_.as<int64_t>();
-    COOC_HIP_TRY(hipMemsetAsync(ownoff, 0, sizeof(int64_t), s));
-    if (U > 0) {
-      hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> oc(sp_ownc_.as<int32_t>(), WidenCount{});
-      size_t b = 0;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, oc, ownoff + 1, int(U), s));
-      COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
-      b = sort_tmp_.cap;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, oc, ownoff + 1, int(U), s));
-      k_sp_owned_contribs<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, owner, part, ownoff, keys_in,
-                                                                  vals_in);
-      COOC_HIP_TRY(hipGetLastError());
-    }
     COOC_HIP_TRY(hipMemcpyAsync(&n_c, ownoff + U, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     COOC_HIP_TRY(hipStreamSynchronize(s));
   }
