@@ -1,7 +1,7 @@
 """The multi-GPU orchestration (sharding.py) with the REAL device core: world_size 2, one process per
 rank, both ranks on the box's one MI355X, torch.distributed over gloo (RCCL refuses two ranks on one
 GPU; the gloo backend moves the same CUDA tensors through host memory).  Every collective the driver's
-N-GPU bench issues -- the item-frequency all-reduce, the history broadcasts of count_owned, the row-sum
+N-GPU bench issues -- the item-frequency all-reduce, the history all-to-alls of count_owned, the row-sum
 all-reduce of topk_owned, the all-to-alls of count_records -- runs here between real library kernels
 on torch's current stream, in the order the bench issues them.
 

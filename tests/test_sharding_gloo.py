@@ -307,3 +307,42 @@ def test_balanced_user_ranges(pkg):
         assert u0 == rng[-1][0] and sup[0] == 0 and len(sit) == sup[-1] == up[rng[-1][1]] - up[rng[-1][0]]
     t = torch.from_numpy(up)
     assert sharding.balanced_user_ranges(t, 4) == sharding.balanced_user_ranges(up, 4)
+
+
+def _gather_worker(rank, world, port, sizes, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
+
+    __graft_entry__.load_package()
+    from flink_cooccurrence_amd import sharding
+
+    part = torch.arange(sizes[rank], dtype=torch.int32) + 1000 * rank
+    out = torch.full((sum(sizes),), -1, dtype=torch.int32)
+    sharding._gather_parts(out, part, sizes)
+    out_q.put((rank, out.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [[5, 0, 7], [0, 3], [4, 4, 4, 0]])
+def test_gather_parts_uneven_gloo(pkg, sizes):
+    """count_owned's history all-gather (one uneven all_to_all_single per array): the ranks' parts land
+    compact and in rank order on every rank, empty parts included."""
+    world = len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [v for r in range(world) for v in range(1000 * r, 1000 * r + sizes[r])]
+    for r in range(world):
+        assert outs[r] == want
