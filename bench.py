@@ -136,6 +136,8 @@ def main():
     ap.add_argument("--config", choices=["c3", "c5", "c2"], default="c3")
     ap.add_argument("--topk", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--permute-items", action="store_true",
+                    help="C3/C5: item ids through the fixed bijection datagen.c3_item_perm (ids not in popularity order)")
     args = ap.parse_args()
 
     import torch
@@ -160,7 +162,7 @@ def main():
         # the job's users [0, N U/8): contiguous ranges balanced on sum n_u (n_u - 1)
         lens_all = datagen.c3_lengths(0, world * U8)
         u0, u1 = sharding.balanced_user_ranges(np.concatenate([[0], np.cumsum(lens_all)]), world)[rank]
-        up, it = datagen.c3_users(u0, u1, device=dev)
+        up, it = datagen.c3_users(u0, u1, device=dev, permute=args.permute_items)
         M = datagen.C3_ITEMS
         P_local = int(np.sum(lens_all[u0:u1] * (lens_all[u0:u1] - 1)))
         kernel = "k_sp_main"
@@ -169,6 +171,9 @@ def main():
                     f"datagen.c3_users seed {datagen.C3_SEED}: users [r*1.25e6, (r+1)*1.25e6) on rank r "
                     f"(1/8 of 1e7 users per GPU; the whole 1e9-interaction log at 8 GPUs), 1e6 items, Zipf(1.0) "
                     "with replacement, lognormal lengths of mean 100, one window")
+        if args.permute_items:
+            workload += (f"; item ids permuted by the fixed bijection datagen.c3_item_perm (PCG64 seed "
+                         f"{datagen.C3_PERM_SEED:#x}): ids carry no popularity order")
         if args.config == "c5":
             workload = (f"C5 (BASELINE configs[4]): co-occurrence counts + LLR scoring of every entry + per-item "
                         f"top-{args.topk} (ItemRowRescorer...java:195-241) on " + workload[:1].lower() + workload[1:])
@@ -328,7 +333,7 @@ def main():
         out["topk_ms"] = float(np.median(topk_ms))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if large:
-            bu, bi = datagen.c3_users(0, 200_000)
+            bu, bi = datagen.c3_users(0, 200_000, permute=args.permute_items)
             out["cpu_baseline"] = cpu_baseline(bu, bi, M, "the same C3 log")
         else:
             out["cpu_baseline"] = cpu_baseline(d["user_ptr"], d["items"], M, "the same C2 log")

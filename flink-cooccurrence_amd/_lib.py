@@ -74,6 +74,32 @@ class CoocDeviceResult(ctypes.Structure):
     ]
 
 
+class CoocOwnedInfo(ctypes.Structure):
+    _fields_ = [
+        ("part", ctypes.c_int32),
+        ("n_parts", ctypes.c_int32),
+        ("observed", ctypes.c_int64),
+        ("local_observed", ctypes.c_int64),
+        ("n_users_all", ctypes.c_int64),
+        ("n_interactions_all", ctypes.c_int64),
+        ("gathered_bytes", ctypes.c_int64),
+        ("owner", vp),
+        ("item_counts", vp),
+    ]
+
+
+# cooc_comm_ops: caller collectives (include/cooc.h)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, vp, ctypes.c_int64, vp)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, vp, vp, ctypes.c_int64, vp)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, vp, i64p, i64p, vp, i64p, i64p, vp)
+
+
+class CoocCommOps(ctypes.Structure):
+    _fields_ = [("allreduce_sum_i64", ALLREDUCE_FN), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
+
+
+COOC_COMM_ID_BYTES = 128
+
 _SIGS = {
     "cooc_abi_version": (ctypes.c_int, []),
     "cooc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
@@ -112,6 +138,13 @@ _SIGS = {
     "cooc_copy_rowsum_device": (ctypes.c_int, [vp, vp, vp]),
     "cooc_merge_partitions": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
                                              ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_comm_unique_id": (ctypes.c_int, [vp]),
+    "cooc_comm_init": (ctypes.c_int, [vp, vp, ctypes.c_int32, ctypes.c_int32]),
+    "cooc_comm_init_ops": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(CoocCommOps), vp]),
+    "cooc_count_owned": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.POINTER(CoocOwnedInfo),
+                                        ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_topk_owned": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "cooc_snake_owner": (ctypes.c_int, [i64p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p]),
     "cooc_shard_plan": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp,
                                        ctypes.c_int64, vp, i64p, i64p]),
     "cooc_shard_count": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int64, vp,

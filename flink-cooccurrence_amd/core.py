@@ -24,7 +24,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import (CoocConfig, CoocDeviceResult, CoocWindowInfo, check, f64p, i16p, i32p, i64p, u32p)
+from ._lib import (CoocCommOps, CoocConfig, CoocDeviceResult, CoocOwnedInfo, CoocWindowInfo, check, f64p, i16p, i32p,
+                   i64p, u32p)
 
 # Configuration.java:160-182 window units -> milliseconds (Time.of(size, unit).toMilliseconds())
 _UNIT_MS = {"MILLISECONDS": 1, "SECONDS": 1000, "MINUTES": 60_000, "HOURS": 3_600_000, "DAYS": 86_400_000}
@@ -51,18 +52,6 @@ def _stream_arg(stream, tensor):
 
     if getattr(tensor, "is_cuda", False):
         return ctypes.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)
-    return None
-
-
-def _current_stream():
-    """torch's current stream on the current device when torch has a GPU, else the null stream."""
-    try:
-        import torch
-
-        if torch.cuda.is_available():
-            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    except ImportError:
-        pass
     return None
 
 
@@ -128,6 +117,8 @@ class CooccurrenceCore:
         self._h = h
         self.n_items = n_items
         self.topk = topk
+        self.device = int(device) if devices is None else int(np.asarray(devices)[subtask % len(devices)])
+        self.comm_world = 0  # > 0 once comm_init / comm_init_ops joined a communicator
 
     def close(self):
         if getattr(self, "_h", None):
@@ -305,12 +296,75 @@ class CooccurrenceCore:
         out = np.zeros(8, np.int64)
         flags = _lib.COOC_VERIFY_SYMMETRY if symmetry else 0
         cs = ctypes.c_void_p(row_checksum.data_ptr()) if row_checksum is not None else None
-        check(_lib.load().cooc_verify_batch(self._h, flags, cs, _p(out, i64p),
-                                            _stream_arg(stream, row_checksum) if row_checksum is not None else
-                                            _current_stream()), self._h)
+        check(_lib.load().cooc_verify_batch(self._h, flags, cs, _p(out, i64p), self._stream(stream)), self._h)
         return {"sum_counts": int(out[0]), "sum_rowsums": int(out[1]), "entries": int(out[2]),
                 "rows_bad_sum": int(out[3]), "rows_bad_entries": int(out[4]),
                 "asymmetric_entries": None if out[5] < 0 else int(out[5])}
+
+    def _stream(self, stream):
+        """An explicit stream as given; else torch's current stream on this context's device (the null
+        stream without a GPU)."""
+        if stream is not None:
+            return ctypes.c_void_p(int(stream))
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                dev = self.device if self.device >= 0 else torch.cuda.current_device()
+                return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        except ImportError:
+            pass
+        return None
+
+    # ---- communicator: the RCCL sharding layer inside the library -------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """cooc_comm_unique_id: rank 0's communicator id (128 opaque bytes) for cooc_comm_init."""
+        buf = (ctypes.c_uint8 * _lib.COOC_COMM_ID_BYTES)()
+        check(_lib.load().cooc_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)), None)
+        return bytes(buf)
+
+    def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        """Join the RCCL communicator `unique_id` as `rank` of `world` (one context per GPU process)."""
+        buf = (ctypes.c_uint8 * _lib.COOC_COMM_ID_BYTES).from_buffer_copy(unique_id)
+        check(_lib.load().cooc_comm_init(self._h, ctypes.cast(buf, ctypes.c_void_p), int(rank), int(world)), self._h)
+        self.comm_world = int(world)
+
+    def comm_init_ops(self, rank: int, world: int, ops: CoocCommOps) -> None:
+        """The library's exchange over caller collectives (cooc_comm_ops); `ops` must stay alive as long
+        as the context (the context keeps a reference)."""
+        check(_lib.load().cooc_comm_init_ops(self._h, int(rank), int(world), ctypes.byref(ops), None), self._h)
+        self._comm_ops = ops
+        self.comm_world = int(world)
+
+    def count_owned(self, user_ptr, items, stream=None):
+        """cooc_count_owned: this rank's users -> the rows it owns over the whole job's users (item
+        counts all-reduced, owner map, histories all-gathered, owned rows counted, pairs all-reduced),
+        all inside the library.  Returns (CoocDeviceResult, CoocOwnedInfo)."""
+        res, info = CoocDeviceResult(), CoocOwnedInfo()
+        n_users = int(user_ptr.numel()) - 1
+        check(_lib.load().cooc_count_owned(self._h, n_users, ctypes.c_void_p(user_ptr.data_ptr()),
+                                           ctypes.c_void_p(items.data_ptr()) if items.numel() else None,
+                                           int(items.numel()), _stream_arg(stream, user_ptr), ctypes.byref(info),
+                                           ctypes.byref(res)), self._h)
+        return res, info
+
+    def topk_owned(self, topk: int, sizes, values, scores, rowsum_global=None, exact_scores: bool = False,
+                   stream=None) -> None:
+        """cooc_topk_owned: the owned rows' row sums all-reduced, then their LLR top-k into device tensors."""
+        check(_lib.load().cooc_topk_owned(
+            self._h, int(topk), _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0, ctypes.c_void_p(sizes.data_ptr()),
+            ctypes.c_void_p(values.data_ptr()), ctypes.c_void_p(scores.data_ptr()),
+            None if rowsum_global is None else ctypes.c_void_p(rowsum_global.data_ptr()), _stream_arg(stream, sizes)),
+            self._h)
+
+    @staticmethod
+    def snake_owner(counts, world: int, head: int = 4096) -> np.ndarray:
+        """cooc_snake_owner (host): the owner map cooc_count_owned builds, from host item counts."""
+        c = np.ascontiguousarray(counts, np.int64)
+        out = np.zeros(len(c), np.int32)
+        check(_lib.load().cooc_snake_owner(_p(c, i64p), len(c), int(world), int(head), _p(out, i32p)), None)
+        return out
 
     def set_kernel_timing(self, enable: bool = True) -> None:
         check(_lib.load().cooc_set_kernel_timing(self._h, 1 if enable else 0), self._h)

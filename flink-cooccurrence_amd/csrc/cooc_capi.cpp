@@ -379,6 +379,74 @@ int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part, const in
   });
 }
 
+int cooc_comm_unique_id(uint8_t *id) {
+  return guarded(nullptr, [&]() -> int {
+    if (!id) return COOC_ERR_ARG;
+    Status s = cooc::Comm::unique_id(id);
+    return s.ok() ? COOC_OK : fail(nullptr, s);
+  });
+}
+
+int cooc_comm_init(cooc_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !id) return COOC_ERR_ARG;
+    if (world < 1 || rank < 0 || rank >= world) return fail(ctx, COOC_ERR_ARG, "rank must lie in [0, world)");
+    if (ctx->comm) return fail(ctx, COOC_ERR_STATE, "the context already has a communicator");
+    auto c = std::make_unique<cooc::Comm>();
+    Status s = c->init_rccl(id, rank, world, ctx->device);
+    if (!s.ok()) return fail(ctx, s);
+    ctx->comm = std::move(c);
+    return COOC_OK;
+  });
+}
+
+int cooc_comm_init_ops(cooc_ctx *ctx, int32_t rank, int32_t world, const cooc_comm_ops *ops, void *user) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !ops) return COOC_ERR_ARG;
+    if (world < 1 || rank < 0 || rank >= world) return fail(ctx, COOC_ERR_ARG, "rank must lie in [0, world)");
+    if (ctx->comm) return fail(ctx, COOC_ERR_STATE, "the context already has a communicator");
+    auto c = std::make_unique<cooc::Comm>();
+    Status s = c->init_ops(rank, world, *ops, user);
+    if (!s.ok()) return fail(ctx, s);
+    ctx->comm = std::move(c);
+    return COOC_OK;
+  });
+}
+
+int cooc_count_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                     int64_t n_interactions, void *hip_stream, cooc_owned_info *info, cooc_device_result *out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !out || !info) return COOC_ERR_ARG;
+    if (n_users < 0 || n_interactions < 0 || (n_users > 0 && (!d_user_ptr || (n_interactions > 0 && !d_items))))
+      return fail(ctx, COOC_ERR_ARG, "bad CSR arguments");
+    Status s = ctx->count_owned(n_users, d_user_ptr, d_items, n_interactions, static_cast<hipStream_t>(hip_stream),
+                                info, out);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_topk_owned(cooc_ctx *ctx, int32_t topk, int32_t flags, int32_t *d_sizes, int32_t *d_values, double *d_scores,
+                    int64_t *d_rowsum_global, void *hip_stream) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    if (!d_sizes || !d_values || !d_scores) return fail(ctx, COOC_ERR_ARG, "bad topk output buffers");
+    Status s = ctx->topk_owned(topk, flags, d_sizes, d_values, d_scores, d_rowsum_global,
+                               static_cast<hipStream_t>(hip_stream));
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_snake_owner(const int64_t *counts, int32_t n_items, int32_t world, int32_t head, int32_t *owner) {
+  return guarded(nullptr, [&]() -> int {
+    if (n_items < 0 || world < 1 || head < 0 || (n_items > 0 && (!counts || !owner))) {
+      cooc_ctx::create_error() = "cooc_snake_owner: bad arguments";
+      return COOC_ERR_ARG;
+    }
+    cooc::snake_owner_host(counts, n_items, world, head, owner);
+    return COOC_OK;
+  });
+}
+
 int cooc_shard_plan(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
                     int64_t n_interactions, int32_t n_parts, uint64_t *d_desc, int32_t *d_row_counts,
                     uint16_t *d_arena, int64_t arena_cap, void *hip_stream, int64_t *h_send, int64_t *h_info) {

@@ -47,8 +47,11 @@ cooc_ctx::~cooc_ctx() {
   stream_state.release();
   sharder.release();
   counter.release();
+  comm.reset();
   cooc::DevBuf *bufs[] = {&b_user_ptr, &b_items, &b_tk_size, &b_tk_val, &b_tk_score, &b_obs3,
-                          &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms, &b_verify};
+                          &b_cut_ptr, &b_cut_items, &b_cut_tmp, &b_llr_terms, &b_verify,
+                          &own_counts, &own_sort, &own_tmp, &own_sizes, &own_owner, &own_lens,
+                          &own_up, &own_items, &own_obs, &own_rowsum};
   for (auto *b : bufs) b->release();
   if (timer.acc_begin) (void)hipEventDestroy(timer.acc_begin);
   if (timer.acc_end) (void)hipEventDestroy(timer.acc_end);

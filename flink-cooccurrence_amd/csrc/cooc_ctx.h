@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/cooc.h"
+#include "cooc_comm.h"
 #include "cooc_device.h"
 #include "cooc_shard.h"
 
@@ -140,6 +141,12 @@ struct cooc_ctx {
   cooc::Status topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,
                           int32_t *values, double *scores);
 
+  // multi-GPU large-universe window over the communicator (cooc_owned.hip): cooc_count_owned / cooc_topk_owned
+  cooc::Status count_owned(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
+                           hipStream_t s, cooc_owned_info *info, cooc_device_result *out);
+  cooc::Status topk_owned(int32_t topk, int32_t flags, int32_t *d_sizes, int32_t *d_values, double *d_scores,
+                          int64_t *d_rowsum_global, hipStream_t s);
+
   static std::string &create_error();
 
   cooc_config cfg{};
@@ -158,6 +165,9 @@ struct cooc_ctx {
   // user_cut > 0: the capped copy of a count_device CSR (first user_cut items of every user)
   cooc::DevBuf b_cut_ptr, b_cut_items, b_cut_tmp;
   cooc::DevBuf b_verify;  // cooc_verify_batch totals
+  // the communicator (cooc_comm_init*) and the owned-rows exchange's buffers
+  std::unique_ptr<cooc::Comm> comm;
+  cooc::DevBuf own_counts, own_sort, own_tmp, own_sizes, own_owner, own_lens, own_up, own_items, own_obs, own_rowsum;
   int32_t batch_topk = 0;
   int32_t batch_topk_flags = 0;
   bool have_batch = false;

@@ -201,9 +201,22 @@ def c3_lengths(u0: int, u1: int, seed: int = C3_SEED, device=None):
     return torch.as_tensor(lens_t, device=device)[(h >> 48) & 0xFFFF]
 
 
-def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None):
+C3_PERM_SEED = 0xC3B1  # the item-id bijection of the permuted C3 log (c3_item_perm)
+
+
+def c3_item_perm(M: int = C3_ITEMS, seed: int = C3_PERM_SEED) -> np.ndarray:
+    """A fixed bijection of [0, M) (numpy PCG64(seed).permutation): the permuted C3 log names the item
+    of Zipf rank r as perm[r], so item ids carry no popularity order (MovieLens / hashed ids)."""
+    key = ("perm", M, seed)
+    if key not in _c3_cache:
+        _c3_cache[key] = np.random.Generator(np.random.PCG64(seed)).permutation(M).astype(np.int32)
+    return _c3_cache[key]
+
+
+def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None, permute: bool = False):
     """CSR (user_ptr int64[U+1], items int32[N]) of users [u0, u1) of the shard-invariant C3 log:
-    numpy arrays when device is None, else torch tensors built on that device."""
+    numpy arrays when device is None, else torch tensors built on that device.  permute: every item id
+    x becomes c3_item_perm()[x] (same log, ids not in popularity order)."""
     lens = c3_lengths(u0, u1, seed, device)
     _, cdf = _c3_tables()
     if device is None:
@@ -213,6 +226,8 @@ def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None):
         h = _splitmix_np(((owner << np.uint64(14)) | j.astype(np.uint64)) ^ np.uint64((seed << 58) | 0x5A5A))
         x = (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
         items = np.minimum(np.searchsorted(cdf, x, side="right"), len(cdf) - 1).astype(np.int32)
+        if permute:
+            items = c3_item_perm(len(cdf))[items]
         return user_ptr, items
     import torch
 
@@ -226,8 +241,10 @@ def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None):
     x = ((h >> 11) & ((1 << 53) - 1)).to(torch.float64) * (1.0 / 9007199254740992.0)
     del h
     cdf_t = torch.as_tensor(cdf, device=device)
-    items = torch.clamp(torch.searchsorted(cdf_t, x, right=True), max=len(cdf) - 1).to(torch.int32)
-    return user_ptr, items
+    items = torch.clamp(torch.searchsorted(cdf_t, x, right=True), max=len(cdf) - 1)
+    if permute:
+        items = torch.as_tensor(c3_item_perm(len(cdf)), device=device)[items]
+    return user_ptr, items.to(torch.int32)
 
 
 def c3_ordered_pairs(u0: int, u1: int, seed: int = C3_SEED) -> int:

@@ -1,7 +1,8 @@
-"""Multi-GPU sharding layer: users sharded over ranks, rows owned by a mod world.
+"""Multi-GPU sharding layer: users sharded over ranks, rows owned by one rank each.
 
-Two exchanges are implemented, both keyed by owner(a) = a mod world (the reference's
-keyBy(ItemCooccurrences::getItem), FlinkCooccurrences.java:152):
+Three exchanges are implemented, all keyed by a row owner (the reference's
+keyBy(ItemCooccurrences::getItem), FlinkCooccurrences.java:152): ``count_owned`` (C3 / C5 universes,
+owner = the frequency-snake map), ``count_records`` and ``count_sharded`` (owner(a) = a mod world):
 
 * ``count_records`` (default) routes the pair RECORDS: every rank all-gathers the users' u16
   histories once (input sized) and all-to-alls one 8-B descriptor per (row, user) record to the
@@ -25,10 +26,14 @@ reference's keyed data-parallelism:
 
 Every library call runs on torch's current stream (cooc.h stream contract), so collectives and
 kernels are ordered by the stream itself; no device-wide synchronisation is needed.
-The compute (local reduce, pack, merge) runs in libcooc_hip.so; this module only moves buffers.
+The compute (local reduce, pack, merge) runs in libcooc_hip.so.  ``count_owned`` / ``topk_owned`` run
+WHOLE inside the library once the context has a communicator (``init_comm``: RCCL over xGMI, the
+product path; ``init_comm_torch_ops``: the same library exchange over torch.distributed collectives,
+e.g. gloo in the 2-process tests); without one this module moves the buffers itself.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
@@ -207,18 +212,126 @@ class OwnedResult:
 
 def _gather_parts(out, part, sizes, group=None):
     """out = the ranks' parts concatenated in rank order (sizes[r] elements from rank r): an uneven
-    all_to_all_single whose input is this rank's part repeated once per destination."""
+    all-to-all with this rank's part as the input of every destination -- over RCCL without a world-fold
+    copy of it (the list form); gloo has only the single-tensor form, which gets a repeated copy, freed at
+    once."""
     world = len(sizes)
     if world == 1:
         out.copy_(part)
         return
+    if dist.get_backend(group) == "nccl":
+        dist.all_to_all(list(out.split(list(sizes))), [part] * world, group=group)
+        return
     n = int(part.numel())
-    dist.all_to_all_single(out, part.repeat(world) if n else part, output_split_sizes=list(sizes),
-                           input_split_sizes=[n] * world, group=group)
+    rep = part.repeat(world) if n else part
+    dist.all_to_all_single(out, rep, output_split_sizes=list(sizes), input_split_sizes=[n] * world, group=group)
+    del rep
+
+
+# ---- the library's communicator ---------------------------------------------------------------------
+def init_comm(core, group=None) -> None:
+    """Give `core` the library's RCCL communicator over the ranks of `group` (one context per GPU
+    process): rank 0 creates the id (cooc_comm_unique_id), torch.distributed broadcasts it, every rank
+    joins (cooc_comm_init).  cooc_count_owned / cooc_topk_owned then run their exchanges inside the
+    library over RCCL (xGMI), on the caller's stream."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    buf = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        buf.copy_(torch.frombuffer(bytearray(core.comm_unique_id()), dtype=torch.uint8))
+    dist.broadcast(buf, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    core.comm_init(bytes(buf.cpu().numpy().tobytes()), rank, world)
+
+
+def init_comm_torch_ops(core, group=None) -> None:
+    """The library's exchange (cooc_count_owned / cooc_topk_owned) over torch.distributed collectives
+    through cooc_comm_ops callbacks (any backend; gloo in the tests): every callback drains the stream,
+    copies its device buffers to the host, runs the collective, and copies the result back."""
+    import numpy as np
+
+    from . import _lib
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    D2H, H2D = 2, 1
+
+    def d2h(ptr, nbytes):
+        a = np.empty(nbytes, np.uint8)
+        if nbytes:
+            assert hip.hipMemcpy(a.ctypes.data, ptr, nbytes, D2H) == 0
+        return a
+
+    def h2d(ptr, a):
+        if a.nbytes:
+            assert hip.hipMemcpy(ptr, a.ctypes.data, a.nbytes, H2D) == 0
+
+    def guard(fn):
+        def wrapped(*args):
+            try:
+                fn(*args)
+                return 0
+            except Exception:  # (a callback cannot raise through the C-ABI)
+                import traceback
+
+                traceback.print_exc()
+                return 1
+        return wrapped
+
+    @guard
+    def allreduce(_user, d_buf, n, stream):
+        assert hip.hipStreamSynchronize(stream) == 0
+        t = torch.from_numpy(d2h(d_buf, 8 * n).view(np.int64).copy())
+        dist.all_reduce(t, group=group)
+        h2d(d_buf, t.numpy().view(np.uint8))
+
+    @guard
+    def allgather(_user, d_send, d_recv, nbytes, stream):
+        assert hip.hipStreamSynchronize(stream) == 0
+        world = dist.get_world_size(group)
+        mine = torch.from_numpy(d2h(d_send, nbytes))
+        out = torch.empty(world * nbytes, dtype=torch.uint8)
+        dist.all_gather(list(out.split(nbytes)), mine, group=group)
+        h2d(d_recv, out.numpy())
+
+    @guard
+    def alltoallv(_user, d_send, send_off, send_bytes, d_recv, recv_off, recv_bytes, stream):
+        assert hip.hipStreamSynchronize(stream) == 0
+        world = dist.get_world_size(group)
+        sb = [int(send_bytes[p]) for p in range(world)]
+        rb = [int(recv_bytes[p]) for p in range(world)]
+        ins = torch.from_numpy(np.concatenate([d2h((d_send or 0) + int(send_off[p]), sb[p]) for p in range(world)]))
+        out = torch.empty(sum(rb), dtype=torch.uint8)
+        dist.all_to_all_single(out, ins, output_split_sizes=rb, input_split_sizes=sb, group=group)
+        pos = 0
+        for p in range(world):
+            h2d((d_recv or 0) + int(recv_off[p]), out[pos:pos + rb[p]].numpy())
+            pos += rb[p]
+
+    ops = _lib.CoocCommOps(_lib.ALLREDUCE_FN(allreduce), _lib.ALLGATHER_FN(allgather), _lib.ALLTOALLV_FN(alltoallv))
+    core.comm_init_ops(dist.get_rank(group), dist.get_world_size(group), ops)
+
+
+def _device_array(ptr: int, n: int, dtype, dev):
+    """A device tensor copy of n elements at a library-owned device pointer (borrowed view)."""
+    out = torch.empty(n, dtype=dtype, device=dev)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                       ctypes.c_void_p]
+        assert hip.hipMemcpyAsync(out.data_ptr(), ptr, out.element_size() * n, 3,
+                                  torch.cuda.current_stream(dev).cuda_stream) == 0
+    return out
 
 
 def count_owned(core, user_ptr, items, group=None, stream=None) -> OwnedResult:
-    """One window over this rank's users; histories all-gathered, owned rows counted here."""
+    """One window over this rank's users; histories all-gathered, owned rows counted here.  With a
+    library communicator (init_comm / init_comm_torch_ops) the whole step is cooc_count_owned."""
+    if getattr(core, "comm_world", 0) > 0:
+        res, info = core.count_owned(user_ptr, items, stream=stream)
+        owner = _device_array(info.owner, core.n_items, torch.int32, items.device)
+        return OwnedResult(info.part, info.n_parts, res, owner, int(info.observed), int(info.local_observed),
+                           int(info.n_users_all), int(info.n_interactions_all), int(info.gathered_bytes))
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = items.device
@@ -268,10 +381,13 @@ def topk_owned(core, owned: OwnedResult, topk: int, group=None, exact_scores: bo
     M = core.n_items
     dev = owned.owner.device
     rowsum = torch.empty(M, dtype=torch.int64, device=dev)
-    core.copy_rowsum_device(rowsum, stream)
-    dist.all_reduce(rowsum, group=group)
     sizes = torch.empty(M, dtype=torch.int32, device=dev)
     values = torch.empty((M, topk), dtype=torch.int32, device=dev)
     scores = torch.empty((M, topk), dtype=torch.float64, device=dev)
+    if getattr(core, "comm_world", 0) > 0:  # the all-reduce and the scoring inside the library
+        core.topk_owned(topk, sizes, values, scores, rowsum_global=rowsum, exact_scores=exact_scores, stream=stream)
+        return TopkResult(sizes, values, scores, rowsum)
+    core.copy_rowsum_device(rowsum, stream)
+    dist.all_reduce(rowsum, group=group)
     core.topk_batch_device(topk, sizes, values, scores, rowsum_global=rowsum, exact_scores=exact_scores, stream=stream)
     return TopkResult(sizes, values, scores, rowsum)

@@ -279,6 +279,66 @@ COOC_API int cooc_merge_partitions(cooc_ctx *ctx, int32_t n_parts, int32_t part,
                                    const uint64_t *d_recv_entries, const int64_t *d_rowsum_global, void *hip_stream,
                                    cooc_device_result *out);
 
+/* ---- communicator: the RCCL sharding layer behind the C-ABI ------------------------------------------
+ * The reference's keyed exchanges -- keyBy(user) (FlinkCooccurrences.java:70), keyBy(ItemCooccurrences::
+ * getItem) (:152) and rowSumStream.broadcast() (:163) -- as collectives inside the library, on the
+ * context's caller stream, over RCCL (xGMI on one node).  One context per GPU process / Flink subtask; the
+ * SURVEY §8(b) "refcounted device/RCCL singleton" is the process-wide RCCL library handle (dlopen'ed once;
+ * a process that already loaded RCCL shares it).
+ *   cooc_comm_unique_id  rank 0 creates the communicator id (COOC_COMM_ID_BYTES opaque bytes) and the
+ *                        caller distributes it (Flink: the job graph's broadcast / a shared file; Python:
+ *                        torch.distributed.broadcast).  Fails with COOC_ERR_HIP when RCCL is absent.
+ *   cooc_comm_init       every rank: joins the world-size communicator as `rank` on the context's device.
+ *   cooc_comm_init_ops   the same exchange over caller-provided collectives (any transport the caller has,
+ *                        e.g. gloo in tests).  Each operation is collective over the ranks, takes device
+ *                        pointers, returns 0 on success and must have completed with respect to hip_stream
+ *                        when it returns (later work enqueued on that stream sees its result):
+ *                          allreduce_sum_i64: d_buf[0, n) summed over the ranks, in place;
+ *                          allgather: rank r's `bytes` at d_send land at d_recv + r * bytes;
+ *                          alltoallv: send_bytes[p] bytes at d_send + send_off[p] go to rank p, which
+ *                            receives them at d_recv + recv_off[sender]; recv_bytes[p] arrive from rank p
+ *                            (host arrays of world entries). */
+#define COOC_COMM_ID_BYTES 128
+typedef struct cooc_comm_ops {
+  int (*allreduce_sum_i64)(void *user, int64_t *d_buf, int64_t n, void *hip_stream);
+  int (*allgather)(void *user, const void *d_send, void *d_recv, int64_t bytes, void *hip_stream);
+  int (*alltoallv)(void *user, const void *d_send, const int64_t *send_off, const int64_t *send_bytes, void *d_recv,
+                   const int64_t *recv_off, const int64_t *recv_bytes, void *hip_stream);
+} cooc_comm_ops;
+COOC_API int cooc_comm_unique_id(uint8_t *id);
+COOC_API int cooc_comm_init(cooc_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);
+COOC_API int cooc_comm_init_ops(cooc_ctx *ctx, int32_t rank, int32_t world, const cooc_comm_ops *ops, void *user);
+
+/* One window of the multi-GPU large-universe job (n_items >= 40,320: C3 / C5), whole inside the library on
+ * hip_stream: this rank's users (keyBy(user)) -> (1) local item frequencies, all-reduced (the planner's
+ * column estimate and the owner map); (2) the row owner map: rows by descending global frequency (ties:
+ * smaller id), the 4,096 most frequent placed greedily on the least loaded rank, the rest dealt in snake
+ * order (cooc_snake_owner); (3) the histories all-gathered (one uneven all-to-all per array: every rank
+ * sends its part to every peer at once, each pair over its own xGMI link); (4) the owned rows counted over
+ * all users (cooc_count_device_owned: the keyBy(getItem) as ownership -- rows are complete on their owner,
+ * nothing is merged); (5) the ordered pairs all-reduced.  *out: the owned rows (borrowed, as
+ * cooc_count_device_owned); *info the totals and borrowed device views of the owner map and the global
+ * item frequencies. */
+typedef struct cooc_owned_info {
+  int32_t part, n_parts;
+  int64_t observed;           /* ordered pairs of the whole job (sum over the ranks) */
+  int64_t local_observed;     /* ordered pairs of this rank's owned rows */
+  int64_t n_users_all, n_interactions_all;
+  int64_t gathered_bytes;     /* history bytes this rank received */
+  const int32_t *owner;       /* device int32[n_items] */
+  const int64_t *item_counts; /* device int64[n_items]: the all-reduced frequencies */
+} cooc_owned_info;
+COOC_API int cooc_count_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
+                              int64_t n_interactions, void *hip_stream, cooc_owned_info *info,
+                              cooc_device_result *out);
+/* C5 after cooc_count_owned: the owned rows' row sums all-reduced (the broadcast row-sum stream,
+ * FlinkCooccurrences.java:163), then every owned row's LLR top-k against them (cooc_topk_batch_device).
+ * d_rowsum_global (device int64[n_items], may be NULL) receives the all-reduced row sums. */
+COOC_API int cooc_topk_owned(cooc_ctx *ctx, int32_t topk, int32_t flags, int32_t *d_sizes, int32_t *d_values,
+                             double *d_scores, int64_t *d_rowsum_global, void *hip_stream);
+/* The owner map of step (2) on the host (no device): counts int64[n_items] -> owner int32[n_items]. */
+COOC_API int cooc_snake_owner(const int64_t *counts, int32_t n_items, int32_t world, int32_t head, int32_t *owner);
+
 /* ---- sharded records (multi-GPU: the keyBy(itemA) of FlinkCooccurrences.java:152 on pair RECORDS) -
  * Users are sharded over n_parts GPUs (keyBy(user), :70); row a is owned by part a mod n_parts.  The
  * reference ships each pair record (itemA, the user's history) to the owner of itemA; here every

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--lib", default=None, help="another build of libcooc_hip.so (e.g. the statistics build)")
     ap.add_argument("--planner", default="auto", help='CooccurrenceCore planner ("sort": every whole row through '
                     'the sort + segmented-reduce path)')
+    ap.add_argument("--permute", action="store_true", help="item ids through datagen.c3_item_perm (not rank-ordered)")
     args = ap.parse_args()
     import torch
 
@@ -40,7 +41,7 @@ def main():
     dev = torch.device("cuda", 0)
     U = datagen.C3_USERS // args.shards
     t0 = time.perf_counter()
-    up, it = datagen.c3_users(0, U, device=dev)
+    up, it = datagen.c3_users(0, U, device=dev, permute=args.permute)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     P = datagen.c3_ordered_pairs(0, U)
@@ -79,6 +80,7 @@ def main():
         "check_sum_rowsum_eq_P": rs_total == P,
         "gen_s": t_gen,
         "planner": args.planner,
+        "permuted_ids": args.permute,
         "sort_path_rows_pairs": core.last_sort_rows(),
         "verify": core.verify_batch(),
     }

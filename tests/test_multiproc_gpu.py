@@ -75,7 +75,7 @@ def _c2_log():
     return up, it, 3000
 
 
-def _worker(rank, world, port, out_dir, n_users, topk):
+def _worker(rank, world, port, out_dir, n_users, topk, exchange):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     sys.path.insert(0, ROOT)
     import torch
@@ -97,6 +97,8 @@ def _worker(rank, world, port, out_dir, n_users, topk):
     up_r = torch.from_numpy(up[u0:u1 + 1] - lo).to(dev)
     it_r = torch.from_numpy(it[lo:hi]).to(dev)
     with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        if exchange == "library":  # cooc_count_owned / cooc_topk_owned: the exchange inside the library
+            sharding.init_comm_torch_ops(core)
         res = sharding.count_owned(core, up_r, it_r)
         torch.cuda.current_stream().synchronize()
         rp, cols, cnt, rowsum = _rows(res.owned, M)
@@ -123,12 +125,16 @@ def _worker(rank, world, port, out_dir, n_users, topk):
     dist.destroy_process_group()
 
 
-def test_two_ranks_real_core_vs_one_process(pkg, torch_cuda, tmp_path):
+@pytest.mark.parametrize("exchange", ["torch", "library"])
+def test_two_ranks_real_core_vs_one_process(pkg, torch_cuda, tmp_path, exchange):
+    """exchange "torch": sharding.py moves the buffers over torch.distributed; "library": the whole C3 step
+    is cooc_count_owned / cooc_topk_owned, the library's exchange over cooc_comm_ops callbacks (gloo here,
+    RCCL in production: the same orchestration code)."""
     import torch
     import torch.multiprocessing as mp
 
     world, n_users, topk = 2, 4000, 10
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_users, topk), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_users, topk, exchange), nprocs=world, join=True)
     parts = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
 
     # the whole log in one process
@@ -185,6 +191,46 @@ def test_two_ranks_real_core_vs_one_process(pkg, torch_cuda, tmp_path):
             sl, ws = slice(p["c2_rp"][i], p["c2_rp"][i + 1]), slice(w_rp[a], w_rp[a + 1])
             assert np.array_equal(p["c2_cols"][sl], w_cols[ws]) and np.array_equal(p["c2_cnt"][sl], w_cnt[ws]), f"row {a}"
             assert p["c2_rowsum"][i] == w_rowsum[a]
+
+
+def test_rccl_world1_count_owned_equals_count_device(pkg, torch_cuda):
+    """The RCCL transport (cooc_comm_init over librccl.so.1) at world size 1: cooc_count_owned (item counts
+    all-reduced, owner map, history exchange, owned count, pairs all-reduced -- every collective through
+    RCCL) owns every row and equals cooc_count_device; cooc_topk_owned equals the batch top-k."""
+    import torch
+
+    up, it, M = _c3_log(3000)
+    dev = torch.device("cuda", 0)
+    up_d, it_d = torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev)
+    topk = 10
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        whole = core.count_device(up_d, it_d)
+        torch.cuda.current_stream().synchronize()
+        w = _rows(whole, M)
+        sizes = torch.empty(M, dtype=torch.int32, device=dev)
+        vals = torch.empty((M, topk), dtype=torch.int32, device=dev)
+        scores = torch.empty((M, topk), dtype=torch.float64, device=dev)
+        core.topk_batch_device(topk, sizes, vals, scores)
+        torch.cuda.current_stream().synchronize()
+        w_tk = (sizes.cpu().numpy(), vals.cpu().numpy(), scores.cpu().numpy())
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        core.comm_init(core.comm_unique_id(), 0, 1)
+        res, info = core.count_owned(up_d, it_d)
+        torch.cuda.current_stream().synchronize()
+        o = _rows(res, M)
+        lens = np.diff(up)
+        assert info.observed == info.local_observed == int(np.sum(lens * (lens - 1)))
+        assert info.n_users_all == len(lens) and info.n_interactions_all == len(it) and info.gathered_bytes == 0
+        assert np.all(_d2h(info.owner, M, np.int32) == 0)
+        assert np.array_equal(_d2h(info.item_counts, M, np.int64), np.bincount(it, minlength=M))
+        for x, y in zip(o, w):
+            assert np.array_equal(x, y)
+        rs = torch.empty(M, dtype=torch.int64, device=dev)
+        core.topk_owned(topk, sizes, vals, scores, rowsum_global=rs)
+        torch.cuda.current_stream().synchronize()
+        assert np.array_equal(rs.cpu().numpy(), w[3])
+        assert np.array_equal(sizes.cpu().numpy(), w_tk[0]) and np.array_equal(vals.cpu().numpy(), w_tk[1])
+        assert np.array_equal(scores.cpu().numpy(), w_tk[2], equal_nan=True)
 
 
 @pytest.fixture(scope="module")

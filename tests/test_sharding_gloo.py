@@ -243,6 +243,21 @@ def test_snake_owner_balances_zipf(pkg):
         assert mass.max() / mass.mean() < 1.03
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_library_snake_owner_equals_python(pkg, world):
+    """cooc_snake_owner (the owner map cooc_count_owned builds inside the library) == sharding.snake_owner,
+    ties in the frequencies included (a smaller id first; a smaller rank first at equal load)."""
+    from flink_cooccurrence_amd import core, sharding
+
+    rng = np.random.default_rng(world)
+    for counts in (np.round(1e7 / np.arange(1, 60_001)).astype(np.int64), rng.integers(0, 50, 30_000),
+                   np.zeros(100, np.int64), np.array([5], np.int64)):
+        want = sharding.snake_owner(torch.from_numpy(counts), world).numpy()
+        assert np.array_equal(core.CooccurrenceCore.snake_owner(counts, world), want)
+        assert np.array_equal(core.CooccurrenceCore.snake_owner(counts, world, head=7),
+                              sharding.snake_owner(torch.from_numpy(counts), world, head=7).numpy())
+
+
 @pytest.mark.parametrize("world,mode", [(2, "partials"), (3, "partials"), (2, "records"), (3, "records"), (2, "owned"),
                                         (3, "owned"), (2, "owned_topk"), (3, "owned_topk")])
 def test_count_sharded_gloo(oracle, pkg, world, mode):
