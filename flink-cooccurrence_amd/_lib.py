@@ -26,6 +26,7 @@ COOC_FLAG_OUTPUT_CSR = 2
 COOC_FLAG_OUTPUT_DENSE = 4
 COOC_FLAG_GENERAL_PLANNER = 8
 COOC_FLAG_SORT_ROWS = 16
+COOC_FLAG_COLUMN_ORDER = 32
 COOC_VERIFY_SYMMETRY = 1
 
 i16p = ctypes.POINTER(ctypes.c_int16)
@@ -113,6 +114,7 @@ _SIGS = {
     "cooc_item_counts": (ctypes.c_int, [vp, vp, ctypes.c_int64, vp, vp]),
     "cooc_count_device_owned": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.c_int32, vp,
                                                ctypes.c_int64, vp, ctypes.POINTER(CoocDeviceResult)]),
+    "cooc_copy_column_order": (ctypes.c_int, [vp, i32p]),
     "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
     "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),

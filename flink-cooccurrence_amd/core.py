@@ -91,13 +91,15 @@ class CooccurrenceCore:
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
                  exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0,
-                 devices=None, subtask: int = 0):
+                 devices=None, subtask: int = 0, column_order: bool = False):
         """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
         planner: "auto" (the batch planner below 40,320 items, the large-universe planner above), "large"
         (the large-universe planner at any n_items; "general" is an alias) or "sort" (large, with every
         whole row through the sort + segmented-reduce path: packed 64-bit pair keys, radix sort, runs).
         user_cut: kMax, 0 = off; else only the first user_cut interactions of every user are expanded
-        (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped)."""
+        (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped).
+        column_order: COOC_FLAG_COLUMN_ORDER (device rows of the large-universe path in column-id order instead
+        of descending batch frequency)."""
         L = _lib.load()
         flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
         if output not in ("auto", "csr", "dense"):
@@ -107,6 +109,7 @@ class CooccurrenceCore:
             raise _lib.IllegalArgumentException(_lib.COOC_ERR_ARG, f"unknown planner {planner!r}")
         flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner != "auto" else 0
         flags |= _lib.COOC_FLAG_SORT_ROWS if planner == "sort" else 0
+        flags |= _lib.COOC_FLAG_COLUMN_ORDER if column_order else 0
         cfg = CoocConfig(device, n_items, topk, flags, window_size_ms, user_cut, 0)
         h = ctypes.c_void_p()
         if devices is None:
@@ -187,6 +190,14 @@ class CooccurrenceCore:
         check(_lib.load().cooc_copy_batch(self._h, _p(rp, i64p), _p(cols, i32p), _p(cnt, u32p), _p(cnt16, i16p),
                                           _p(rs, i64p), _p(rs32, i32p)), self._h)
         return BatchResult(rp, cols, cnt, cnt16, rs, rs32, int(observed))
+
+    def column_order(self) -> np.ndarray:
+        """cooc_copy_column_order: the position of every column in the last batch's device row order (its
+        top-k iteration order): the descending-frequency rank after the large-universe relabel, else the
+        column id."""
+        out = np.zeros(self.n_items, np.int32)
+        check(_lib.load().cooc_copy_column_order(self._h, _p(out, i32p)), self._h)
+        return out
 
     def topk_batch(self, topk: int, exact_scores: bool = False, stream=None):
         """LLR top-k of every row of the last batch -> (sizes [M], values [M, k], scores [M, k])."""

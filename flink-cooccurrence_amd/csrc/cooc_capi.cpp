@@ -135,6 +135,22 @@ int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactio
   });
 }
 
+int cooc_copy_column_order(cooc_ctx *ctx, int32_t *rank_of) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !rank_of) return COOC_ERR_ARG;
+    if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no batch result on this context");
+    (void)hipSetDevice(ctx->device);
+    const int32_t M = ctx->cfg.n_items;
+    if (!ctx->batch_result.rank_of) {
+      for (int32_t a = 0; a < M; a++) rank_of[a] = a;
+      return COOC_OK;
+    }
+    hipError_t e = hipMemcpy(rank_of, ctx->batch_result.rank_of, sizeof(int32_t) * size_t(M), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(ctx, COOC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    return COOC_OK;
+  });
+}
+
 int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
                     cooc_window_info *info) {
   return guarded(ctx, [&]() -> int {

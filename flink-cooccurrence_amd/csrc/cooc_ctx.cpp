@@ -38,6 +38,7 @@ Status cooc_ctx::init(const cooc_config &c) {
   counter.set_output_layout((c.flags & COOC_FLAG_OUTPUT_DENSE) ? 2 : (c.flags & COOC_FLAG_OUTPUT_CSR) ? 1 : 0);
   counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0);
   counter.set_sort_rows((c.flags & COOC_FLAG_SORT_ROWS) != 0);
+  counter.set_relabel((c.flags & COOC_FLAG_COLUMN_ORDER) == 0);
   return Status::Ok();
 }
 
@@ -175,9 +176,11 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
   uint32_t *d_cnt;
   COOC_TRY(counter.pack(stream, &d_rp, &d_col, &d_cnt));
   COOC_HIP_TRY(hipStreamSynchronize(stream));
-  if (row_ptr) COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
-  if (cols && batch_nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
-  if ((cnt || cnt16) && batch_nnz) {
+  if (!batch_result.rank_of) {
+    if (row_ptr) COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
+    if (cols && batch_nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
+  }
+  if ((cnt || cnt16 || batch_result.rank_of) && batch_nnz) {
     std::vector<uint32_t> tmp;
     uint32_t *dst = cnt;
     if (!dst) {
@@ -185,8 +188,31 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
       dst = tmp.data();
     }
     COOC_HIP_TRY(hipMemcpy(dst, d_cnt, sizeof(uint32_t) * batch_nnz, hipMemcpyDeviceToHost));
+    if (batch_result.rank_of) {
+      // the device rows are in descending-frequency column order (the large-universe relabel): the packed
+      // host copy is in ascending column order, each row sorted as (column, count) pairs
+      std::vector<int64_t> rp(static_cast<size_t>(M) + 1);
+      std::vector<int32_t> cc(static_cast<size_t>(batch_nnz));
+      COOC_HIP_TRY(hipMemcpy(rp.data(), d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
+      COOC_HIP_TRY(hipMemcpy(cc.data(), d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
+      std::vector<uint64_t> kv;
+      for (int32_t a = 0; a < M; a++) {
+        const int64_t b0 = rp[size_t(a)], b1 = rp[size_t(a) + 1];
+        kv.resize(size_t(b1 - b0));
+        for (int64_t i = b0; i < b1; i++) kv[size_t(i - b0)] = (uint64_t(uint32_t(cc[size_t(i)])) << 32) | dst[i];
+        std::sort(kv.begin(), kv.end());
+        for (int64_t i = b0; i < b1; i++) {
+          cc[size_t(i)] = int32_t(kv[size_t(i - b0)] >> 32);
+          dst[i] = uint32_t(kv[size_t(i - b0)]);
+        }
+      }
+      if (row_ptr) std::copy(rp.begin(), rp.end(), row_ptr);
+      if (cols) std::copy(cc.begin(), cc.end(), cols);
+    }
     if (cnt16)  // Int2ShortOpenHashMap value: the count modulo 2^16 as a signed short
       for (int64_t i = 0; i < batch_nnz; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
+  } else if (batch_result.rank_of && row_ptr) {
+    COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
   }
   if (rowsum || rowsum32) {
     std::vector<int64_t> tmp(M);

@@ -124,6 +124,9 @@ struct CountResult {
   uint32_t *cnt = nullptr;
   int64_t *rowsum = nullptr;
   uint32_t *dense = nullptr;  // dense output: row-major [M x M] counts (row_base / col / cnt unused)
+  // the column order of the rows: ascending rank_of[col] (the large-universe batch path numbers the columns
+  // by descending frequency); NULL = ascending column id
+  const int32_t *rank_of = nullptr;
   int64_t nnz = 0;
   int64_t observed = 0;  // ordered pairs of the run
   int64_t work = 0;
@@ -182,6 +185,8 @@ class Counter {
   // COOC_FLAG_SORT_ROWS: every whole row of the large-universe path through the sort + segmented-reduce
   // path (otherwise only rows whose LDS hash table overflowed); rows and pairs it took in the last run
   void set_sort_rows(bool on) { sort_rows_ = on; }
+  void set_relabel(bool on) { relabel_ = on; }
+  const int32_t *last_rank_of() const { return last_rank_of_; }
   int64_t last_deferred_rows() const { return last_deferred_; }
   int64_t last_deferred_pairs() const { return last_deferred_pairs_; }
   static constexpr int32_t kBatchMaxItems = 40320;
@@ -234,6 +239,11 @@ class Counter {
   DevBuf sp_defer_, sr_keys_, sr_ukeys_, sr_ucnt_, sr_aux_;
   int64_t last_deferred_ = 0, last_deferred_pairs_ = 0;
   bool sort_rows_ = false;  // COOC_FLAG_SORT_ROWS
+  // batch windows of the large-universe path: columns relabelled by descending frequency (off: column ids,
+  // COOC_FLAG_COLUMN_ORDER); the last run's maps (NULL without a relabel)
+  bool relabel_ = true;
+  DevBuf sp_rank_, sp_rkeys_;
+  const int32_t *last_col_of_ = nullptr, *last_rank_of_ = nullptr;
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
                       const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;

@@ -144,7 +144,16 @@ struct SpArgs {
   const int64_t *spre;      // streaming window: [n_contrib + 1] prefix of the kSelfBit flags; NULL: all set
   int32_t *deferred;        // [M] whole rows left to the sort + segmented-reduce path (k_sr_*), in tot->n_deferred
   int32_t sort_all;         // COOC_FLAG_SORT_ROWS: every whole row goes to that path (A/B and tests)
+  // column relabel (batch windows): the kernels work in frequency-rank space -- column k of the arenas,
+  // tiles, tables and staging rows is the item of rank k -- and write col_of[k] to the output.
+  // NULL: identity (streaming windows)
+  const int32_t *col_of;    // [M] rank -> item id
+  const int32_t *rank_of;   // [M] item id -> rank
 };
+
+// the item of column rank r / the rank of item a (identity without a relabel)
+__device__ inline int32_t sp_col(const SpArgs &A, uint32_t r) { return A.col_of ? A.col_of[r] : int32_t(r); }
+__device__ inline int32_t sp_rank(const SpArgs &A, int32_t a) { return A.rank_of ? A.rank_of[a] : a; }
 
 #ifdef COOC_SP_TRACE
 #define PROG(A, k, v) do { if (threadIdx.x == 0) __hip_atomic_store((A).prog + blockIdx.x * 64 + (k), (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
@@ -246,7 +255,8 @@ constexpr uint32_t kSink16 = 0xFFFFu;  // (arena0 pads; never a tile-0 id)
 __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t *__restrict__ up,
                                                         const int32_t *__restrict__ items, int32_t M,
                                                         uint64_t *__restrict__ len, const int32_t *__restrict__ owner,
-                                                        int32_t part, int32_t *__restrict__ ownc) {
+                                                        int32_t part, int32_t *__restrict__ ownc,
+                                                        const int32_t *__restrict__ rank_of) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -261,8 +271,10 @@ __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t
 #pragma unroll
       for (int k = 0; k < 4; k++) {  // (an invalid id goes to tile 0 in k_sp_tile_lists, which reports it)
         const bool in = p0 + 64 * k + lane < n;
-        n0 += int32_t(__popcll(__ballot(in && (uint32_t(it[k]) < uint32_t(kTW) || uint32_t(it[k]) >= uint32_t(M)))));
-        if (owner) mine += int32_t(__popcll(__ballot(uint32_t(it[k]) < uint32_t(M) && owner[it[k]] == part)));
+        const bool valid = uint32_t(it[k]) < uint32_t(M);
+        const uint32_t rk = valid && rank_of ? uint32_t(rank_of[it[k]]) : uint32_t(it[k]);
+        n0 += int32_t(__popcll(__ballot(in && (rk < uint32_t(kTW) || !valid))));
+        if (owner) mine += int32_t(__popcll(__ballot(valid && owner[it[k]] == part)));
       }
     }
     if (lane == 0) {
@@ -287,7 +299,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
                                                        uint32_t *__restrict__ keys,
                                                        uint32_t *__restrict__ vals, const int32_t *__restrict__ owner,
                                                        int32_t part, const int64_t *__restrict__ ownoff,
-                                                       PlanTotals *__restrict__ tot) {
+                                                       PlanTotals *__restrict__ tot, const int32_t *__restrict__ rank_of) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int32_t *c = cur[wave];
@@ -320,9 +332,10 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
     int32_t n0 = 0;  // (tile-0 ids, the Zipf head, counted by ballot: no same-address LDS atomics)
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     int64_t o = owner ? ownoff[j] : 0;  // (owned contributions: at ownoff[j], in list order)
-    auto count = [&](bool in, int32_t p, int32_t it, bool valid) {
-      n0 += __popcll(__ballot(in && (it >> kTShift) == 0));
-      if (in && (it >> kTShift)) atomicAdd(&c[it >> kTShift], 1);
+    // it: the item id (contributions, owner map); rk: its column rank (tiles, arenas)
+    auto count = [&](bool in, int32_t p, int32_t it, int32_t rk, bool valid) {
+      n0 += __popcll(__ballot(in && (rk >> kTShift) == 0));
+      if (in && (rk >> kTShift)) atomicAdd(&c[rk >> kTShift], 1);
       if (!owner) {
         if (keys && in) {  // (NULL: the contributions come from elsewhere, k_sp_window_contribs)
           keys[s + p] = uint32_t(it);
@@ -339,13 +352,15 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
       }
     };
     bool valid[kTlR];
+    int32_t rk[kTlR];
 #pragma unroll
     for (int k = 0; k < kTlR; k++) {
       valid[k] = uint32_t(r[k]) < uint32_t(M);
       if (!valid[k]) r[k] = 0;
+      rk[k] = rank_of && lane + 64 * k < n ? rank_of[r[k]] : r[k];
     }
 #pragma unroll
-    for (int k = 0; k < kTlR; k++) count(lane + 64 * k < n, lane + 64 * k, r[k], valid[k]);
+    for (int k = 0; k < kTlR; k++) count(lane + 64 * k < n, lane + 64 * k, r[k], rk[k], valid[k]);
     for (int32_t p0 = 64 * kTlR; p0 < n; p0 += 64) {
       const int32_t p = p0 + lane;
       int32_t it = p < n ? items[s + p] : 0;
@@ -354,7 +369,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
         bad = true;
         it = 0;
       }
-      count(p < n, p, it, v);
+      count(p < n, p, it, rank_of && p < n ? rank_of[it] : it, v);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -398,12 +413,12 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
       q0 += int32_t(__popcll(b));
     };
 #pragma unroll
-    for (int k = 0; k < kTlR; k++) place(lane + 64 * k < n, r[k]);
+    for (int k = 0; k < kTlR; k++) place(lane + 64 * k < n, rk[k]);
     for (int32_t p0 = 64 * kTlR; p0 < n; p0 += 64) {  // (long lists: L1 / L2 lines of the first pass)
       const int32_t p = p0 + lane;
       int32_t it = p < n ? items[s + p] : 0;
       if (uint32_t(it) >= uint32_t(M)) it = 0;
-      place(p < n, it);
+      place(p < n, rank_of && p < n ? rank_of[it] : it);
     }
     if (lane < ((n0 + 7) & ~7) - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
     if (lane < ((n1 + 3) & ~3) - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
@@ -443,6 +458,41 @@ __global__ __launch_bounds__(256) void k_sp_window_contribs(int64_t U, const int
       vals[c + p] = p >= o ? (uint32_t(2 * j) | kSelfBit) : uint32_t(2 * j + 1);
     }
   }
+}
+
+// The (item, user) contributions of a batch in CSR order, for the item sort (the keyBy(itemA) regrouping,
+// FlinkCooccurrences.java:152) ahead of the column relabel; an invalid id (k_sp_tile_lists reports it)
+// becomes row 0.  One wave per user.
+__global__ __launch_bounds__(256) void k_sp_contribs(int64_t U, const int64_t *__restrict__ up,
+                                                     const int32_t *__restrict__ items, int32_t M,
+                                                     uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = gw; j < U; j += n_waves) {
+    const int64_t s = up[j], e = up[j + 1];
+    for (int64_t p = s + lane; p < e; p += 64) {
+      const int32_t it = items[p];
+      keys[p] = uint32_t(it) < uint32_t(M) ? uint32_t(it) : 0u;
+      vals[p] = uint32_t(j);
+    }
+  }
+}
+
+// Column relabel: sort keys = the items' frequencies (the row lengths of the item-sorted contributions, or
+// the caller's global counts), values = the ids; a stable descending sort then gives col_of (rank -> id,
+// ties: the smaller id first), and k_rank_scatter its inverse.
+__global__ void k_rank_keys(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ freq, int32_t M,
+                            uint64_t *__restrict__ keys, int32_t *__restrict__ ids) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  keys[a] = uint64_t(freq ? freq[a] : row_ptr[a + 1] - row_ptr[a]);
+  ids[a] = a;
+}
+
+__global__ void k_rank_scatter(const int32_t *__restrict__ col_of, int32_t M, int32_t *__restrict__ rank_of) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < M) rank_of[col_of[r]] = r;
 }
 
 struct WidenCount {
@@ -1065,7 +1115,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
         if (!v[k]) continue;
         if (base >= 0) {
           if (BCHK(A, pos >= 0 && pos < A.cap, 64)) {
-            A.col_out[pos] = c0 + b + k;
+            A.col_out[pos] = sp_col(A, uint32_t(c0 + b + k));
             A.cnt_out[pos] = v[k];
           }
         }
@@ -1178,7 +1228,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
       if (ek[i] == ~0u) continue;
       const uint32_t col = ek[i], r = er[i];
       const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
-      sc[q] = uint32_t(c0) + col;
+      sc[q] = uint32_t(sp_col(A, uint32_t(c0) + col));
       sn[q] = ec[i];
     }
     __syncthreads();
@@ -1213,7 +1263,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
       const uint32_t col = ek[i], r = er[i];
       const int64_t pos = base + cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
       if (BCHK(A, pos >= 0 && pos < A.cap, 128)) {
-        A.col_out[pos] = c0 + int32_t(col);
+        A.col_out[pos] = sp_col(A, uint32_t(c0) + col);
         A.cnt_out[pos] = ec[i];
       }
     }
@@ -1265,6 +1315,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (tid == 0) next = atomicAdd(A.qctr, 1);
     const SpWork it = A.queue[w];
     const int32_t a = it.row;
+    const int32_t ra = sp_rank(A, a);  // the row's own column (the self term), in column-rank space
     const bool split = it.kind == -2;  // a share of a split row's contributions, every tile, into staging
     const int64_t k0 = it.k0, k1 = it.k1;
     int t = 0;
@@ -1399,15 +1450,15 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
         __syncthreads();
         STAT_ADD(26, STAT_CLOCK() - c_walked);  // the share's flush of this tile into the staging row
       } else if (dense) {
-        if (tid == 0 && a >= c0 && a < c1) L.R[a - c0] -= self;
+        if (tid == 0 && ra >= c0 && ra < c1) L.R[ra - c0] -= self;
         __syncthreads();
         sp_dense_compact(A, L, S_, c1 - c0, c0, rsum);
         STAT_ADD(2, STAT_CLOCK() - c_walked);
       } else {
-        if (tid == 0 && a >= c0 && a < c1) {
-          uint32_t h = (uint32_t(a) * 0x9E3779B1u) >> op.hshift;
+        if (tid == 0 && ra >= c0 && ra < c1) {
+          uint32_t h = (uint32_t(ra) * 0x9E3779B1u) >> op.hshift;
           for (int p = 0; p < H; p++) {
-            if (L.R[h] == uint32_t(a) + 1u) {
+            if (L.R[h] == uint32_t(ra) + 1u) {
               L.R[kHashMax + h] -= self;
               break;
             }
@@ -1482,13 +1533,16 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
                                                                     int64_t *__restrict__ row_base,
                                                                     int32_t *__restrict__ row_nnz,
                                                                     PlanTotals *__restrict__ tot,
-                                                                    const int64_t *__restrict__ spre) {
+                                                                    const int64_t *__restrict__ spre,
+                                                                    const int32_t *__restrict__ col_of,
+                                                                    const int32_t *__restrict__ rank_of) {
   __shared__ uint32_t s_w[kFinWaves];
   __shared__ uint64_t s_red[kFinWaves];
   __shared__ int64_t s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t s = blockIdx.x;
   const int32_t a = split_row[s];
+  const int32_t ra = rank_of ? rank_of[a] : a;  // staging rows are in column-rank space
   const uint32_t self = uint32_t(spre ? spre[row_ptr[a + 1]] - spre[row_ptr[a]] : row_ptr[a + 1] - row_ptr[a]);
   const uint32_t *row = staging + int64_t(s) * stride;
   constexpr int32_t kStep = 64 * 4 * kFinU;  // columns per wave step
@@ -1505,7 +1559,7 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
       for (int k = 0; k < 4; k++) v[k] = b + k < hi ? row[b + k] : 0u;
     }
     for (int k = 0; k < 4; k++)
-      if (b + k == a) v[k] -= self;
+      if (b + k == ra) v[k] -= self;
   };
   uint32_t cnt = 0;
   uint64_t sum = 0;
@@ -1562,7 +1616,7 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (v[u][k]) {
-          col_out[pos] = b + k;
+          col_out[pos] = col_of ? col_of[b + k] : b + k;
           cnt_out[pos] = v[u][k];
           pos++;
         }
@@ -1654,11 +1708,13 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
                                                         int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
                                                         unsigned long long *__restrict__ bump, int64_t cap,
                                                         int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
-                                                        PlanTotals *__restrict__ tot) {
+                                                        PlanTotals *__restrict__ tot, const int32_t *__restrict__ col_of,
+                                                        const int32_t *__restrict__ rank_of) {
   __shared__ int64_t s_diag, s_base;
   __shared__ unsigned long long s_sum;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int32_t a = rows[j];
+  const uint32_t ra = uint32_t(rank_of ? rank_of[a] : a);  // the keys' columns are ranks
   const int64_t r0 = rstart[j], r1 = rstart[j + 1];
   const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1];
   const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
@@ -1670,7 +1726,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
   uint64_t sum = 0;
   for (int64_t r = r0 + tid; r < r1; r += kSrThreads) {
     sum += ucnt[r];
-    if (uint32_t(ukeys[r]) == uint32_t(a)) s_diag = r;
+    if (uint32_t(ukeys[r]) == ra) s_diag = r;
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
   if ((tid & 63) == 0) atomicAdd(&s_sum, (unsigned long long)sum);
@@ -1699,7 +1755,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
   for (int64_t r = r0 + tid; r < r1; r += kSrThreads) {
     if (drop && r == diag) continue;
     const int64_t q = base + (r - r0) - (drop && r > diag ? 1 : 0);
-    col_out[q] = int32_t(uint32_t(ukeys[r]));
+    col_out[q] = col_of ? col_of[uint32_t(ukeys[r])] : int32_t(uint32_t(ukeys[r]));
     cnt_out[q] = ucnt[r] - (r == diag ? self : 0u);
   }
 }
@@ -1779,6 +1835,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
     }
     // 3. run heads (a 256-bit mask in four ballots), counts, the diagonal's self term
     const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
+    const uint32_t ra = uint32_t(sp_rank(A, a));
     uint64_t hm[kTinyW / 64];
 #pragma unroll
     for (int g = 0; g < kTinyW / 64; g++) {
@@ -1803,7 +1860,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
             if (nx == W && hm[g2]) nx = uint32_t(g2 * 64 + __ffsll((long long)hm[g2]) - 1);
         }
         cnt = nx - q;
-        if (b[q] == uint32_t(a)) cnt -= self;
+        if (b[q] == ra) cnt -= self;
       }
       my_cnt[g] = cnt;
       keep[g] = __ballot(cnt != 0u);
@@ -1836,7 +1893,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
     for (int g = 0; g < kTinyW / 64; g++) {
       if (my_cnt[g]) {
         const int64_t pos = base + before + uint32_t(__popcll(keep[g] & lt));
-        A.col_out[pos] = int32_t(b[g * 64 + lane]);
+        A.col_out[pos] = sp_col(A, b[g * 64 + lane]);
         A.cnt_out[pos] = my_cnt[g];
         rsum += my_cnt[g];
       }
@@ -1974,8 +2031,50 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
 
-  // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
   const int64_t waves = std::min<int64_t>(std::max<int64_t>(U, 1), 65536);
+  // 0. column relabel (batch windows; not streaming ones, whose delta rows merge into column-ordered global
+  // rows): columns are numbered by descending frequency -- the frequencies of this log, or the caller's
+  // global counts -- so that the hot columns fill the u16 tile 0 and the tiles' masses fall monotonically,
+  // whatever order the ids come in.  Rows come out in that column order (CountResult.rank_of).
+  const bool relabel = relabel_ && !win;
+  int32_t *col_of = nullptr, *rank_of = nullptr;
+  const int64_t *freq_rank = nullptr;  // the frequencies in rank order (the planner's column estimate)
+  bool sorted_early = false;           // contributions sorted ahead of the relabel (no owner)
+  if (relabel) {
+    COOC_TRY(sp_rank_.reserve(sizeof(int32_t) * size_t(3 * M)));
+    COOC_TRY(sp_rkeys_.reserve(sizeof(uint64_t) * size_t(2 * M)));
+    col_of = sp_rank_.as<int32_t>();
+    rank_of = col_of + M;
+    int32_t *ids = rank_of + M;
+    uint64_t *rk_in = sp_rkeys_.as<uint64_t>(), *rk_out = rk_in + M;
+    int64_t n_tot = n;
+    if (!owner) {  // the log's own frequencies: the row lengths of the item-sorted contributions
+      if (U > 0) k_sp_contribs<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, keys_in, vals_in);
+      if (n > 0) {
+        size_t b = sort_tmp_.cap;
+        COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, kb, s));
+        b = sort_tmp_.cap;
+        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, len_it, epre + 1, int(n), s));
+      }
+      k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
+      sorted_early = true;
+    } else {
+      n_tot = n_freq;
+    }
+    k_rank_keys<<<nblocks(M, 256), 256, 0, s>>>(row_ptr, owner ? freq : nullptr, M, rk_in, ids);
+    size_t b = 0;
+    const int fb = bits_for(std::max<int64_t>(n_tot, 1) + 1);
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, rk_in, rk_out, ids, col_of, M, 0, fb, s));
+    COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, rk_in, rk_out, ids, col_of, M, 0, fb, s));
+    k_rank_scatter<<<nblocks(M, 256), 256, 0, s>>>(col_of, M, rank_of);
+    COOC_HIP_TRY(hipGetLastError());
+    freq_rank = reinterpret_cast<const int64_t *>(rk_out);
+  }
+  last_col_of_ = col_of;
+  last_rank_of_ = rank_of;
+  // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
   if (owner) {
     COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
     COOC_TRY(sp_ownoff_.reserve(sizeof(int64_t) * size_t(U1 + 1)));
@@ -1983,7 +2082,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(uint64_t), s));
   if (U > 0) {
     k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen, owner, part,
-                                                             sp_ownc_.as<int32_t>());
+                                                             sp_ownc_.as<int32_t>(), rank_of);
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
   }
@@ -2002,7 +2101,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   if (U > 0) {
     k_sp_tile_lists<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_tb_.as<int32_t>(),
                                                             sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), pbase,
-                                                            win ? nullptr : keys_in, vals_in, owner, part, ownoff, tot);
+                                                            (win || sorted_early) ? nullptr : keys_in, vals_in, owner,
+                                                            part, ownoff, tot, rank_of);
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
@@ -2019,7 +2119,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   }
   SPT("partition");
   // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152); 3. row pointer; 4. pair work
-  if (n_c > 0) {
+  if (n_c > 0 && !sorted_early) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n_c), 0, kb, s));
     b = sort_tmp_.cap;
@@ -2040,11 +2140,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     }
   }
   SPT("sort+scan");
-  k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n_c, M, row_ptr);
+  if (!sorted_early) k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n_c, M, row_ptr);
   // 5. expected distinct keys per tile; 6. per-row plan
-  // column frequencies: of this log's interactions (owner == NULL), else the caller's global counts
+  // column frequencies: of this log's interactions (owner == NULL), else the caller's global counts; in rank
+  // order after a relabel
   const int64_t n_est = freq ? n_freq : win ? n_c : n;
-  if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, freq, M, n_est, est, gmass);
+  if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, relabel ? freq_rank : freq, M, n_est, est, gmass);
   else COOC_HIP_TRY(hipMemsetAsync(est, 0, sizeof(float) * (T * kEstK + T), s));
   SPT("est");
   k_sp_plan<<<nblocks(M, 256), 256, 0, s>>>(M, T, row_ptr, epre, est, gmass, rowsum_.as<int64_t>(),
@@ -2164,6 +2265,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sp_defer_.reserve(sizeof(int32_t) * size_t(M)));
   proto.deferred = sp_defer_.as<int32_t>();
   proto.sort_all = sort_rows_ ? 1 : 0;
+  proto.col_of = col_of;
+  proto.rank_of = rank_of;
   int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
@@ -2230,7 +2333,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       k_sp_split_finalize<<<unsigned(n_split), kFinThreads, 0, s>>>(
           split_row_.as<int32_t>(), staging_.as<uint32_t>(), sstride, M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
           cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-          tot, spre);
+          tot, spre, col_of, rank_of);
       COOC_HIP_TRY(hipGetLastError());
     }
   SPT("finalize");
@@ -2300,6 +2403,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   out->cnt = cnt_.as<uint32_t>();
   out->dense = nullptr;
   out->rowsum = rowsum_.as<int64_t>();
+  out->rank_of = rank_of;
   out->work = work_total;
   out->observed = work_total - self_total;  // ordered pairs of the counted rows
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
@@ -2374,7 +2478,7 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
       k_sr_emit<<<unsigned(nb), kSrThreads, 0, s>>>(rows + j0, rstart, ukeys, ucnt, row_ptr, spre, rowsum_.as<int64_t>(),
                                                     col_.as<int32_t>(), cnt_.as<uint32_t>(), bump_.as<unsigned long long>(),
                                                     cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-                                                    tot_.as<PlanTotals>());
+                                                    tot_.as<PlanTotals>(), last_col_of_, last_rank_of_);
       COOC_HIP_TRY(hipGetLastError());
       // kb (host) is reused by the next batch's upload: the copy must have been consumed
       COOC_HIP_TRY(hipStreamSynchronize(s));

@@ -4,7 +4,9 @@
 // of a global row must equal the item's row sum (ItemRowRescorer...java:183-193).  These kernels run
 // that check, and the ones the CSR contract adds, over a whole cooc_count_device result in HBM:
 //   * sum over the row's counts == rowsum[a] (the closed form W_a - c_a the planner wrote),
-//   * columns strictly ascending within a row and inside [0, n_items), every stored count > 0
+//   * columns strictly ascending within a row (in the result's column order: ascending rank_of[col] after the
+//     large-universe path's frequency relabel, else ascending id) and inside [0, n_items), every stored
+//     count > 0
 //     (a key exists iff it was touched: every increment is +1, ItemRowAggregator.java:29),
 //   * optionally C[a, b] == C[b, a] for every entry (the ordered pairs of a user are symmetric),
 // and write a per-row fingerprint, sum over the row's keys of splitmix64(col << 32 ^ count) mod 2^64,
@@ -37,6 +39,7 @@ __device__ inline uint64_t wave_sum(uint64_t v) {
 __global__ __launch_bounds__(256) void k_verify_csr(int32_t M, const int64_t *__restrict__ row_base,
                                                     const int32_t *__restrict__ row_nnz, const int32_t *__restrict__ col,
                                                     const uint32_t *__restrict__ cnt, const int64_t *__restrict__ rowsum,
+                                                    const int32_t *__restrict__ rank_of,
                                                     uint64_t *__restrict__ cs_out, unsigned long long *__restrict__ tot) {
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -50,7 +53,11 @@ __global__ __launch_bounds__(256) void k_verify_csr(int32_t M, const int64_t *__
       const uint32_t v = cnt[b + i];
       h += row_key_hash(c, v);
       s += v;
-      const bool ok = c >= 0 && c < M && v > 0u && (i + 1 == n || col[b + i + 1] > c);
+      bool ok = c >= 0 && c < M && v > 0u;
+      if (ok && i + 1 < n) {
+        const int32_t c1 = col[b + i + 1];
+        ok = rank_of ? (c1 >= 0 && c1 < M && rank_of[c1] > rank_of[c]) : c1 > c;
+      }
       bad += ok ? 0u : 1u;
     }
     h = wave_sum(h);
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(256) void k_verify_symmetry(int32_t M, const int64_
                                                          const int32_t *__restrict__ row_nnz,
                                                          const int32_t *__restrict__ col,
                                                          const uint32_t *__restrict__ cnt,
+                                                         const int32_t *__restrict__ rank_of,
                                                          unsigned long long *__restrict__ tot) {
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -138,10 +146,13 @@ __global__ __launch_bounds__(256) void k_verify_symmetry(int32_t M, const int64_
       }
       const int32_t nb = row_nnz[b];
       const int64_t bb = nb > 0 ? row_base[b] : 0;
+      // (rows are sorted in the result's column order, k_verify_csr checks that)
+      const int32_t ka = rank_of ? rank_of[a] : int32_t(a);
       int32_t lo = 0, hi = nb;
       while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
-        if (col[bb + mid] < int32_t(a)) lo = mid + 1; else hi = mid;
+        const int32_t cm = col[bb + mid];
+        if ((rank_of ? rank_of[cm] : cm) < ka) lo = mid + 1; else hi = mid;
       }
       bad += !(lo < nb && col[bb + lo] == int32_t(a) && cnt[bb + lo] == v);
     }
@@ -160,8 +171,8 @@ Status launch_verify(hipStream_t s, int32_t M, const CountResult &r, bool symmet
   if (r.dense) {
     k_verify_dense<<<grid, 256, 0, s>>>(M, r.dense, r.row_nnz, r.rowsum, d_cs, d_tot);
   } else {
-    k_verify_csr<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, d_cs, d_tot);
-    if (symmetry) k_verify_symmetry<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, d_tot);
+    k_verify_csr<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, r.rank_of, d_cs, d_tot);
+    if (symmetry) k_verify_symmetry<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rank_of, d_tot);
   }
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();

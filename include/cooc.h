@@ -83,6 +83,14 @@ enum cooc_status {
  * pair keys, radix-sorted, runs counted) instead of the LDS hash / dense-tile chunks.  That path always
  * takes the rows whose LDS hash table overflows; the flag sends all of them (A/B and tests). */
 #define COOC_FLAG_SORT_ROWS 16
+/* Large universes, batch windows: keep the columns of a row in ascending id order.  By default the
+ * large-universe path numbers the columns of a batch by descending frequency (that batch's item counts, or
+ * the global counts of cooc_count_device_owned; ties: the smaller id first) so that its tiling works
+ * whatever order the ids come in, and a device result's rows are in THAT order -- which is also the order
+ * the rescorer scores them in (the top-k tie order).  The host copies (cooc_copy_batch) are always in
+ * ascending column order.  This flag restores id order on the device at the price of the relabel's gain
+ * (ids not numbered by popularity run up to ~1.8x slower). */
+#define COOC_FLAG_COLUMN_ORDER 32
 
 typedef struct cooc_ctx cooc_ctx;
 
@@ -124,7 +132,9 @@ typedef struct cooc_device_result {
   int64_t observed;       /* exact ordered pairs sum_u n_u (n_u - 1) */
   const int64_t *row_base;  /* [n_items]: first entry of row a in col/cnt (rows padded, not packed) */
   const int32_t *row_nnz;   /* [n_items]: entries of row a (both layouts) */
-  const int32_t *col;       /* ascending within a row */
+  const int32_t *col;       /* ascending within a row in the result's column order: column id, or, for a
+                               large-universe batch (n_items >= 40,320 without COOC_FLAG_COLUMN_ORDER),
+                               descending batch frequency of the column (ties: smaller id first) */
   const uint32_t *cnt;      /* exact counts */
   const int64_t *rowsum;    /* [n_items]: exact row sums sum_b C[a,b] */
   const uint32_t *dense;    /* [n_items * n_items] row-major exact counts, 0 = key absent */
@@ -169,6 +179,10 @@ COOC_API int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64
  * contended global atomics on them. */
 COOC_API int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactions, int64_t *d_counts,
                               void *hip_stream);
+/* The column order of the last batch result's device rows (and of its top-k iteration, the tie order):
+ * rank_of int32[n_items] gets the position of every column in that order -- its rank by descending batch
+ * frequency after the large-universe relabel, else the column id itself (see COOC_FLAG_COLUMN_ORDER). */
+COOC_API int cooc_copy_column_order(cooc_ctx *ctx, int32_t *rank_of);
 /* Same from host buffers; afterwards cooc_copy_batch copies the packed CSR out. */
 COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
                     cooc_window_info *info);

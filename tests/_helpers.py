@@ -125,11 +125,16 @@ def assert_topk_equal(got, want, rtol=1e-6):
             assert set(gv[gs > kth + margin].tolist()) == set(wv[ws > kth + margin].tolist())
 
 
-def oracle_row_topk(oracle, cols, cnt16, rs32, a: int, k: int, observed: int):
-    """The rescorer's heap for row a (ItemRowRescorer...java:195-223) fed in ascending column order
-    with the reference's views: int16 counts, int32 row sums, observed = sum of the int32 row sums."""
+def oracle_row_topk(oracle, cols, cnt16, rs32, a: int, k: int, observed: int, order=None):
+    """The rescorer's heap for row a (ItemRowRescorer...java:195-223) fed in the device's column order --
+    ascending order[col] (CooccurrenceCore.column_order(); None: ascending column id) -- with the
+    reference's views: int16 counts, int32 row sums, observed = sum of the int32 row sums."""
     q = oracle.PriorityQueue(k)
-    for b, c16 in zip(np.asarray(cols).tolist(), np.asarray(cnt16).tolist()):
+    cols, cnt16 = np.asarray(cols), np.asarray(cnt16)
+    if order is not None:
+        o = np.argsort(np.asarray(order)[cols], kind="stable")
+        cols, cnt16 = cols[o], cnt16[o]
+    for b, c16 in zip(cols.tolist(), cnt16.tolist()):
         sc = oracle.score_item(int(c16), int(rs32[a]), int(rs32[b]), observed)
         if q.size() < k:
             q.add(b, sc)

@@ -9,7 +9,9 @@ key count, count sum; oracle.RowChecks restates the same):
   restatements, ItemRowAggregator.java:26-31), plus the symmetry of every entry;
 * 1/64 (~4.2e9 pairs) and the benchmark's own workload, 1/8 of C3 (1.25e6 users, 3.36e10 pairs, what
   bench.py times), against the closed-form restatement (oracle.row_checksums; it agrees with the
-  record-by-record one and with scipy in tests/test_oracle_semantics.py).
+  record-by-record one and with scipy in tests/test_oracle_semantics.py);
+* the same log with its item ids permuted (datagen.c3_item_perm: ids carry no popularity order), at 1/256
+  and at the benchmark's 1/8 (bench.py --permute-items).
 
 Bar: bit-exact (every row's fingerprint, key count and count sum equal), plus the device-side
 invariants (sum of counts == sum of row sums == P, sorted rows, no zero count).  Needs an MI355X.
@@ -61,12 +63,13 @@ def _compare(res, chk, cs, nnz, want, P):
     assert len(bad) == 0, f"{len(bad)} rows differ from the oracle, e.g. {bad[:10].tolist()}"
 
 
-def test_c3_256th_every_row_vs_record_by_record_oracle(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("permute", [False, True])
+def test_c3_256th_every_row_vs_record_by_record_oracle(pkg, oracle, torch_cuda, permute):
     torch = torch_cuda
     from flink_cooccurrence_amd import datagen
 
     U, M = datagen.C3_USERS // 256, datagen.C3_ITEMS
-    up, it = datagen.c3_users(0, U)
+    up, it = datagen.c3_users(0, U, permute=permute)
     dev = torch.device("cuda", 0)
     res, chk, cs, nnz = _device_checks(pkg, torch, torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev), M,
                                        symmetry=True)
@@ -75,15 +78,15 @@ def test_c3_256th_every_row_vs_record_by_record_oracle(pkg, oracle, torch_cuda):
     _compare(res, chk, cs, nnz, want, datagen.ordered_pairs(up))
 
 
-@pytest.mark.parametrize("share", [64, 8])
-def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share):
+@pytest.mark.parametrize("share,permute", [(64, False), (8, False), (8, True)])
+def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share, permute):
     """share = 8 is the benchmark's workload (bench.py, N = 1): users [0, 1.25e6) of the 1B log."""
     torch = torch_cuda
     from flink_cooccurrence_amd import datagen
 
     U, M = datagen.C3_USERS // share, datagen.C3_ITEMS
     dev = torch.device("cuda", 0)
-    up_d, it_d = datagen.c3_users(0, U, device=dev)
+    up_d, it_d = datagen.c3_users(0, U, device=dev, permute=permute)
     res, chk, cs, nnz = _device_checks(pkg, torch, up_d, it_d, M, symmetry=share >= 64)
     if share >= 64:
         assert chk["asymmetric_entries"] == 0

@@ -43,8 +43,12 @@ class _Rows:
         self.rowsum = _d2h(res.rowsum, M, np.int64)
 
     def row(self, a):
+        """Row a in ascending column order (the device row's own order -- descending batch frequency after
+        the large-universe relabel -- is checked by cooc_verify_batch)."""
         n, b = int(self.nnz[a]), int(self.base[a])
-        return _d2h(self.res.col, n, np.int32, b), _d2h(self.res.cnt, n, np.uint32, b).astype(np.int64)
+        c, v = _d2h(self.res.col, n, np.int32, b), _d2h(self.res.cnt, n, np.uint32, b).astype(np.int64)
+        o = np.argsort(c, kind="stable")
+        return c[o], v[o]
 
 
 class _Brute:
@@ -232,10 +236,11 @@ def test_c5_topk_c3_shape_vs_oracle(pkg, oracle, torch_cuda):
         sizes, vals, scores = core.topk_items(sample, k)
         empty = np.setdiff1d(np.arange(0, M, 9973), rows)[:5]
         esz, _, _ = core.topk_items(empty, k)
+        order = core.column_order()  # the device rows' column order (descending frequency): the tie order
     assert np.all(esz == 0)
     for i, a in enumerate(sample.tolist()):
         s, e = got.row_ptr[a], got.row_ptr[a + 1]
-        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed)
+        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed, order)
         assert_row_topk(sizes[i], vals[i], scores[i], want, where=f"row {a}")
 
 
@@ -427,9 +432,10 @@ def test_c5_topk_long_rows_vs_oracle(pkg, oracle, torch_cuda):
         sz, v, sc = sz.cpu().numpy(), v.cpu().numpy(), sc.cpu().numpy()
         sample = np.array([0, 1, 2, 500, 20_001, 44_999], np.int64)
         s_sz, s_v, s_sc = core.topk_items(sample, k)
+        order = core.column_order()
     for i, a in enumerate(sample.tolist()):
         s, e = got.row_ptr[a], got.row_ptr[a + 1]
-        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed)
+        want = oracle_row_topk(oracle, got.cols[s:e], got.cnt16[s:e], rs32, a, k, observed, order)
         assert_row_topk(sz[a], v[a], sc[a], want, where=f"batch row {a}")
         assert_row_topk(s_sz[i], s_v[i], s_sc[i], want, where=f"sampled row {a}")
         n = int(sz[a])
