@@ -124,8 +124,8 @@ struct CountResult {
   uint32_t *cnt = nullptr;
   int64_t *rowsum = nullptr;
   uint32_t *dense = nullptr;  // dense output: row-major [M x M] counts (row_base / col / cnt unused)
-  // the column order of the rows: ascending rank_of[col] (the large-universe batch path numbers the columns
-  // by descending frequency); NULL = ascending column id
+  // the column order of the rows: ascending rank_of[col] (the large-universe batch path puts the batch's
+  // 16,384 most frequent items first, then the rest, each group by id); NULL = ascending column id
   const int32_t *rank_of = nullptr;
   int64_t nnz = 0;
   int64_t observed = 0;  // ordered pairs of the run
@@ -186,7 +186,7 @@ class Counter {
   // path (otherwise only rows whose LDS hash table overflowed); rows and pairs it took in the last run
   void set_sort_rows(bool on) { sort_rows_ = on; }
   void set_relabel(bool on) { relabel_ = on; }
-  const int32_t *last_rank_of() const { return last_rank_of_; }
+  const int32_t *last_rank_of() const { return last_pos_of_; }
   int64_t last_deferred_rows() const { return last_deferred_; }
   int64_t last_deferred_pairs() const { return last_deferred_pairs_; }
   static constexpr int32_t kBatchMaxItems = 40320;
@@ -243,7 +243,7 @@ class Counter {
   // COOC_FLAG_COLUMN_ORDER); the last run's maps (NULL without a relabel)
   bool relabel_ = true;
   DevBuf sp_rank_, sp_rkeys_;
-  const int32_t *last_col_of_ = nullptr, *last_rank_of_ = nullptr;
+  const int32_t *last_hot_col_ = nullptr, *last_pos_of_ = nullptr;
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
                       const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;

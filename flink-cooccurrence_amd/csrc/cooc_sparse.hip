@@ -144,16 +144,22 @@ struct SpArgs {
   const int64_t *spre;      // streaming window: [n_contrib + 1] prefix of the kSelfBit flags; NULL: all set
   int32_t *deferred;        // [M] whole rows left to the sort + segmented-reduce path (k_sr_*), in tot->n_deferred
   int32_t sort_all;         // COOC_FLAG_SORT_ROWS: every whole row goes to that path (A/B and tests)
-  // column relabel (batch windows): the kernels work in frequency-rank space -- column k of the arenas,
-  // tiles, tables and staging rows is the item of rank k -- and write col_of[k] to the output.
-  // NULL: identity (streaming windows)
-  const int32_t *col_of;    // [M] rank -> item id
-  const int32_t *rank_of;   // [M] item id -> rank
+  // column relabel (batch windows, k_relabel_*): the kernels work in relabelled column space -- tile 0 holds
+  // the batch's kTW most frequent items (hot_col[c], ascending ids), column c >= kTW the item c - kTW (its
+  // own id shifted one tile up; the hot items leave holes there) -- and write the item ids to the output.
+  // NULL: identity (streaming windows, and universes of at most one tile).
+  const int32_t *hot_col;   // [kTW] column < kTW -> item id
+  const int32_t *pos_of;    // [M] item id -> column
 };
 
-// the item of column rank r / the rank of item a (identity without a relabel)
-__device__ inline int32_t sp_col(const SpArgs &A, uint32_t r) { return A.col_of ? A.col_of[r] : int32_t(r); }
-__device__ inline int32_t sp_rank(const SpArgs &A, int32_t a) { return A.rank_of ? A.rank_of[a] : a; }
+// the item of relabelled column r: a table lookup in tile 0 (64 KB, cache resident), arithmetic above it
+__device__ inline int32_t relabel_col(const int32_t *hot_col, uint32_t r) {
+  if (!hot_col) return int32_t(r);
+  return r < uint32_t(kTW) ? hot_col[r] : int32_t(r) - kTW;
+}
+__device__ inline int32_t relabel_pos(const int32_t *pos_of, uint32_t a) { return pos_of ? pos_of[a] : int32_t(a); }
+__device__ inline int32_t sp_col(const SpArgs &A, uint32_t r) { return relabel_col(A.hot_col, r); }
+__device__ inline int32_t sp_rank(const SpArgs &A, int32_t a) { return relabel_pos(A.pos_of, uint32_t(a)); }
 
 #ifdef COOC_SP_TRACE
 #define PROG(A, k, v) do { if (threadIdx.x == 0) __hip_atomic_store((A).prog + blockIdx.x * 64 + (k), (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
@@ -272,7 +278,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t
       for (int k = 0; k < 4; k++) {  // (an invalid id goes to tile 0 in k_sp_tile_lists, which reports it)
         const bool in = p0 + 64 * k + lane < n;
         const bool valid = uint32_t(it[k]) < uint32_t(M);
-        const uint32_t rk = valid && rank_of ? uint32_t(rank_of[it[k]]) : uint32_t(it[k]);
+        const uint32_t rk = valid ? uint32_t(relabel_pos(rank_of, uint32_t(it[k]))) : uint32_t(it[k]);
         n0 += int32_t(__popcll(__ballot(in && (rk < uint32_t(kTW) || !valid))));
         if (owner) mine += int32_t(__popcll(__ballot(valid && owner[it[k]] == part)));
       }
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
     for (int k = 0; k < kTlR; k++) {
       valid[k] = uint32_t(r[k]) < uint32_t(M);
       if (!valid[k]) r[k] = 0;
-      rk[k] = rank_of && lane + 64 * k < n ? rank_of[r[k]] : r[k];
+      rk[k] = lane + 64 * k < n ? relabel_pos(rank_of, uint32_t(r[k])) : r[k];
     }
 #pragma unroll
     for (int k = 0; k < kTlR; k++) count(lane + 64 * k < n, lane + 64 * k, r[k], rk[k], valid[k]);
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
         bad = true;
         it = 0;
       }
-      count(p < n, p, it, rank_of && p < n ? rank_of[it] : it, v);
+      count(p < n, p, it, p < n ? relabel_pos(rank_of, uint32_t(it)) : it, v);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -418,7 +424,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
       const int32_t p = p0 + lane;
       int32_t it = p < n ? items[s + p] : 0;
       if (uint32_t(it) >= uint32_t(M)) it = 0;
-      place(p < n, rank_of && p < n ? rank_of[it] : it);
+      place(p < n, p < n ? relabel_pos(rank_of, uint32_t(it)) : it);
     }
     if (lane < ((n0 + 7) & ~7) - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
     if (lane < ((n1 + 3) & ~3) - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
@@ -479,20 +485,48 @@ __global__ __launch_bounds__(256) void k_sp_contribs(int64_t U, const int64_t *_
   }
 }
 
-// Column relabel: sort keys = the items' frequencies (the row lengths of the item-sorted contributions, or
-// the caller's global counts), values = the ids; a stable descending sort then gives col_of (rank -> id,
-// ties: the smaller id first), and k_rank_scatter its inverse.
+// Column relabel: the kTW most frequent items of the batch (its own frequencies -- the row lengths of the
+// item-sorted contributions -- or the caller's global counts; ties: the smaller id first) become tile 0, in
+// ascending id order; every other item keeps its id shifted one tile up.  So tile 0 (u16 arena, dense LDS
+// tiles) holds the Zipf head whatever order the ids come in, and a column maps back to its item by a lookup
+// in a 64 KB table (tile 0) or a subtraction (above).
 __global__ void k_rank_keys(const int64_t *__restrict__ row_ptr, const int64_t *__restrict__ freq, int32_t M,
-                            uint64_t *__restrict__ keys, int32_t *__restrict__ ids) {
+                            uint64_t *__restrict__ keys, int32_t *__restrict__ ids, uint8_t *__restrict__ hot) {
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= M) return;
   keys[a] = uint64_t(freq ? freq[a] : row_ptr[a + 1] - row_ptr[a]);
   ids[a] = a;
+  hot[a] = 0;
 }
 
-__global__ void k_rank_scatter(const int32_t *__restrict__ col_of, int32_t M, int32_t *__restrict__ rank_of) {
+__global__ void k_hot_mark(const int32_t *__restrict__ order, int32_t h, uint8_t *__restrict__ hot) {
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < M) rank_of[col_of[r]] = r;
+  if (r < h) hot[order[r]] = 1;
+}
+
+struct IsHot {
+  const uint8_t *hot;
+  __host__ __device__ bool operator()(int32_t a) const { return hot[a] != 0; }
+};
+
+// pos_of (item -> column) and the frequencies in column order (the planner's per-tile estimate; the holes of
+// the hot items above tile 0 count 0)
+__global__ void k_relabel_pos(const uint8_t *__restrict__ hot, const uint64_t *__restrict__ freq_by_id, int32_t M,
+                              int32_t *__restrict__ pos_of, int64_t *__restrict__ freq_col) {
+  const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= M) return;
+  const bool h = hot[a] != 0;
+  if (!h) pos_of[a] = a + kTW;
+  freq_col[kTW + a] = h ? 0 : int64_t(freq_by_id[a]);
+}
+
+__global__ void k_relabel_hot(const int32_t *__restrict__ hot_col, const uint64_t *__restrict__ freq_by_id,
+                              int32_t *__restrict__ pos_of, int64_t *__restrict__ freq_col) {
+  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= kTW) return;
+  const int32_t a = hot_col[c];
+  pos_of[a] = c;
+  freq_col[c] = int64_t(freq_by_id[a]);
 }
 
 struct WidenCount {
@@ -1097,10 +1131,21 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
     off += wv < wave ? x : 0u;
     tot += x;
   }
+  // after a relabel the output ids of tile 0 are hot_col[b]: 16-B loads of the lane's 4 ids, two steps ahead
+  // (their latency overlaps the reservation and the steps before); above tile 0 they are c0 + b - kTW
+  const bool map = A.hot_col != nullptr && c0 == 0;
+  auto colq = [&](int32_t b) -> uint4 {
+    return (map && b < hi) ? *reinterpret_cast<const uint4 *>(A.hot_col + b) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  uint4 q0 = colq(lo + 4 * lane), q1 = colq(lo + 256 + 4 * lane);
   const int64_t base = sp_reserve(A, S_, tot);  // (barrier: every wave has read wtot)
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int32_t b0 = lo; b0 < hi; b0 += 256) {
     const int32_t b = b0 + 4 * lane;
+    const uint4 qc = q0;
+    q0 = q1;
+    q1 = colq(b0 + 512 + 4 * lane);
+    const uint32_t ids[4] = {qc.x, qc.y, qc.z, qc.w};
     uint32_t v[4];
     load(b, v);
     const uint32_t c = (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
@@ -1115,7 +1160,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
         if (!v[k]) continue;
         if (base >= 0) {
           if (BCHK(A, pos >= 0 && pos < A.cap, 64)) {
-            A.col_out[pos] = sp_col(A, uint32_t(c0 + b + k));
+            A.col_out[pos] = map ? int32_t(ids[k]) : c0 + b + k - (A.hot_col ? kTW : 0);
             A.cnt_out[pos] = v[k];
           }
         }
@@ -1223,13 +1268,36 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     // and count areas), then leave in order: 16-B stores of whole column / count runs instead of one
     // scattered 4-B store per entry and array
     uint32_t *sc = keys + kWStage, *sn = cnts + kWStage;
+    if (!A.hot_col || c0 >= kTW) {
+      // (above tile 0 a relabelled column maps back by a subtraction)
+      const uint32_t base_id = uint32_t(c0) - (A.hot_col ? uint32_t(kTW) : 0u);
 #pragma unroll
-    for (int i = 0; i < kHashMax / kSpThreads; i++) {
-      if (ek[i] == ~0u) continue;
-      const uint32_t col = ek[i], r = er[i];
-      const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
-      sc[q] = uint32_t(sp_col(A, uint32_t(c0) + col));
-      sn[q] = ec[i];
+      for (int i = 0; i < kHashMax / kSpThreads; i++) {
+        if (ek[i] == ~0u) continue;
+        const uint32_t col = ek[i], r = er[i];
+        const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
+        sc[q] = base_id + col;
+        sn[q] = ec[i];
+      }
+    } else {
+      // a chunk over tile 0 after a relabel: every entry's sorted position (er), then the hot_col loads of its
+      // tile-0 entries issued back to back (ek is free once the position is known), then the LDS stores
+#pragma unroll
+      for (int i = 0; i < kHashMax / kSpThreads; i++) {
+        if (ek[i] == ~0u) continue;
+        const uint32_t col = ek[i], r = er[i];
+        er[i] = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
+        ek[i] = uint32_t(c0) + col;
+      }
+#pragma unroll
+      for (int i = 0; i < kHashMax / kSpThreads; i++)
+        if (ec[i]) ek[i] = ek[i] < uint32_t(kTW) ? uint32_t(A.hot_col[ek[i]]) : ek[i] - uint32_t(kTW);
+#pragma unroll
+      for (int i = 0; i < kHashMax / kSpThreads; i++) {
+        if (!ec[i]) continue;
+        sc[er[i]] = ek[i];
+        sn[er[i]] = ec[i];
+      }
     }
     __syncthreads();
     const uint32_t head = min(ne, uint32_t((4 - (base & 3)) & 3));  // entries before the first 16-B boundary
@@ -1534,15 +1602,15 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
                                                                     int32_t *__restrict__ row_nnz,
                                                                     PlanTotals *__restrict__ tot,
                                                                     const int64_t *__restrict__ spre,
-                                                                    const int32_t *__restrict__ col_of,
-                                                                    const int32_t *__restrict__ rank_of) {
+                                                                    const int32_t *__restrict__ hot_col,
+                                                                    const int32_t *__restrict__ pos_of) {
   __shared__ uint32_t s_w[kFinWaves];
   __shared__ uint64_t s_red[kFinWaves];
   __shared__ int64_t s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t s = blockIdx.x;
   const int32_t a = split_row[s];
-  const int32_t ra = rank_of ? rank_of[a] : a;  // staging rows are in column-rank space
+  const int32_t ra = relabel_pos(pos_of, uint32_t(a));  // staging rows are in relabelled column space
   const uint32_t self = uint32_t(spre ? spre[row_ptr[a + 1]] - spre[row_ptr[a]] : row_ptr[a + 1] - row_ptr[a]);
   const uint32_t *row = staging + int64_t(s) * stride;
   constexpr int32_t kStep = 64 * 4 * kFinU;  // columns per wave step
@@ -1616,7 +1684,7 @@ __global__ __launch_bounds__(kFinThreads) void k_sp_split_finalize(const int32_t
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (v[u][k]) {
-          col_out[pos] = col_of ? col_of[b + k] : b + k;
+          col_out[pos] = relabel_col(hot_col, uint32_t(b + k));
           cnt_out[pos] = v[u][k];
           pos++;
         }
@@ -1708,13 +1776,13 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
                                                         int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
                                                         unsigned long long *__restrict__ bump, int64_t cap,
                                                         int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
-                                                        PlanTotals *__restrict__ tot, const int32_t *__restrict__ col_of,
-                                                        const int32_t *__restrict__ rank_of) {
+                                                        PlanTotals *__restrict__ tot, const int32_t *__restrict__ hot_col,
+                                                        const int32_t *__restrict__ pos_of) {
   __shared__ int64_t s_diag, s_base;
   __shared__ unsigned long long s_sum;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int32_t a = rows[j];
-  const uint32_t ra = uint32_t(rank_of ? rank_of[a] : a);  // the keys' columns are ranks
+  const uint32_t ra = uint32_t(relabel_pos(pos_of, uint32_t(a)));  // the keys' columns are relabelled
   const int64_t r0 = rstart[j], r1 = rstart[j + 1];
   const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1];
   const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
@@ -1755,7 +1823,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
   for (int64_t r = r0 + tid; r < r1; r += kSrThreads) {
     if (drop && r == diag) continue;
     const int64_t q = base + (r - r0) - (drop && r > diag ? 1 : 0);
-    col_out[q] = col_of ? col_of[uint32_t(ukeys[r])] : int32_t(uint32_t(ukeys[r]));
+    col_out[q] = relabel_col(hot_col, uint32_t(ukeys[r]));
     cnt_out[q] = ucnt[r] - (r == diag ? self : 0u);
   }
 }
@@ -1930,25 +1998,43 @@ int bits_for(int64_t v) {
 
 namespace {
 
-// Item frequencies of a log (the multi-GPU owner map and the planner's column estimate): ids below
-// kHistLds are counted in LDS (Zipf ranks: the hot ids; no contended global atomics), the rest with
-// global 64-bit atomics (each such bin is cold); the LDS bins are flushed once per workgroup.
-constexpr int kHistLds = 16384;
-__global__ __launch_bounds__(1024) void k_item_counts(const int32_t *__restrict__ items, int64_t n, int32_t M,
-                                                      unsigned long long *__restrict__ counts) {
-  __shared__ uint32_t h[kHistLds];
-  for (int i = threadIdx.x; i < kHistLds; i += 1024) h[i] = 0u;
-  __syncthreads();
-  const uint32_t hot = uint32_t(min(M, kHistLds));
-  const int64_t stride = int64_t(gridDim.x) * 1024;
-  for (int64_t i = int64_t(blockIdx.x) * 1024 + threadIdx.x; i < n; i += stride) {
-    const uint32_t it = uint32_t(items[i]);
-    if (it < hot) atomicAdd(&h[it], 1u);
-    else if (it < uint32_t(M)) atomicAdd(counts + it, 1ull);
+// Item frequencies of a log (the multi-GPU owner map and the planner's column estimate).  Zipf logs put most
+// interactions on a few items, whose global counters would serialise at L2 under per-interaction atomics;
+// each workgroup therefore keeps the items it sees most in an LDS table (open addressing: an item claims a
+// slot with a compare-and-swap, kHistProbe probes at most) and flushes it once; an item that finds no slot
+// (the table is full of the workgroup's earlier items) goes to a global 64-bit atomic -- such items are rare
+// in the workgroup's share, so their counters are not contended.  Whatever order the ids come in.
+constexpr int kHistSlots = 8192, kHistProbe = 8, kHistThreads = 1024;
+__global__ __launch_bounds__(kHistThreads) void k_item_counts(const int32_t *__restrict__ items, int64_t n, int32_t M,
+                                                              unsigned long long *__restrict__ counts) {
+  __shared__ uint32_t hk[kHistSlots], hc[kHistSlots];
+  for (int i = threadIdx.x; i < kHistSlots; i += kHistThreads) {
+    hk[i] = 0u;
+    hc[i] = 0u;
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < hot; b += 1024)
-    if (h[b]) atomicAdd(counts + b, (unsigned long long)h[b]);
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;  // a contiguous share per workgroup
+  const int64_t i0 = int64_t(blockIdx.x) * per, i1 = min(n, i0 + per);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += kHistThreads) {
+    const uint32_t it = uint32_t(items[i]);
+    if (it >= uint32_t(M)) continue;
+    const uint32_t key = it + 1u;
+    uint32_t h = (it * 0x9E3779B1u) >> (32 - 13);
+    bool done = false;
+    for (int p = 0; p < kHistProbe; p++) {
+      const uint32_t cur = atomicCAS(hk + h, 0u, key);
+      if (cur == 0u || cur == key) {
+        atomicAdd(hc + h, 1u);
+        done = true;
+        break;
+      }
+      h = (h + 1u) & (kHistSlots - 1u);
+    }
+    if (!done) atomicAdd(counts + it, 1ull);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHistSlots; i += kHistThreads)
+    if (hk[i]) atomicAdd(counts + (hk[i] - 1u), (unsigned long long)hc[i]);
 }
 }  // namespace
 
@@ -1958,8 +2044,8 @@ Status launch_item_counts(hipStream_t s, const int32_t *items, int64_t n, int32_
     int dev = 0, n_cu = 256;
     COOC_HIP_TRY(hipGetDevice(&dev));
     COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    const int64_t want = (n + 1023) / 1024;
-    k_item_counts<<<unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 2))), 1024, 0, s>>>(
+    const int64_t want = (n + 4095) / 4096;
+    k_item_counts<<<unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 2))), kHistThreads, 0, s>>>(
         items, n, M, reinterpret_cast<unsigned long long *>(counts));
     COOC_HIP_TRY(hipGetLastError());
   }
@@ -1970,7 +2056,14 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                            CountResult *out, KernelTimer *timer, const int32_t *owner, int32_t part,
                            const int64_t *freq, int64_t n_freq, const SparseWindow *win) {
   const int32_t M = M_;
-  const int32_t T = int32_t((int64_t(M) + kTW - 1) / kTW);
+  // 0. column relabel (batch windows; not streaming ones, whose delta rows merge into column-ordered global
+  // rows): the batch's kTW most frequent items -- its own frequencies, or the caller's global counts -- become
+  // tile 0 and the rest move one tile up (k_relabel_*), so that the hot columns fill the u16 tile 0 and the
+  // tiling works whatever order the ids come in.  Rows come out in that column order (CountResult.rank_of).
+  // Mc: the columns of the relabelled space (M + kTW; holes where the hot items were).
+  const bool relabel = relabel_ && !win && M > kTW && int64_t(M) + kTW <= int64_t(kSpMaxTiles) * kTW;
+  const int32_t Mc = relabel ? M + kTW : M;
+  const int32_t T = int32_t((int64_t(Mc) + kTW - 1) / kTW);
   if (T > kSpMaxTiles)
     return Status{1, "n_items > " + std::to_string(int64_t(kSpMaxTiles) * kTW) + " is not supported"};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
@@ -2032,21 +2125,18 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sort_tmp_.reserve(tmp));
 
   const int64_t waves = std::min<int64_t>(std::max<int64_t>(U, 1), 65536);
-  // 0. column relabel (batch windows; not streaming ones, whose delta rows merge into column-ordered global
-  // rows): columns are numbered by descending frequency -- the frequencies of this log, or the caller's
-  // global counts -- so that the hot columns fill the u16 tile 0 and the tiles' masses fall monotonically,
-  // whatever order the ids come in.  Rows come out in that column order (CountResult.rank_of).
-  const bool relabel = relabel_ && !win;
-  int32_t *col_of = nullptr, *rank_of = nullptr;
-  const int64_t *freq_rank = nullptr;  // the frequencies in rank order (the planner's column estimate)
-  bool sorted_early = false;           // contributions sorted ahead of the relabel (no owner)
+  int32_t *hot_col = nullptr, *pos_of = nullptr;
+  const int64_t *freq_col = nullptr;  // the frequencies in relabelled column order (the planner's estimate)
+  bool sorted_early = false;          // contributions sorted ahead of the relabel (no owner)
   if (relabel) {
-    COOC_TRY(sp_rank_.reserve(sizeof(int32_t) * size_t(3 * M)));
-    COOC_TRY(sp_rkeys_.reserve(sizeof(uint64_t) * size_t(2 * M)));
-    col_of = sp_rank_.as<int32_t>();
-    rank_of = col_of + M;
-    int32_t *ids = rank_of + M;
+    COOC_TRY(sp_rank_.reserve(sizeof(int32_t) * size_t(3 * M + kTW + 8) + size_t(M)));
+    COOC_TRY(sp_rkeys_.reserve(sizeof(uint64_t) * size_t(2 * M) + sizeof(int64_t) * size_t(Mc)));
+    pos_of = sp_rank_.as<int32_t>();
+    hot_col = pos_of + M;
+    int32_t *ids = hot_col + kTW, *order = ids + M, *n_sel = order + M;
+    uint8_t *hot = reinterpret_cast<uint8_t *>(n_sel + 8);
     uint64_t *rk_in = sp_rkeys_.as<uint64_t>(), *rk_out = rk_in + M;
+    int64_t *fc = reinterpret_cast<int64_t *>(rk_out + M);
     int64_t n_tot = n;
     if (!owner) {  // the log's own frequencies: the row lengths of the item-sorted contributions
       if (U > 0) k_sp_contribs<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, keys_in, vals_in);
@@ -2061,19 +2151,25 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     } else {
       n_tot = n_freq;
     }
-    k_rank_keys<<<nblocks(M, 256), 256, 0, s>>>(row_ptr, owner ? freq : nullptr, M, rk_in, ids);
-    size_t b = 0;
+    k_rank_keys<<<nblocks(M, 256), 256, 0, s>>>(row_ptr, owner ? freq : nullptr, M, rk_in, ids, hot);
+    size_t b = 0, b2 = 0;
     const int fb = bits_for(std::max<int64_t>(n_tot, 1) + 1);
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, rk_in, rk_out, ids, col_of, M, 0, fb, s));
-    COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, rk_in, rk_out, ids, order, M, 0, fb, s));
+    hipcub::CountingInputIterator<int32_t> from0(0);
+    COOC_HIP_TRY(hipcub::DeviceSelect::If(nullptr, b2, from0, hot_col, n_sel, M, IsHot{hot}, s));
+    COOC_TRY(sort_tmp_.reserve(std::max({b, b2, tmp})));
     b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, rk_in, rk_out, ids, col_of, M, 0, fb, s));
-    k_rank_scatter<<<nblocks(M, 256), 256, 0, s>>>(col_of, M, rank_of);
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, rk_in, rk_out, ids, order, M, 0, fb, s));
+    k_hot_mark<<<nblocks(kTW, 256), 256, 0, s>>>(order, kTW, hot);
+    b = sort_tmp_.cap;
+    COOC_HIP_TRY(hipcub::DeviceSelect::If(sort_tmp_.p, b, from0, hot_col, n_sel, M, IsHot{hot}, s));  // kTW of them
+    k_relabel_pos<<<nblocks(M, 256), 256, 0, s>>>(hot, rk_in, M, pos_of, fc);
+    k_relabel_hot<<<nblocks(kTW, 256), 256, 0, s>>>(hot_col, rk_in, pos_of, fc);
     COOC_HIP_TRY(hipGetLastError());
-    freq_rank = reinterpret_cast<const int64_t *>(rk_out);
+    freq_col = fc;
   }
-  last_col_of_ = col_of;
-  last_rank_of_ = rank_of;
+  last_hot_col_ = hot_col;
+  last_pos_of_ = pos_of;
   // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
   if (owner) {
     COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
@@ -2082,7 +2178,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(uint64_t), s));
   if (U > 0) {
     k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen, owner, part,
-                                                             sp_ownc_.as<int32_t>(), rank_of);
+                                                             sp_ownc_.as<int32_t>(), pos_of);
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
   }
@@ -2102,7 +2198,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     k_sp_tile_lists<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_tb_.as<int32_t>(),
                                                             sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), pbase,
                                                             (win || sorted_early) ? nullptr : keys_in, vals_in, owner,
-                                                            part, ownoff, tot, rank_of);
+                                                            part, ownoff, tot, pos_of);
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions
@@ -2145,7 +2241,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   // column frequencies: of this log's interactions (owner == NULL), else the caller's global counts; in rank
   // order after a relabel
   const int64_t n_est = freq ? n_freq : win ? n_c : n;
-  if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, relabel ? freq_rank : freq, M, n_est, est, gmass);
+  if (n_est > 0) k_sp_est<<<dim3(T, kEstK), 256, 0, s>>>(row_ptr, relabel ? freq_col : freq, Mc, n_est, est, gmass);
   else COOC_HIP_TRY(hipMemsetAsync(est, 0, sizeof(float) * (T * kEstK + T), s));
   SPT("est");
   k_sp_plan<<<nblocks(M, 256), 256, 0, s>>>(M, T, row_ptr, epre, est, gmass, rowsum_.as<int64_t>(),
@@ -2203,7 +2299,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipGetLastError());
   }
   SPT("queue");
-  const int64_t sstride = (int64_t(M) + 3) & ~int64_t(3);  // 16-B aligned staging rows
+  const int64_t sstride = (int64_t(Mc) + 3) & ~int64_t(3);  // 16-B aligned staging rows (relabelled columns)
   if (n_split > 0) {
     const size_t need = sizeof(uint32_t) * size_t(n_split) * size_t(sstride);
     COOC_TRY(staging_.reserve(need));
@@ -2252,7 +2348,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   proto.slab = slab;
   proto.row_base = row_base_.as<int64_t>();
   proto.row_nnz = row_nnz_.as<int32_t>();
-  proto.M = M;
+  proto.M = Mc;  // (k_sp_main's column range)
   proto.T = T;
   proto.n_contrib = n_c;
   proto.n_users = U;
@@ -2265,8 +2361,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sp_defer_.reserve(sizeof(int32_t) * size_t(M)));
   proto.deferred = sp_defer_.as<int32_t>();
   proto.sort_all = sort_rows_ ? 1 : 0;
-  proto.col_of = col_of;
-  proto.rank_of = rank_of;
+  proto.hot_col = hot_col;
+  proto.pos_of = pos_of;
   int64_t last_err = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     COOC_TRY(col_.reserve(sizeof(int32_t) * size_t(cap + 1)));
@@ -2331,9 +2427,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   SPT("main");
     if (n_split > 0) {
       k_sp_split_finalize<<<unsigned(n_split), kFinThreads, 0, s>>>(
-          split_row_.as<int32_t>(), staging_.as<uint32_t>(), sstride, M, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
+          split_row_.as<int32_t>(), staging_.as<uint32_t>(), sstride, Mc, row_ptr, rowsum_.as<int64_t>(), col_.as<int32_t>(),
           cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-          tot, spre, col_of, rank_of);
+          tot, spre, hot_col, pos_of);
       COOC_HIP_TRY(hipGetLastError());
     }
   SPT("finalize");
@@ -2403,7 +2499,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   out->cnt = cnt_.as<uint32_t>();
   out->dense = nullptr;
   out->rowsum = rowsum_.as<int64_t>();
-  out->rank_of = rank_of;
+  out->rank_of = pos_of;
   out->work = work_total;
   out->observed = work_total - self_total;  // ordered pairs of the counted rows
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total
@@ -2478,7 +2574,7 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
       k_sr_emit<<<unsigned(nb), kSrThreads, 0, s>>>(rows + j0, rstart, ukeys, ucnt, row_ptr, spre, rowsum_.as<int64_t>(),
                                                     col_.as<int32_t>(), cnt_.as<uint32_t>(), bump_.as<unsigned long long>(),
                                                     cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-                                                    tot_.as<PlanTotals>(), last_col_of_, last_rank_of_);
+                                                    tot_.as<PlanTotals>(), last_hot_col_, last_pos_of_);
       COOC_HIP_TRY(hipGetLastError());
       // kb (host) is reused by the next batch's upload: the copy must have been consumed
       COOC_HIP_TRY(hipStreamSynchronize(s));

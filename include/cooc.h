@@ -173,10 +173,8 @@ COOC_API int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64
 /* Item frequencies of a device item array (d_items int32[n_interactions]) into d_counts int64[n_items]
  * (device, overwritten) on hip_stream: the local part of the global frequencies that
  * cooc_count_device_owned's caller all-reduces (owner map, planner estimate).  Ids outside
- * [0, n_items) are not counted.  Performance note: ids below 16,384 are counted in LDS bins and the rest
- * with global 64-bit atomics, which is fast when the frequent items have the low ids (items numbered by
- * popularity rank, as the synthetic logs are); a log whose hot items have high ids stays exact but pays
- * contended global atomics on them. */
+ * [0, n_items) are not counted.  Each workgroup counts the items it meets most in an LDS table (the
+ * Zipf head, whatever its ids) and sends the rest to global 64-bit atomics. */
 COOC_API int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactions, int64_t *d_counts,
                               void *hip_stream);
 /* The column order of the last batch result's device rows (and of its top-k iteration, the tie order):

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--planner", default="auto", help='CooccurrenceCore planner ("sort": every whole row through '
                     'the sort + segmented-reduce path)')
     ap.add_argument("--permute", action="store_true", help="item ids through datagen.c3_item_perm (not rank-ordered)")
+    ap.add_argument("--column-order", action="store_true", help="COOC_FLAG_COLUMN_ORDER (no frequency relabel)")
     args = ap.parse_args()
     import torch
 
@@ -46,7 +47,7 @@ def main():
     t_gen = time.perf_counter() - t0
     P = datagen.c3_ordered_pairs(0, U)
     M = datagen.C3_ITEMS
-    core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner)
+    core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner, column_order=args.column_order)
     core.set_kernel_timing(True)
     res = core.count_device(up, it)  # warm-up (allocations)
     torch.cuda.synchronize()
@@ -81,6 +82,7 @@ def main():
         "gen_s": t_gen,
         "planner": args.planner,
         "permuted_ids": args.permute,
+        "column_order": args.column_order,
         "sort_path_rows_pairs": core.last_sort_rows(),
         "verify": core.verify_batch(),
     }

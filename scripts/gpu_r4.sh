@@ -18,8 +18,8 @@ if [ "${AB:-0}" = "1" ]; then
 fi
 T=${TESTS:-none}
 if [ "$T" != "none" ]; then
-  K=""; [ "$T" != "all" ] && K="-k $T"
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TFILES:-tests} -m gpu -x -v --timeout 300 --timeout-method thread $K \
+  K=(); [ "$T" != "all" ] && K=(-k "$T")
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TFILES:-tests} -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
     > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|Error|FAIL" gpurun_out/pytest_gpu.log | tail -8; fatal $rc
   [ $rc -eq 0 ] || exit 1
