@@ -125,7 +125,8 @@ _SIGS = {
     "cooc_submit_batch": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, i32p, i64p, i32p]),
     "cooc_finish_window": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_window_delta": (ctypes.c_int, [vp, i32p, i64p, i32p, u32p, i16p]),
-    "cooc_copy_window_delta_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, i32p, u32p, i16p]),
+    "cooc_copy_window_delta_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, i32p, u32p,
+                                                    i16p]),
     "cooc_copy_window_rowsums": (ctypes.c_int, [vp, i32p, i64p, i32p]),
     "cooc_copy_window_topk": (ctypes.c_int, [vp, i32p, i32p, i32p, f64p]),
     "cooc_global_rowsums": (ctypes.c_int, [vp, i64p, i32p]),

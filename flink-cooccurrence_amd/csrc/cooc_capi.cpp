@@ -245,11 +245,11 @@ int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32
   });
 }
 
-int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *cols, uint32_t *cnt,
+int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int64_t cap, int32_t *cols, uint32_t *cnt,
                                  int16_t *cnt16) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;
-    Status s = ctx->stream_state.copy_delta_range(*ctx, row_begin, row_end, cols, cnt, cnt16);
+    Status s = ctx->stream_state.copy_delta_range(*ctx, row_begin, row_end, cap, cols, cnt, cnt16);
     return s.ok() ? COOC_OK : fail(ctx, s);
   });
 }

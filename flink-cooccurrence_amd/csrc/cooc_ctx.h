@@ -28,7 +28,8 @@ class StreamState {
   Status finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info);
   Status copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
   // entries of the delta rows [r0, r1) (row indices as in copy_delta): a window streams out in row ranges
-  Status copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+  Status copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int64_t cap, int32_t *cols, uint32_t *cnt,
+                          int16_t *cnt16);
   Status copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, int32_t *delta32);
   Status copy_topk(cooc_ctx &ctx, int32_t *rows, int32_t *sizes, int32_t *values, double *scores);
   Status global_rowsums(cooc_ctx &ctx, int64_t *exact, int32_t *v32);

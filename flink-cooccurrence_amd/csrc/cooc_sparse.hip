@@ -1268,36 +1268,17 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     // and count areas), then leave in order: 16-B stores of whole column / count runs instead of one
     // scattered 4-B store per entry and array
     uint32_t *sc = keys + kWStage, *sn = cnts + kWStage;
-    if (!A.hot_col || c0 >= kTW) {
-      // (above tile 0 a relabelled column maps back by a subtraction)
-      const uint32_t base_id = uint32_t(c0) - (A.hot_col ? uint32_t(kTW) : 0u);
+    // (after a relabel a column maps back by a lookup in tile 0's 64 KB table, a subtraction above)
+    const bool hot0 = A.hot_col && c0 < kTW;
+    const uint32_t shift = A.hot_col ? uint32_t(kTW) : 0u;
 #pragma unroll
-      for (int i = 0; i < kHashMax / kSpThreads; i++) {
-        if (ek[i] == ~0u) continue;
-        const uint32_t col = ek[i], r = er[i];
-        const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
-        sc[q] = base_id + col;
-        sn[q] = ec[i];
-      }
-    } else {
-      // a chunk over tile 0 after a relabel: every entry's sorted position (er), then the hot_col loads of its
-      // tile-0 entries issued back to back (ek is free once the position is known), then the LDS stores
-#pragma unroll
-      for (int i = 0; i < kHashMax / kSpThreads; i++) {
-        if (ek[i] == ~0u) continue;
-        const uint32_t col = ek[i], r = er[i];
-        er[i] = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
-        ek[i] = uint32_t(c0) + col;
-      }
-#pragma unroll
-      for (int i = 0; i < kHashMax / kSpThreads; i++)
-        if (ec[i]) ek[i] = ek[i] < uint32_t(kTW) ? uint32_t(A.hot_col[ek[i]]) : ek[i] - uint32_t(kTW);
-#pragma unroll
-      for (int i = 0; i < kHashMax / kSpThreads; i++) {
-        if (!ec[i]) continue;
-        sc[er[i]] = ek[i];
-        sn[er[i]] = ec[i];
-      }
+    for (int i = 0; i < kHashMax / kSpThreads; i++) {
+      if (ek[i] == ~0u) continue;
+      const uint32_t col = ek[i], r = er[i];
+      const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
+      const uint32_t c = uint32_t(c0) + col;
+      sc[q] = hot0 && c < uint32_t(kTW) ? uint32_t(A.hot_col[c]) : c - shift;
+      sn[q] = ec[i];
     }
     __syncthreads();
     const uint32_t head = min(ne, uint32_t((4 - (base & 3)) & 3));  // entries before the first 16-B boundary
@@ -1551,7 +1532,10 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
       rsum = 0;
       if (tid == 0) {
         A.deferred[atomicAdd(reinterpret_cast<unsigned long long *>(&A.tot->n_deferred), 1ull)] = a;
-        S_.row_n = 0;  // (the row's rows so far are abandoned; its region space is not reused)
+        // the row's entries so far are abandoned: at the tail of the workgroup's slab they are handed back
+        // (a row region of its own is restored below and its space stays unused)
+        if (!S_.own) S_.slab_cur = S_.row_begin;
+        S_.row_n = 0;
       }
     }
     if (!split) {  // the row-sum check: every count of the row, summed exactly (u64), == W_a - c_a
@@ -2067,7 +2051,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   if (T > kSpMaxTiles)
     return Status{1, "n_items > " + std::to_string(int64_t(kSpMaxTiles) * kTW) + " is not supported"};
   if (n > int64_t(INT32_MAX)) return Status{1, "more than 2^31 interactions in one window"};
-  if (U >= int64_t(UINT32_MAX)) return Status{1, "more than 2^32 - 1 users in one window"};
+  // (a contribution keeps its list index in bits 0..30, kSelfBit in bit 31)
+  if (U > int64_t(kListMask)) return Status{1, "more than 2^31 - 1 user lists in one window"};
   const int64_t U1 = std::max<int64_t>(U, 1), n1 = std::max<int64_t>(n, 1);
   COOC_TRY(tot_.reserve(sizeof(PlanTotals)));
   COOC_TRY(queue_.reserve(sizeof(int32_t) * 4));

@@ -432,8 +432,8 @@ Status StreamState::copy_entries(int64_t e0, int64_t e1, int32_t *cols, uint32_t
   return Status::Ok();
 }
 
-Status StreamState::copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int32_t *cols, uint32_t *cnt,
-                                     int16_t *cnt16) {
+Status StreamState::copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int64_t cap, int32_t *cols,
+                                     uint32_t *cnt, int16_t *cnt16) {
   if (!have_window_) return Status{COOC_ERR_STATE, "no finished window"};
   COOC_HIP_TRY(hipSetDevice(ctx.device));
   const int32_t R = empty_window_ ? 0 : last_.n_rows;
@@ -442,6 +442,10 @@ Status StreamState::copy_delta_range(cooc_ctx &ctx, int32_t r0, int32_t r1, int3
                                     std::to_string(R) + ")"};
   if (r0 == r1) return Status::Ok();
   COOC_TRY(pack_delta(ctx));
+  const int64_t n = delta_start_[r1] - delta_start_[r0];
+  if ((cols || cnt || cnt16) && n > cap)  // (the caller's buffers are smaller than the range)
+    return Status{COOC_ERR_ARG, "delta rows [" + std::to_string(r0) + ", " + std::to_string(r1) + ") hold " +
+                                    std::to_string(n) + " entries, more than the " + std::to_string(cap) + " given"};
   return copy_entries(delta_start_[r0], delta_start_[r1], cols, cnt, cnt16);
 }
 

@@ -153,7 +153,8 @@ JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyDel
   scratch c, v;
   c.p = v.p = NULL;
   if (!scratch_get(env, &c, cols, sizeof(jint), n, 0, 'I') && !scratch_get(env, &v, cnt16, sizeof(jshort), n, 0, 'S'))
-    check(env, H(h), cooc_copy_window_delta_range(H(h), rowBegin, rowEnd, (int32_t *)c.p, NULL, (int16_t *)v.p));
+    check(env, H(h), cooc_copy_window_delta_range(H(h), rowBegin, rowEnd, (int64_t)n, (int32_t *)c.p, NULL,
+                                                  (int16_t *)v.p));
   scratch_put(env, &v, 1, 'S', n);
   scratch_put(env, &c, 1, 'I', n);
 }

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 4
+#define COOC_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -236,10 +236,11 @@ COOC_API int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_in
 COOC_API int cooc_copy_window_delta(cooc_ctx *ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,
                            int16_t *cnt16);
 /* The entries of delta rows [row_begin, row_end) only (row indices as in cooc_copy_window_delta's rows[]):
- * cols/cnt/cnt16 [row_ptr[row_end] - row_ptr[row_begin]].  A window whose delta holds more entries than
+ * cols/cnt/cnt16 [row_ptr[row_end] - row_ptr[row_begin]], each holding at least `cap` entries: a range of
+ * more entries than cap is COOC_ERR_ARG and nothing is written.  A window whose delta holds more entries than
  * one Java array can (2^31 - 1) streams out in row ranges: first cooc_copy_window_delta(rows, row_ptr,
  * NULL, NULL, NULL), then ranges sized from row_ptr.  The packed copy-out view is built once per window. */
-COOC_API int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *cols,
+COOC_API int cooc_copy_window_delta_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int64_t cap, int32_t *cols,
                                           uint32_t *cnt, int16_t *cnt16);
 /* Row-sum updates of the last window, one per delta row (same order as rows): exact int64 and the
  * reference's int view (RowSumAggregator.java:25-27; the reference drops an update whose int

@@ -86,7 +86,7 @@ class JniReplay:
                 r1 += 1
             n = int(row_ptr[r1] - row_ptr[r0])
             cols, cnt16 = np.zeros(n, np.int32), np.zeros(n, np.int16)
-            self.check(self.L.cooc_copy_window_delta_range(self.h, r0, r1, self._p(cols, ctypes.c_int32), None,
+            self.check(self.L.cooc_copy_window_delta_range(self.h, r0, r1, n, self._p(cols, ctypes.c_int32), None,
                                                            self._p(cnt16, ctypes.c_int16)), self.h)
             self.ranges += 1
             for r in range(r0, r1):
@@ -172,6 +172,12 @@ def test_delta_range_arguments(pkg, torch_cuda):
     n = len(w.rows)
     for r0, r1 in [(-1, 1), (2, 1), (0, n + 1)]:
         with pytest.raises(_lib.IllegalArgumentException):
-            _lib.check(L.cooc_copy_window_delta_range(h, r0, r1, None, None, None), h)
-    _lib.check(L.cooc_copy_window_delta_range(h, 1, 1, None, None, None), h)
+            _lib.check(L.cooc_copy_window_delta_range(h, r0, r1, 0, None, None, None), h)
+    _lib.check(L.cooc_copy_window_delta_range(h, 1, 1, 0, None, None, None), h)
+    # a buffer smaller than the range (the JNI sizes its scratch from the Java length) is refused
+    nb = int(w.row_ptr[n] - w.row_ptr[0])
+    small = np.zeros(max(nb - 1, 0), np.int32)
+    with pytest.raises(_lib.IllegalArgumentException):
+        _lib.check(L.cooc_copy_window_delta_range(h, 0, n, nb - 1, small.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                  None, None), h)
     op.close()
