@@ -1,0 +1,28 @@
+"""The host-only parsers of untrusted bytes -- the Kryo record codec (cooc_codec.cpp,
+ItemCooccurrences.java:113-147) and the text splitter (cooc_ingest.cpp, FlinkCooccurrences.java:207-229)
+-- compiled with AddressSanitizer and UndefinedBehaviorSanitizer (g++; no device code) and driven by
+tests/sanitize/host_fuzz.cpp: random round trips, every truncation, bit flips, random bytes and random
+text through the two-phase (size, then fill) protocol.  Any out-of-bounds access or undefined operation
+aborts the driver.  The device-side code is not sanitized (GPU sanitizers are not available on the pool)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "flink-cooccurrence_amd", "csrc")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_host_parsers_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "host_fuzz")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-Wall", "-o", exe, os.path.join(ROOT, "tests", "sanitize", "host_fuzz.cpp"),
+           os.path.join(CSRC, "cooc_codec.cpp"), os.path.join(CSRC, "cooc_ingest.cpp")]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)  # (the sanitizer runtime must come first)
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "host_fuzz ok" in r.stdout
