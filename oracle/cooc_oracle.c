@@ -1067,3 +1067,58 @@ EXPORT int64_t oc_row_checksums(int64_t n_users, const int64_t *user_ptr, const 
   if (pairs) *pairs = pr;
   return nnz;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* The rescorer's top-k loop over given rows (ItemRowRescorerTwoInputStreamOperator.java:195-223, */
+/* scoreItem :230-241, IntDoublePriorityQueue add/update :132-150), each row's entries fed in the */
+/* order given (a device row's own order: the tie order).  Row j is item row_items[j] with entries */
+/* [row_ptr[j], row_ptr[j + 1]) of cols / cnt16 (the Int2ShortOpenHashMap values); rs32 holds every */
+/* item's int row sum (Int2IntOpenHashMap.get, 0 when absent) and observed the rescorer's long.    */
+/* Rows are dealt to n_threads threads.  Heaps out as sizes[n_rows], values / scores[n_rows * k],  */
+/* positions 1..size (iterator(), IntDoublePriorityQueue.java:215-242).                            */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int64_t n_rows, j0, j1;
+  const int32_t *row_items;
+  const int64_t *row_ptr;
+  const int32_t *cols;
+  const int16_t *cnt16;
+  const int32_t *rs32;
+  int64_t observed;
+  int32_t k;
+  int32_t *sizes, *values;
+  double *scores;
+} topk_job;
+
+static void *topk_run(void *arg) {
+  topk_job *j = (topk_job *)arg;
+  oc_pq *q = oc_pq_create(j->k);
+  for (int64_t r = j->j0; r < j->j1; r++) {
+    oc_pq_reset(q);
+    const int32_t a = j->row_items[r];
+    for (int64_t e = j->row_ptr[r]; e < j->row_ptr[r + 1]; e++) {
+      const int32_t b = j->cols[e];
+      pq_offer(q, j->k, b, oc_score_item(j->cnt16[e], j->rs32[a], j->rs32[b], j->observed));
+    }
+    j->sizes[r] = q->size;
+    oc_pq_entries(q, j->values + r * j->k, j->scores + r * j->k);
+  }
+  oc_pq_destroy(q);
+  return NULL;
+}
+
+EXPORT void oc_rows_topk(int64_t n_rows, const int32_t *row_items, const int64_t *row_ptr, const int32_t *cols,
+                         const int16_t *cnt16, const int32_t *rs32, int64_t observed, int32_t k, int32_t n_threads,
+                         int32_t *sizes, int32_t *values, double *scores) {
+  if (n_threads < 1) n_threads = 1;
+  topk_job *jobs = (topk_job *)calloc((size_t)n_threads, sizeof(topk_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+  for (int32_t t = 0; t < n_threads; t++) {
+    jobs[t] = (topk_job){n_rows, n_rows * t / n_threads, n_rows * (t + 1) / n_threads, row_items, row_ptr, cols,
+                         cnt16, rs32, observed, k, sizes, values, scores};
+    pthread_create(&th[t], NULL, topk_run, &jobs[t]);
+  }
+  for (int32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+}

@@ -101,6 +101,8 @@ def lib():
                                                     u64p, i64p, i64p]),
         "oc_row_checksums": (ctypes.c_int64, [ctypes.c_int64, i64p, i32p, ctypes.c_int32, ctypes.c_int32, i64p,
                                               u64p, i64p, i64p]),
+        "oc_rows_topk": (None, [ctypes.c_int64, i32p, i64p, i32p, ctypes.POINTER(ctypes.c_int16), i32p, ctypes.c_int64,
+                                ctypes.c_int32, ctypes.c_int32, i32p, i32p, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -125,6 +127,26 @@ def llr(k11: int, k12: int, k21: int, k22: int) -> float:
 def score_item(k11_i16: int, item_row_sum: int, other_row_sum: int, observed: int) -> float:
     """ItemRowRescorerTwoInputStreamOperator.scoreItem, :230-241."""
     return lib().oc_score_item(k11_i16, item_row_sum, other_row_sum, observed)
+
+
+def rows_topk(row_items, row_ptr, cols, cnt16, rs32, observed: int, k: int, n_threads: int = 1):
+    """The rescorer's heaps of the given rows (ItemRowRescorer...java:195-223), entries fed in the order
+    given: row j is item row_items[j], entries [row_ptr[j], row_ptr[j+1]) of cols / cnt16 (int16 counts);
+    rs32 = every item's int row sum; observed = the rescorer's long.  -> (sizes [n], values [n, k],
+    scores [n, k]) in IntDoublePriorityQueue order (positions 1..size)."""
+    ri = np.ascontiguousarray(row_items, np.int32)
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    c = np.ascontiguousarray(cols, np.int32)
+    v = np.ascontiguousarray(cnt16, np.int16)
+    rs = np.ascontiguousarray(rs32, np.int32)
+    n = len(ri)
+    sizes = np.zeros(n, np.int32)
+    vals = np.zeros((n, k), np.int32)
+    scores = np.zeros((n, k), np.float64)
+    lib().oc_rows_topk(n, _p(ri, i32p), _p(rp, i64p), _p(c, i32p), v.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+                       _p(rs, i32p), int(observed), int(k), int(n_threads), _p(sizes, i32p), _p(vals, i32p),
+                       scores.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return sizes, vals, scores
 
 
 class PriorityQueue:

@@ -94,3 +94,66 @@ def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share
     del up_d, it_d
     want = oracle.row_checksums(up, it, M, _threads())
     _compare(res, chk, cs, nnz, want, datagen.c3_ordered_pairs(0, U))
+
+
+def _d2h(ptr, n, dtype, offset=0):
+    import ctypes
+
+    out = np.zeros(n, dtype)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        src = ctypes.c_void_p(ptr + offset * out.itemsize)
+        assert hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), src, ctypes.c_size_t(out.nbytes), ctypes.c_int(2)) == 0
+    return out
+
+
+def test_c5_topk_benched_share_vs_oracle(pkg, oracle, torch_cuda):
+    """C5 at the benchmark's size (bench.py --config c5: 1/8 of C3, top-50, the reference's int16 / int32
+    views): the device heaps of rows 0-63 (the hottest: ~1e6 entries, int16 wraps), 1,000 random rows and
+    EVERY row whose heap root is NaN (a wrapped k11 < 0 or the reference's k22 = observed + k11 - k12 - k21
+    going negative, ItemRowRescorer...java:238) against the oracle's rescorer loop (ItemRowRescorer...java:
+    195-223, LogLikelihood.java:41-57, IntDoublePriorityQueue.java:132-205) fed each row's entries in the
+    device row's order (the tie order).  Scores within 1e-6 relative, NaN where NaN; the identical heap
+    layout whenever every score agrees bit for bit."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    from tests._helpers import assert_row_topk
+
+    U, M, k = datagen.C3_USERS // 8, datagen.C3_ITEMS, 50
+    dev = torch.device("cuda", 0)
+    up_d, it_d = datagen.c3_users(0, U, device=dev)
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(up_d, it_d)
+        del up_d, it_d
+        sizes = torch.empty(M, dtype=torch.int32, device=dev)
+        vals = torch.empty((M, k), dtype=torch.int32, device=dev)
+        scores = torch.empty((M, k), dtype=torch.float64, device=dev)
+        core.topk_batch_device(k, sizes, vals, scores)
+        rowsum = torch.empty(M, dtype=torch.int64, device=dev)
+        core.copy_rowsum_device(rowsum)
+        torch.cuda.synchronize()
+        sz, v, sc = sizes.cpu().numpy(), vals.cpu().numpy(), scores.cpu().numpy()
+        del vals, scores
+        rs = rowsum.cpu().numpy()
+        base = _d2h(res.row_base, M, np.int64)
+        nnz = _d2h(res.row_nnz, M, np.int32).astype(np.int64)
+        rng = np.random.default_rng(42)
+        nonempty = np.flatnonzero(nnz)
+        nan_root = np.flatnonzero((sz > 0) & np.isnan(sc[:, 0]))
+        rows = np.unique(np.concatenate([np.arange(64), rng.choice(nonempty, 1000, replace=False), nan_root]))
+        rp = np.concatenate([[0], np.cumsum(nnz[rows])])
+        cols = np.zeros(int(rp[-1]), np.int32)
+        cnt = np.zeros(int(rp[-1]), np.uint32)
+        for j, a in enumerate(rows.tolist()):  # each row in the device's own order (the tie order)
+            cols[rp[j]:rp[j + 1]] = _d2h(res.col, int(nnz[a]), np.int32, int(base[a]))
+            cnt[rp[j]:rp[j + 1]] = _d2h(res.cnt, int(nnz[a]), np.uint32, int(base[a]))
+    rs32 = rs.astype(np.int64).astype(np.uint64).astype(np.uint32).view(np.int32)  # Java int row sums
+    observed = int(rs32.astype(np.int64).sum())  # the rescorer's long: the sum of the int deltas (:154)
+    cnt16 = cnt.astype(np.uint16).view(np.int16)
+    w_sz, w_v, w_sc = oracle.rows_topk(rows, rp, cols, cnt16, rs32, observed, k, _threads())
+    assert len(nan_root) > 0, "the benched share has NaN heap roots (int16 wraps): they must be covered"
+    for j, a in enumerate(rows.tolist()):
+        want = [(int(w_v[j, i]), float(w_sc[j, i])) for i in range(int(w_sz[j]))]
+        assert_row_topk(sz[a], v[a], sc[a], want, where=f"row {a}")
+    print(f"checked {len(rows)} heaps ({len(nan_root)} with a NaN root) over {int(rp[-1])} entries")
