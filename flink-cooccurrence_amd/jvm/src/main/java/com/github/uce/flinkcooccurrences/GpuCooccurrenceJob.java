@@ -17,7 +17,8 @@ import org.apache.flink.streaming.api.windowing.time.Time;
  * windows) and returns the same rescorer wiring as :162-167.  In main:
  * <pre>
  *   DataStream&lt;Tuple2&lt;Integer, IntDoublePriorityQueue&gt;&gt; topKStream = skipCuts
- *       ? GpuCooccurrenceJob.topK(interactionStream, windowSize, windowUnit, nItems, devices, configuration.getTopK())
+ *       ? GpuCooccurrenceJob.topK(interactionStream, windowSize, windowUnit, nItems, devices, configuration.getTopK(),
+ *                                 gpuRescore)
  *       : ...the reference's sampled graph...;
  * </pre>
  * Uncompiled here (no JDK); see GpuNonSampledCooccurrenceRowsOperator.
@@ -30,6 +31,26 @@ final class GpuCooccurrenceJob {
   static DataStream<Tuple2<Integer, IntDoublePriorityQueue>> topK(
       DataStream<Tuple3<Integer, Integer, Long>> interactionStream, int windowSize, TimeUnit windowUnit, int nItems,
       int[] devices, short topK) {
+    return topK(interactionStream, windowSize, windowUnit, nItems, devices, topK, false);
+  }
+
+  /**
+   * gpuRescore: the rescorer runs on the device too (GpuNonSampledCooccurrenceTopKOperator replaces
+   * FlinkCooccurrences.java:65-74 AND :135-167); one subtask holds every user and the global rows.
+   * Otherwise the rows operator feeds the reference's ItemRowRescorerTwoInputStreamOperator.
+   */
+  static DataStream<Tuple2<Integer, IntDoublePriorityQueue>> topK(
+      DataStream<Tuple3<Integer, Integer, Long>> interactionStream, int windowSize, TimeUnit windowUnit, int nItems,
+      int[] devices, short topK, boolean gpuRescore) {
+    if (gpuRescore) {
+      return interactionStream
+          .keyBy(0)
+          .transform(
+              "GpuNonSampledCooccurrenceTopK (" + windowSize + " " + windowUnit + ", top " + topK + ")",
+              GpuNonSampledCooccurrenceTopKOperator.getOutputType(),
+              new GpuNonSampledCooccurrenceTopKOperator(windowSize, windowUnit, nItems, devices, topK))
+          .setParallelism(1);
+    }
     final SingleOutputStreamOperator<Void> counter = interactionStream
         .keyBy(0)
         .transform(

@@ -181,3 +181,86 @@ def test_delta_range_arguments(pkg, torch_cuda):
         _lib.check(L.cooc_copy_window_delta_range(h, 0, n, nb - 1, small.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                                   None, None), h)
     op.close()
+
+
+class JniTopKReplay(JniReplay):
+    """cooc_jni.c + GpuNonSampledCooccurrenceTopKOperator (the rescorer on the device too), call for call:
+    create(topK) -> processElements -> processWatermark until nothing fires -> per fired window
+    cooc_copy_window_topk(rows, sizes, values, scores) -> one IntDoublePriorityQueue per rescored row,
+    rebuilt with add() in heap order (IntDoublePriorityQueue.java:132-137)."""
+
+    def __init__(self, lib, n_items: int, window_ms: int, topk: int):
+        from flink_cooccurrence_amd._lib import CoocConfig, check
+
+        self.L, self.check, self.k = lib, check, topk
+        cfg = CoocConfig(-1, n_items, topk, 0, window_ms, 0, 0)
+        h = ctypes.c_void_p()
+        devs = np.zeros(1, np.int32)
+        check(lib.cooc_create_on(ctypes.byref(cfg), devs.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 1, 0,
+                                 ctypes.byref(h)))
+        self.h = h
+
+    def _emit_window(self, info):
+        """emitTopK: (ts, {item: [(value, score) in heap order]}) of one fired window."""
+        from oracle import oracle
+
+        n, k = info.n_topk, info.topk
+        assert k == self.k
+        rows, sizes = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        vals, scores = np.zeros(n * k, np.int32), np.zeros(n * k, np.float64)
+        if n:
+            self.check(self.L.cooc_copy_window_topk(self.h, self._p(rows, ctypes.c_int32), self._p(sizes, ctypes.c_int32),
+                                                    self._p(vals, ctypes.c_int32), self._p(scores, ctypes.c_double)),
+                       self.h)
+        heaps = {}
+        for r in range(n):
+            q = oracle.PriorityQueue(k)  # topKReuse.reset(); add() in heap order
+            for i in range(int(sizes[r])):
+                q.add(int(vals[r * k + i]), float(scores[r * k + i]))
+            got = q.entries()
+            want = list(zip(vals[r * k:r * k + sizes[r]].tolist(), scores[r * k:r * k + sizes[r]].tolist()))
+            assert [v for v, _ in got] == [v for v, _ in want], "add() in heap order changed the layout"
+            heaps[int(rows[r])] = got
+        return info.ts, heaps
+
+
+@pytest.mark.parametrize("n_items", [1000, 1_000_000])
+def test_topk_operator_call_sequence_vs_reference_rescorer(pkg, oracle, torch_cuda, n_items):
+    """GpuNonSampledCooccurrenceTopKOperator's output -- one Tuple2<Integer, IntDoublePriorityQueue> per
+    rescored item and window -- against the reference's ItemRowRescorerTwoInputStreamOperator fed by its own
+    windows (oracle.OracleStream with topK: ItemRowRescorer...java:116-241), window by window, with an int16
+    wrap on the way.  Heaps by the tolerance contract of SURVEY §8(a) (scores within 1e-6 relative, items
+    strictly above the k-th score equal; the identical layout wherever every score agrees bit for bit)."""
+    from flink_cooccurrence_amd import _lib, datagen
+
+    from tests._helpers import assert_row_topk
+
+    L, k = _lib.load(), 5
+    d = datagen.config_c1(seed=12, U=700, M=n_items, mean=22.0)
+    users, items, ts = datagen.to_records(d["user_ptr"], d["items"], d["ts"])
+    users = np.concatenate([users, np.full(200, 10**6, np.int32)])
+    items = np.concatenate([items, np.full(200, 3, np.int32)])
+    ts = np.concatenate([ts, np.full(200, int(ts[-1]), np.int64)])
+    order = np.argsort(ts, kind="stable")
+    users, items, ts = users[order], items[order], ts[order]
+    op = JniTopKReplay(L, n_items, 1000, k)
+    ref = oracle.OracleStream(1000, topk=k)
+    got, want, step = [], [], 2500
+    for lo in range(0, len(users), step):
+        sl = slice(lo, lo + step)
+        wm = int(ts[sl][-1]) - 1 if lo + step < len(users) else 2**63 - 1
+        got += op.process_watermark(users[sl], items[sl], ts[sl], wm)[0]
+        ref.process_elements(users[sl], items[sl], ts[sl])
+        want += ref.process_watermark(wm)
+    assert len(got) == len(want) > 3
+    n_heaps = 0
+    for (gts, heaps), w in zip(got, want):
+        assert gts == w.ts
+        assert sorted(heaps) == sorted(w.topk_rows.tolist()), f"window {w.ts}: rescored items differ"
+        for r, a in enumerate(w.topk_rows.tolist()):
+            g = heaps[a]
+            want_r = [(int(w.topk_values[r, i]), float(w.topk_scores[r, i])) for i in range(int(w.topk_sizes[r]))]
+            assert_row_topk(len(g), [v for v, _ in g], [s for _, s in g], want_r, where=f"window {w.ts} row {a}")
+            n_heaps += 1
+    assert n_heaps > 100
+    op.close()
