@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 namespace cooc {
@@ -244,6 +245,9 @@ class Counter {
   bool relabel_ = true;
   DevBuf sp_rank_, sp_rkeys_;
   const int32_t *last_hot_col_ = nullptr, *last_pos_of_ = nullptr;
+  int32_t last_mc_ = 0;       // columns of the last run's (relabelled) space
+  // deferred rows through the library radix sort (COOC_SR_HIPCUB=1, A/B) instead of k_srb_row
+  bool srb_hipcub_ = getenv("COOC_SR_HIPCUB") && getenv("COOC_SR_HIPCUB")[0] == '1';
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
                       const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;

@@ -1964,6 +1964,249 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
   }
 }
 
+// ---- the hand-written sort path (the default for deferred rows; hipCUB only as the fallback) -------------
+// The overflow fallback of the per-row Int2ShortOpenHashMap (ItemRowAggregator.java:21-31) as an MSD radix
+// sort by hand: one 1,024-thread workgroup per deferred row.
+//  1. the first digit: the row's pairs are partitioned by column tile (kTW columns).  The tile histogram
+//     comes from the users' tile tables (tb: a list is already grouped by tile), so the partition is a set
+//     of contiguous segment copies into the row's scratch range; no id is read twice;
+//  2. every tile bucket, in column order, becomes (column, count) runs: a bucket of <= kSrbSort ids is
+//     bitonic-sorted in LDS and its runs counted (the segmented reduce of the +1 increments); a larger one
+//     is counted in kTW LDS counters (a counting sort of the last digit) and compacted in column order.  The
+//     runs are written to the front of the row's scratch range (behind the buckets already consumed); the
+//     diagonal loses the row's self term (dropped at zero);
+//  3. the runs are copied to an exactly sized output slice (relabelled columns mapped back), with the
+//     row-sum check of the other paths.
+// ~16 B of HBM traffic per pair (segment copy 4 + 4, bucket read 4, run copy) against ~40 for the
+// library radix sort of 8-B keys.
+constexpr int kSrbThreads = 1024, kSrbWaves = kSrbThreads / 64, kSrbSort = 4096;
+static_assert(4 * kSrbSort <= kTW, "sort buffer, run starts, counts and columns share the bucket's LDS");
+
+__device__ inline uint32_t srb_block_excl_scan(uint32_t x, uint32_t *total, uint32_t *s_wt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(x);
+  if (lane == 63) s_wt[wave] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kSrbWaves; w++) {
+    const uint32_t v = s_wt[w];
+    pre += w < wave ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  *total = uni(tot);
+  return pre + inc - x;
+}
+
+__global__ __launch_bounds__(kSrbThreads) void k_srb_row(
+    const int32_t *__restrict__ rows, const int64_t *__restrict__ kbase, const int64_t *__restrict__ row_ptr,
+    const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb, const uint16_t *__restrict__ arena0,
+    const uint32_t *__restrict__ arena1, int32_t T, int32_t Mc, uint32_t *__restrict__ scr_ids,
+    uint32_t *__restrict__ scr_cnt, const int64_t *__restrict__ spre, const int64_t *__restrict__ rowsum,
+    const int32_t *__restrict__ hot_col, const int32_t *__restrict__ pos_of, int32_t *__restrict__ col_out,
+    uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump, int64_t cap,
+    int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, PlanTotals *__restrict__ tot) {
+  __shared__ uint32_t buf[kTW];  // dense counters | sorted bucket keys [0, kSrbSort) + run starts above
+  __shared__ uint32_t s_hist[kSpMaxTiles + 1], s_off[kSpMaxTiles + 1], s_cur[kSpMaxTiles + 1];
+  __shared__ uint32_t s_wt[kSrbWaves];
+  __shared__ uint32_t s_o;        // runs written so far (the row's entries)
+  __shared__ int32_t s_drop;      // the bucket's run index of a diagonal that drops to zero (-1: none)
+  __shared__ unsigned long long s_sum;
+  __shared__ int64_t s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t j = blockIdx.x, a = rows[j];
+  const uint32_t ra = uint32_t(relabel_pos(pos_of, uint32_t(a)));
+  const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1], rb = kbase[j];
+  const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
+  for (int i = tid; i < kTW; i += kSrbThreads) buf[i] = 0u;
+  if (tid <= kSpMaxTiles) {
+    s_hist[tid] = 0u;
+    s_cur[tid] = 0u;
+  }
+  if (tid == 0) {
+    s_o = 0u;
+    s_sum = 0ull;
+  }
+  __syncthreads();
+  // 1a. the tile histogram from the tile tables: one thread per contribution
+  for (int64_t k = k0 + tid; k < k1; k += kSrbThreads) {
+    const int32_t *tbu = tb + int64_t(vals[k] & kListMask) * (T + 2);
+    const uint32_t n0 = uint32_t(tbu[T + 1] - tbu[0]);
+    if (n0) atomicAdd(&s_hist[0], n0);
+    int32_t prev = tbu[1];
+    for (int32_t t = 1; t < T; t++) {
+      const int32_t nx = tbu[t + 1];
+      if (nx > prev) atomicAdd(&s_hist[t], uint32_t(nx - prev));
+      prev = nx;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int32_t t = 0; t < T; t++) {
+      s_off[t] = run;
+      run += s_hist[t];
+    }
+    s_off[T] = run;
+  }
+  __syncthreads();
+  // 1b. the partition: a wave per contribution; lane t >= 1 copies its tile's segment (a few ids), the whole
+  // wave the tile-0 segment (the Zipf head: most of the list, u16)
+  for (int64_t k = k0 + wave; k < k1; k += kSrbWaves) {
+    const int32_t *tbu = tb + int64_t(vals[k] & kListMask) * (T + 2);
+    if (lane >= 1 && lane < T) {
+      const int32_t s1 = tbu[lane], e1 = tbu[lane + 1];
+      if (e1 > s1) {
+        const uint32_t d = atomicAdd(&s_cur[lane], uint32_t(e1 - s1));
+        uint32_t *dst = scr_ids + rb + s_off[lane] + d;
+        for (int32_t q = s1; q < e1; q++) dst[q - s1] = arena1[q];
+      }
+    }
+    const int32_t s0 = tbu[0], n0 = tbu[T + 1] - s0;
+    if (n0 > 0) {
+      uint32_t d = 0;
+      if (lane == 0) d = atomicAdd(&s_cur[0], uint32_t(n0));
+      d = __shfl(d, 0, 64);
+      uint32_t *dst = scr_ids + rb + s_off[0] + d;
+      for (int32_t q = lane; q < n0; q += 64) dst[q] = arena0[s0 + q];
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the buckets are read back by other waves)
+  // 2. the buckets in column order
+  uint64_t sum = 0;
+  for (int32_t t = 0; t < T; t++) {
+    const uint32_t n = uni(s_hist[t]);
+    if (n == 0) continue;
+    const uint32_t *src = scr_ids + rb + s_off[t];
+    const uint32_t o = uni(s_o);
+    const uint32_t c0 = uint32_t(t) * uint32_t(kTW);
+    if (n <= uint32_t(kSrbSort)) {
+      // bitonic sort of the bucket in LDS, then its runs
+      uint32_t P = 64;
+      while (P < n) P <<= 1;
+      for (uint32_t i = tid; i < P; i += kSrbThreads) buf[i] = i < n ? src[i] : 0xFFFFFFFFu;
+      __syncthreads();
+      for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+          for (uint32_t q = tid; q < P / 2; q += kSrbThreads) {
+            const uint32_t lo = 2 * q - (q & (jj - 1)), hi = lo + jj;
+            const uint32_t x = buf[lo], y = buf[hi];
+            if ((x > y) == ((lo & kk) == 0)) {
+              buf[lo] = y;
+              buf[hi] = x;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // run heads: thread tid owns positions 4 tid .. 4 tid + 3 (n <= 4096)
+      uint32_t hm = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const uint32_t i = 4u * uint32_t(tid) + uint32_t(e);
+        if (i < n && (i == 0 || buf[i] != buf[i - 1])) hm |= 1u << e;
+      }
+      uint32_t n_runs;
+      const uint32_t r0 = srb_block_excl_scan(uint32_t(__popc(hm)), &n_runs, s_wt);
+      if (tid == 0) s_drop = -1;
+      {
+        uint32_t r = r0;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if ((hm >> e) & 1u) buf[kSrbSort + r++] = 4u * uint32_t(tid) + uint32_t(e);
+      }
+      __syncthreads();
+      for (uint32_t r = tid; r < n_runs; r += kSrbThreads) {
+        const uint32_t st = buf[kSrbSort + r], en = r + 1 < n_runs ? buf[kSrbSort + r + 1] : n;
+        const uint32_t col = buf[st];
+        uint32_t c = en - st;
+        sum += c;
+        if (col == ra) {
+          c -= self;
+          if (c == 0u) s_drop = int32_t(r);
+        }
+        buf[2 * kSrbSort + r] = c;    // (n_runs <= kSrbSort: counts and columns in the areas above the starts)
+        buf[3 * kSrbSort + r] = col;
+      }
+      __syncthreads();
+      const int32_t drop = uni(s_drop);
+      for (uint32_t r = tid; r < n_runs; r += kSrbThreads) {
+        if (int32_t(r) == drop) continue;
+        const uint32_t q = o + r - (drop >= 0 && int32_t(r) > drop ? 1u : 0u);
+        scr_ids[rb + q] = buf[3 * kSrbSort + r];
+        scr_cnt[rb + q] = buf[2 * kSrbSort + r];
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < uint32_t(kTW); i += kSrbThreads) buf[i] = 0u;
+      if (tid == 0) s_o = o + n_runs - (drop >= 0 ? 1u : 0u);
+      __syncthreads();
+    } else {
+      // counting sort of the bucket's last digit: kTW LDS counters, then a column-order compaction
+      const uint32_t w = uint32_t(min(int64_t(kTW), int64_t(Mc) - int64_t(c0)));
+      for (uint32_t i = tid; i < n; i += kSrbThreads) atomicAdd(&buf[src[i] - c0], 1u);
+      __syncthreads();
+      if (tid == 0 && ra >= c0 && ra < c0 + w) buf[ra - c0] -= self;  // (the self pairs were counted too)
+      __syncthreads();
+      constexpr uint32_t per = uint32_t(kTW) / kSrbWaves;  // columns per wave (1,024)
+      const uint32_t lo = min(w, uint32_t(wave) * per), hi = min(w, lo + per);
+      uint32_t c = 0;
+      for (uint32_t b = lo + lane; b < hi; b += 64) c += buf[b] != 0u;
+      for (int x = 32; x > 0; x >>= 1) c += __shfl_xor(c, x, 64);
+      uint32_t n_out;
+      uint32_t off = srb_block_excl_scan(lane == 0 ? c : 0u, &n_out, s_wt);
+      off = __shfl(off, 0, 64);
+      const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+      for (uint32_t b0 = lo; b0 < hi; b0 += 64) {
+        const uint32_t b = b0 + uint32_t(lane);
+        const uint32_t v = b < hi ? buf[b] : 0u;
+        const uint64_t m = __ballot(v != 0u);
+        if (v) {
+          const uint32_t q = o + off + uint32_t(__popcll(m & lt));
+          scr_ids[rb + q] = c0 + b;
+          scr_cnt[rb + q] = v;
+          sum += v;
+          buf[b] = 0u;
+        }
+        off += uint32_t(__popcll(m));
+      }
+      if (tid == 0) {
+        s_o = o + n_out;
+        if (ra >= c0 && ra < c0 + w) sum += self;  // (sum counts the self pairs on both paths)
+      }
+      __syncthreads();
+    }
+  }
+  // 3. the exact output slice; the row-sum check
+  for (int x = 32; x > 0; x >>= 1) sum += __shfl_xor(sum, x, 64);
+  if (lane == 0 && sum) atomicAdd(&s_sum, (unsigned long long)sum);
+  __syncthreads();
+  const uint32_t d = s_o;
+  if (tid == 0) {
+    int64_t b = d ? int64_t(atomicAdd(bump, (unsigned long long)d)) : 0;
+    if (b + int64_t(d) > cap) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 4ull);
+      b = -1;
+    }
+    s_base = b;
+    row_base[a] = b < 0 ? 0 : b;
+    row_nnz[a] = b < 0 ? 0 : int32_t(d);
+    if (s_sum != (unsigned long long)(rowsum[a] + self)) {
+      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
+      tot->bad_row = a;
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int64_t base = s_base;
+  if (base < 0) return;
+  for (uint32_t i = tid; i < d; i += kSrbThreads) {
+    col_out[base + i] = relabel_col(hot_col, scr_ids[rb + i]);
+    cnt_out[base + i] = scr_cnt[rb + i];
+  }
+}
+
 __global__ void k_sr_pair_work(const int32_t *__restrict__ rows, int64_t n, const int64_t *__restrict__ row_w,
                                int64_t *__restrict__ out) {
   const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -2155,6 +2398,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   }
   last_hot_col_ = hot_col;
   last_pos_of_ = pos_of;
+  last_mc_ = Mc;
   // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
   if (owner) {
     COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
@@ -2497,7 +2741,7 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
                              const uint32_t *vals, const int64_t *spre, int64_t cap, hipStream_t s) {
   const int32_t *rows = sp_defer_.as<int32_t>();
   // the rows' pair work (sp_roww_), to the host in deferral order
-  COOC_TRY(sr_aux_.reserve(sizeof(int64_t) * size_t(3 * n_def + 4)));
+  COOC_TRY(sr_aux_.reserve(sizeof(int64_t) * size_t(3 * n_def + 8)));
   int64_t *d_w = sr_aux_.as<int64_t>();
   k_sr_pair_work<<<nblocks(n_def, 256), 256, 0, s>>>(rows, n_def, sp_roww_.as<int64_t>(), d_w);
   COOC_HIP_TRY(hipGetLastError());
@@ -2520,6 +2764,33 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
     acc += w[size_t(j)];
   }
   const int64_t nk = std::max<int64_t>(max_batch, 1);
+  if (!srb_hipcub_) {
+    // the hand-written path (k_srb_row): the batch's pairs as u32 ids + u32 run counts in scratch
+    COOC_TRY(sr_keys_.reserve(sizeof(uint32_t) * size_t(2 * nk)));
+    uint32_t *ids = sr_keys_.as<uint32_t>(), *cn = ids + nk;
+    std::vector<int64_t> kb;
+    for (int64_t j0 = 0; j0 < n_def;) {
+      int64_t j1 = j0, acc = 0;
+      kb.assign(1, 0);
+      while (j1 < n_def && (j1 == j0 || acc + w[size_t(j1)] <= budget)) {
+        acc += w[size_t(j1)];
+        kb.push_back(acc);
+        j1++;
+      }
+      last_deferred_pairs_ += acc;
+      int64_t *kbase = d_w + n_def + 2;
+      COOC_HIP_TRY(hipMemcpyAsync(kbase, kb.data(), sizeof(int64_t) * kb.size(), hipMemcpyHostToDevice, s));
+      k_srb_row<<<unsigned(j1 - j0), kSrbThreads, 0, s>>>(
+          rows + j0, kbase, row_ptr, vals, sp_tb_.as<int32_t>(), sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), T,
+          last_mc_, ids, cn, spre, rowsum_.as<int64_t>(), last_hot_col_, last_pos_of_, col_.as<int32_t>(),
+          cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
+          tot_.as<PlanTotals>());
+      COOC_HIP_TRY(hipGetLastError());
+      COOC_HIP_TRY(hipStreamSynchronize(s));  // (kb is reused by the next batch's upload)
+      j0 = j1;
+    }
+    return Status::Ok();
+  }
   COOC_TRY(sr_keys_.reserve(sizeof(uint64_t) * size_t(2 * nk)));
   COOC_TRY(sr_ukeys_.reserve(sizeof(uint64_t) * size_t(nk)));
   COOC_TRY(sr_ucnt_.reserve(sizeof(uint32_t) * size_t(nk)));

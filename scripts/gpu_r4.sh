@@ -28,6 +28,12 @@ if [ "${SMOKE:-0}" = "1" ]; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
 fi
+if [ "${SORTB:-0}" = "1" ]; then
+  for v in 0 ${SORTB_HIPCUB:-}; do
+    COOC_SR_HIPCUB=$v timeout -k 10 600 python -u scripts/bench_c3.py --steps 2 --planner sort > gpurun_out/sort_$v.json 2> gpurun_out/sort_$v.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/sort_$v.json'));print('sort hipcub=$v ms', round(d['ms'],1), 'rows,pairs', d['sort_path_rows_pairs'], 'verify', d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'], d['nnz'])"
+  done
+fi
 if [ "${BENCH:-0}" = "1" ]; then
   timeout -k 10 600 python -u bench.py --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err
