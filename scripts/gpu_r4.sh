@@ -12,8 +12,18 @@ if [ "${AB:-0}" = "1" ]; then
     for p in "" "--permute"; do
       n=rank; [ -n "$p" ] && n=perm
       timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || exit 1
+      if [ "${AB_COLORDER:-0}" = "1" ]; then
+        timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p --column-order > gpurun_out/ab_${n}_co.json 2> gpurun_out/ab_${n}_co.err || exit 1
+        python -c "import json;d=json.load(open('gpurun_out/ab_${n}_co.json'));print('$n column-order', 'ms', round(d['ms'],2), 'k_sp_main', round(d['k_sp_main_ms'],2))"
+      fi
       python -c "import json;d=json.load(open('gpurun_out/ab_$n.json'));print('$n', 'ms', round(d['ms'],2), 'k_sp_main', round(d['k_sp_main_ms'],2), 'nnz', d['nnz'], d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'])"
     done
+  done
+fi
+if [ "${SORTB:-0}" = "1" ]; then
+  for v in 0 ${SORTB_HIPCUB:-}; do
+    COOC_SR_HIPCUB=$v timeout -k 10 600 python -u scripts/bench_c3.py --steps 2 --planner sort > gpurun_out/sort_$v.json 2> gpurun_out/sort_$v.err || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/sort_$v.json'));print('sort hipcub=$v ms', round(d['ms'],1), 'rows,pairs', d['sort_path_rows_pairs'], 'verify', d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'], d['nnz'])"
   done
 fi
 T=${TESTS:-none}
@@ -27,12 +37,6 @@ fi
 if [ "${SMOKE:-0}" = "1" ]; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
-fi
-if [ "${SORTB:-0}" = "1" ]; then
-  for v in 0 ${SORTB_HIPCUB:-}; do
-    COOC_SR_HIPCUB=$v timeout -k 10 600 python -u scripts/bench_c3.py --steps 2 --planner sort > gpurun_out/sort_$v.json 2> gpurun_out/sort_$v.err || exit 1
-    python -c "import json;d=json.load(open('gpurun_out/sort_$v.json'));print('sort hipcub=$v ms', round(d['ms'],1), 'rows,pairs', d['sort_path_rows_pairs'], 'verify', d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'], d['nnz'])"
-  done
 fi
 if [ "${BENCH:-0}" = "1" ]; then
   timeout -k 10 600 python -u bench.py --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err

@@ -355,9 +355,9 @@ def test_item_counts_vs_bincount(pkg, torch_cuda):
 @pytest.mark.parametrize("M", [40_500, 1_000_000])
 def test_streaming_sparse_global_rows_vs_oracle(pkg, oracle, torch_cuda, M):
     """Streaming windows above the batch planner's range: the global rows are sorted row slabs merged
-    per window (the rescorer's itemRows) instead of the dense matrix.  40,500 items: windows counted by
-    the general planner; 1e6 items (C3's universe): a window's delta rows are C(full histories) -
-    C(histories before the window) of its users, both from the large-universe planner.  Every window's
+    per window (the rescorer's itemRows) instead of the dense matrix.  A window's delta rows come from one
+    pass of the large-universe planner over its active users (old / new positions: a new position walks
+    the user's whole history, an old one the window's new items, k_sp_window_contribs).  Every window's
     delta rows, row sums, observed and top-k against the oracle's rescorer, then the final global rows,
     row sums and accumulators; the slabs move and the arena compacts along the way."""
     from flink_cooccurrence_amd import datagen
