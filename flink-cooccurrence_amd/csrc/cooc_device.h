@@ -104,6 +104,8 @@ struct PlanTotals {
   int64_t n_deferred;     // whole rows handed to the sort + segmented-reduce path (hash table overflow)
   int64_t n_tiny;         // whole rows of <= kTinyW pairs (the queue's tail): one wave each (k_sp_tiny)
   int64_t tiny_ctr;       // k_sp_tiny's work counter
+  int64_t n_small;        // whole rows of kTinyW < W <= kSmallW pairs (before the tiny ones): a workgroup each (k_sp_small)
+  int64_t small_ctr;      // k_sp_small's work counter
 };
 
 // One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR

@@ -79,6 +79,7 @@ constexpr int kMaxProbe = 64;                          // linear probes before a
 constexpr int kSpU = 4;                                // partner loads in flight per lane
 constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
 constexpr int kTinyW = 256;                            // rows of at most this many pairs: one wave each (k_sp_tiny)
+constexpr int kSmallW = 4096;                          // ... of at most this many: one 256-thread workgroup each (k_sp_small)
 #ifndef COOC_SP_SPLIT_LG
 #define COOC_SP_SPLIT_LG 23
 #endif
@@ -598,7 +599,8 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
                                                  int32_t tiny_on) {
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0, n_tiny = 0;
+  uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0, n_tiny = 0,
+           n_small = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -614,6 +616,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     if (c > 0) {
       n_active = 1;
       n_tiny = (tiny_on && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
+      n_small = (tiny_on && W > kTinyW && W <= kSmallW) ? 1 : 0;  // (... just before the tiny ones)
       bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
@@ -682,6 +685,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   for (int o = 32; o > 0; o >>= 1) {
     act += __shfl_xor(act, o, 64);
     n_tiny += __shfl_xor(n_tiny, o, 64);
+    n_small += __shfl_xor(n_small, o, 64);
     n_gather += __shfl_xor(n_gather, o, 64);
     max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
   }
@@ -697,6 +701,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   }
   if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
   if (lane == 0 && n_tiny) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_tiny), (unsigned long long)n_tiny);
+  if (lane == 0 && n_small) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_small), (unsigned long long)n_small);
   if (lane == 0 && n_gather)
     atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_gather_rows), (unsigned long long)n_gather);
 }
@@ -1348,7 +1353,8 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
     S_.slab_cur = S_.slab_end = 0;
     S_.flag = 0u;
   }
-  const int64_t n_work = A.tot->n_chunks - A.tot->n_tiny;  // (the tiny rows at the queue's tail: k_sp_tiny)
+  // (the queue's tail: the small rows (k_sp_small), then the tiny ones (k_sp_tiny))
+  const int64_t n_work = A.tot->n_chunks - A.tot->n_tiny - A.tot->n_small;
 #ifdef COOC_SP_STATS
   if (threadIdx.x < 48) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
@@ -1696,6 +1702,7 @@ __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict
   tot->nnz_total = 0;
   tot->n_deferred = 0;
   tot->tiny_ctr = 0;
+  tot->small_ctr = 0;
   qctr[0] = 0;
   bump[0] = 0;
 }
@@ -1809,6 +1816,153 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
     const int64_t q = base + (r - r0) - (drop && r > diag ? 1 : 0);
     col_out[q] = relabel_col(hot_col, uint32_t(ukeys[r]));
     cnt_out[q] = ucnt[r] - (r == diag ? self : 0u);
+  }
+}
+
+// ---- small rows: one 256-thread workgroup per row -----------------------------------------------------
+// A whole row of kTinyW < W <= kSmallW pairs -- at C3 the half million rows of the Zipf tail, each one LDS
+// hash chunk over every tile in k_sp_main (~20 us per chunk there, two chunks per CU) -- sorted instead: its
+// lists gathered into 16 KB of LDS (a wave per contribution, coalesced), bitonic-sorted by the workgroup,
+// equal columns counted (the segmented reduce of the +1 increments), the diagonal's self term removed, the
+// entries written in column order from a per-workgroup output slab.  At 16 KB per workgroup a CU holds
+// eight rows in flight.
+constexpr int kSmallThreads = 256, kSmallWaves = kSmallThreads / 64;
+constexpr int64_t kSmallSlab = 16384;  // output entries reserved per workgroup at a time
+
+__global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_sp_small(SpArgs A) {
+  __shared__ uint32_t b[kSmallW];
+  __shared__ uint32_t s_wt[kSmallWaves];
+  __shared__ int64_t s_i, s_pos, s_cur, s_end;
+  __shared__ unsigned long long s_sum;
+  __shared__ int32_t s_drop;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t first = A.tot->n_chunks - A.tot->n_tiny - A.tot->n_small, n_small = A.tot->n_small;
+  const uint16_t *a0 = reinterpret_cast<const uint16_t *>(A.tarena0);
+  const uint32_t *a1 = reinterpret_cast<const uint32_t *>(A.tarena);
+  if (tid == 0) s_cur = s_end = 0;
+  for (;;) {
+    if (tid == 0) {
+      s_i = int64_t(atomicAdd(reinterpret_cast<unsigned long long *>(&A.tot->small_ctr), 1ull));
+      s_sum = 0ull;
+      s_drop = -1;
+    }
+    __syncthreads();
+    const int64_t i = uni(s_i);
+    if (i >= n_small) break;
+    const SpWork it = A.queue[first + i];
+    const int32_t a = it.row;
+    const uint32_t ra = uint32_t(sp_rank(A, a));
+    const int64_t k0 = it.k0, k1 = it.k1, e0 = A.epre[k0];
+    const uint32_t W = uint32_t(A.epre[k1] - e0);
+    const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
+    // 1. the lists, a wave per contribution, at their prefix positions (epre)
+    for (int64_t k = k0 + wave; k < k1; k += kSmallWaves) {
+      const int32_t *tbu = A.tb + int64_t(A.vals[k] & kListMask) * (A.T + 2);
+      const uint32_t s0 = uint32_t(tbu[0]), n0 = uint32_t(tbu[A.T + 1]) - s0;
+      const uint32_t s1 = uint32_t(tbu[1]), n1 = uint32_t(tbu[A.T]) - s1;
+      uint32_t *d = b + (A.epre[k] - e0);
+      for (uint32_t q = lane; q < n0; q += 64) d[q] = a0[s0 + q];
+      for (uint32_t q = lane; q < n1; q += 64) d[n0 + q] = a1[s1 + q];
+    }
+    uint32_t n2 = 64;
+    while (n2 < W) n2 <<= 1;
+    for (uint32_t q = W + tid; q < n2; q += kSmallThreads) b[q] = kSink;
+    __syncthreads();
+    // 2. bitonic sort of b[0, n2)
+    for (uint32_t kk = 2; kk <= n2; kk <<= 1) {
+      for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (uint32_t q = tid; q < n2 / 2; q += kSmallThreads) {
+          const uint32_t lo = 2 * q - (q & (jj - 1)), hi = lo + jj;
+          const uint32_t x = b[lo], y = b[hi];
+          if ((x > y) == ((lo & kk) == 0)) {
+            b[lo] = y;
+            b[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // 3. runs: thread tid owns positions 16 tid .. 16 tid + 15; a head counts its run forward
+    constexpr int kPer = kSmallW / kSmallThreads;
+    uint32_t hm = 0;
+#pragma unroll
+    for (int e = 0; e < kPer; e++) {
+      const uint32_t p = uint32_t(tid) * kPer + uint32_t(e);
+      if (p < W && (p == 0 || b[p] != b[p - 1])) hm |= 1u << e;
+    }
+    const uint32_t inc = wave_incl_scan(uint32_t(__popc(hm)));
+    if (lane == 63) s_wt[wave] = inc;
+    __syncthreads();
+    uint32_t r = inc - uint32_t(__popc(hm)), n_runs = 0;
+#pragma unroll
+    for (int w = 0; w < kSmallWaves; w++) {
+      r += w < wave ? s_wt[w] : 0u;
+      n_runs += s_wt[w];
+    }
+    n_runs = uni(n_runs);
+    uint64_t sum = 0;
+    uint32_t cnt[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; e++) {
+      cnt[e] = 0;
+      if (!((hm >> e) & 1u)) continue;
+      const uint32_t p = uint32_t(tid) * kPer + uint32_t(e), key = b[p];
+      uint32_t q = p + 1;
+      while (q < W && b[q] == key) q++;
+      uint32_t c = q - p;
+      sum += c;
+      if (key == ra) {
+        c -= self;
+        if (c == 0u) s_drop = int32_t(r + uint32_t(__popc(hm & ((1u << e) - 1u))));
+      }
+      cnt[e] = c;
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0 && sum) atomicAdd(&s_sum, (unsigned long long)sum);
+    __syncthreads();
+    const int32_t drop = uni(s_drop);
+    const uint32_t n_keep = n_runs - (drop >= 0 ? 1u : 0u);
+    if (tid == 0) {
+      s_pos = -1;
+      if (s_cur + int64_t(n_keep) > s_end) {
+        const int64_t take = max<int64_t>(kSmallSlab, int64_t(n_keep));
+        const int64_t nb = int64_t(atomicAdd(A.bump, (unsigned long long)take));
+        if (nb + take > A.cap) {
+          atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 4ull);
+          s_cur = s_end = 0;
+        } else {
+          s_cur = nb;
+          s_end = nb + take;
+        }
+      }
+      if (s_cur + int64_t(n_keep) <= s_end) {
+        s_pos = s_cur;
+        s_cur += n_keep;
+      }
+      A.row_base[a] = (n_keep && s_pos >= 0) ? s_pos : 0;
+      A.row_nnz[a] = s_pos >= 0 ? int32_t(n_keep) : 0;
+      // the row-sum check: the runs (self pairs included) add up to W
+      if (s_sum != (unsigned long long)W) {
+        atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull);
+        A.tot->bad_row = a;
+      }
+    }
+    __syncthreads();
+    const int64_t pos = uni(s_pos);
+    if (pos >= 0) {
+      uint32_t rr = r;
+#pragma unroll
+      for (int e = 0; e < kPer; e++) {
+        if (!((hm >> e) & 1u)) continue;
+        if (int32_t(rr) != drop) {
+          const int64_t q = pos + rr - (drop >= 0 && int32_t(rr) > drop ? 1 : 0);
+          A.col_out[q] = sp_col(A, b[uint32_t(tid) * kPer + uint32_t(e)]);
+          A.cnt_out[q] = cnt[e];
+        }
+        rr++;
+      }
+    }
+    __syncthreads();  // (b and the shared scalars are rewritten by the next row)
   }
 }
 
@@ -2555,7 +2709,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * grid)));
   const int64_t n_tiny = h_tot_->n_tiny;
   const int64_t grid_tiny = std::min<int64_t>((n_tiny + kTinyWaves - 1) / kTinyWaves, int64_t(n_cu_) * 8);
-  const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0);
+  const int64_t n_small = h_tot_->n_small;
+  const int64_t grid_small = std::min<int64_t>(n_small, int64_t(n_cu_) * 8);
+  const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0) +
+                        (n_small ? grid_small * kSmallSlab : 0);
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
   cap = std::max<int64_t>(1, std::min(cap, budget));
@@ -2623,7 +2780,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-    if (n_work > n_tiny) {
+    if (n_work > n_tiny + n_small) {
       k_sp_main<<<unsigned(grid), kSpThreads, kSpLds, s>>>(A);
       COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_TRACE
@@ -2648,7 +2805,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       fprintf(stderr, "[sp] bounds flags %llx\n", prog[2047]);
 #endif
     }
-    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
+    if (n_small > 0) {
+      k_sp_small<<<unsigned(grid_small), kSmallThreads, 0, s>>>(A);
+      COOC_HIP_TRY(hipGetLastError());
+    }
     if (n_tiny > 0) {
       k_sp_tiny<<<unsigned(grid_tiny), kTinyThreads, 0, s>>>(A);
       COOC_HIP_TRY(hipGetLastError());
@@ -2661,6 +2821,9 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
           tot, spre, hot_col, pos_of);
       COOC_HIP_TRY(hipGetLastError());
     }
+    // (the timed span: every counting kernel of the run -- k_sp_main, k_sp_small, k_sp_tiny, the split rows'
+    // finalize -- so that moving rows between them cannot flatter the kernel time)
+    if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_end, s));
   SPT("finalize");
     COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
     COOC_HIP_TRY(hipStreamSynchronize(s));
