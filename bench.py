@@ -165,7 +165,9 @@ def main():
         up, it = datagen.c3_users(u0, u1, device=dev, permute=args.permute_items)
         M = datagen.C3_ITEMS
         P_local = int(np.sum(lens_all[u0:u1] * (lens_all[u0:u1] - 1)))
-        kernel = "k_sp_main"
+        # the timed span (HIP events on the stream): every counting kernel of the step -- k_sp_main (hash / dense
+        # chunks, split shares), k_sp_small and k_sp_tiny (radix- and bitonic-sorted rows), k_sp_split_finalize
+        kernel = "k_sp_main+k_sp_small+k_sp_tiny+k_sp_split_finalize"
         pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_sp_main.json"))
         workload = ("C3 Zipf-skewed 1B log (BASELINE configs[2]), shard-invariant generator "
                     f"datagen.c3_users seed {datagen.C3_SEED}: users [r*1.25e6, (r+1)*1.25e6) on rank r "
@@ -319,8 +321,9 @@ def main():
             "algorithmic_bytes_per_launch": b_alg,
             "units_per_launch": {"ordered_pairs": P_counted, "interactions": N_seen, "users": U_seen,
                                  "distinct_keys": D},
-            "note": "B_alg = 4P + 4N + 8(U+1) + 12D per launch of the dominant kernel (SURVEY.md §8(d)), "
-                    "divided by its time from HIP events on its stream; frac > 1 would flag cache reuse. "
+            "note": "B_alg = 4P + 4N + 8(U+1) + 12D per launch of the dominant kernel (SURVEY.md §8(d); for C3 the "
+                    "counting kernels together, which share the rows between them), divided by its time from HIP "
+                    "events on its stream; frac > 1 would flag cache reuse. "
                     "traffic = HBM-side bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, "
                     "profiles/pmc_<kernel>.json) when collected; see DESIGN.md §4",
         },

@@ -250,6 +250,7 @@ class Counter {
   int32_t last_mc_ = 0;       // columns of the last run's (relabelled) space
   // deferred rows through the library radix sort (COOC_SR_HIPCUB=1, A/B) instead of k_srb_row
   bool srb_hipcub_ = getenv("COOC_SR_HIPCUB") && getenv("COOC_SR_HIPCUB")[0] == '1';
+  bool small_off_ = getenv("COOC_SP_SMALL") && getenv("COOC_SP_SMALL")[0] == '0';  // (A/B: small rows in k_sp_main)
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
                       const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;

@@ -615,8 +615,8 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     int32_t nw = 0;
     if (c > 0) {
       n_active = 1;
-      n_tiny = (tiny_on && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
-      n_small = (tiny_on && W > kTinyW && W <= kSmallW) ? 1 : 0;  // (... just before the tiny ones)
+      n_tiny = ((tiny_on & 1) && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
+      n_small = ((tiny_on & 2) && W > kTinyW && W <= kSmallW) ? 1 : 0;  // (... just before the tiny ones)
       bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
@@ -1819,18 +1819,86 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
   }
 }
 
-// ---- small rows: one 256-thread workgroup per row -----------------------------------------------------
+// ---- small rows: one 512-thread workgroup per row -----------------------------------------------------
 // A whole row of kTinyW < W <= kSmallW pairs -- at C3 the half million rows of the Zipf tail, each one LDS
 // hash chunk over every tile in k_sp_main (~20 us per chunk there, two chunks per CU) -- sorted instead: its
-// lists gathered into 16 KB of LDS (a wave per contribution, coalesced), bitonic-sorted by the workgroup,
-// equal columns counted (the segmented reduce of the +1 increments), the diagonal's self term removed, the
-// entries written in column order from a per-workgroup output slab.  At 16 KB per workgroup a CU holds
-// eight rows in flight.
-constexpr int kSmallThreads = 256, kSmallWaves = kSmallThreads / 64;
+// lists gathered into 16 KB of LDS (a wave per contribution, coalesced), LSD-radix-sorted by the workgroup
+// (7-bit digits, wave ballots rank equal digits), equal columns counted (the segmented reduce of the +1
+// increments), the diagonal's self term removed, the entries written in column order from a
+// per-workgroup output slab.  At 33 KB per workgroup a CU holds four rows in flight.
+constexpr int kSmallThreads = 512, kSmallWaves = kSmallThreads / 64;
 constexpr int64_t kSmallSlab = 16384;  // output entries reserved per workgroup at a time
+constexpr int kRadixBits = 7;
+
+// Stable LSD radix sort of k[0, n), n <= kSmallW, keys < 2^bits, kRadixBits per pass, ping-ponging between
+// k and t; returns the buffer that holds the sorted keys.  Wave w owns positions [w P, (w + 1) P),
+// P = kSmallW / kWaves, 64 at a time: a lane's rank among equal digits is the popcount of the ballot
+// match below it plus the wave's running count h[digit][w]; one exclusive scan over (digit, wave) turns
+// the counts into the scatter bases.  Four LDS accesses per key per pass.
+template <int kThreads>
+__device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uint32_t *s_wt, uint32_t n, int bits) {
+  constexpr int kWaves = kThreads / 64, kE = kSmallW / kThreads, kD = 1 << kRadixBits;
+  static_assert(kD * kWaves == 2 * kThreads, "two scan entries per thread");
+  static_assert(kE * 64 <= 512 && kRadixBits <= 7, "rank and digit pack into 16 bits");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t below_mask = (1ull << lane) - 1ull;
+  const uint32_t base = uint32_t(wave) * uint32_t(kE * 64);
+  for (int sh = 0; sh < bits; sh += kRadixBits) {
+    reinterpret_cast<uint32_t *>(h)[tid] = 0u;
+    __syncthreads();
+    uint32_t pk[kE / 2];  // (digit << 9 | rank), two per register; 0xffff: no key
+#pragma unroll
+    for (int e = 0; e < kE / 2; e++) pk[e] = 0xffffffffu;
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const uint32_t p0 = base + uint32_t(e) * 64u;
+      if (p0 >= n) continue;  // (wave-uniform)
+      const uint32_t p = p0 + uint32_t(lane);
+      const bool v = p < n;
+      const uint32_t d = v ? (k[p] >> sh) & uint32_t(kD - 1) : 0u;
+      uint64_t m = __ballot(v);
+#pragma unroll
+      for (int b = 0; b < kRadixBits; b++) {
+        const uint64_t bb = __ballot(v && ((d >> b) & 1u));
+        m &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      if (v) {
+        uint16_t *hd = h + d * kWaves + uint32_t(wave);
+        const uint32_t old = *hd, below = uint32_t(__popcll(m & below_mask));
+        const uint32_t sh16 = (e & 1) * 16;
+        pk[e / 2] = (pk[e / 2] & ~(0xffffu << sh16)) | (((old + below) | (d << 9)) << sh16);
+        if (below == 0u) *hd = uint16_t(old + uint32_t(__popcll(m)));  // the group's first lane
+      }
+    }
+    __syncthreads();
+    const uint32_t h0 = h[2 * tid], h1 = h[2 * tid + 1];
+    const uint32_t inc = wave_incl_scan(h0 + h1);
+    if (lane == 63) s_wt[wave] = inc;
+    __syncthreads();
+    uint32_t ex = inc - h0 - h1;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) ex += w < wave ? s_wt[w] : 0u;
+    h[2 * tid] = uint16_t(ex);
+    h[2 * tid + 1] = uint16_t(ex + h0);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const uint32_t x = (pk[e / 2] >> ((e & 1) * 16)) & 0xffffu;
+      if (x == 0xffffu) continue;
+      const uint32_t p = base + uint32_t(e) * 64u + uint32_t(lane), d = x >> 9;
+      t[uint32_t(h[d * kWaves + uint32_t(wave)]) + (x & 511u)] = k[p];
+    }
+    __syncthreads();
+    uint32_t *x = k;
+    k = t;
+    t = x;
+  }
+  return k;
+}
 
 __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_sp_small(SpArgs A) {
-  __shared__ uint32_t b[kSmallW];
+  __shared__ uint32_t b0[kSmallW + 1], b1[kSmallW + 1];  // (+1: the run starts' end marker)
+  __shared__ uint16_t s_h[(1 << kRadixBits) * kSmallWaves];
   __shared__ uint32_t s_wt[kSmallWaves];
   __shared__ int64_t s_i, s_pos, s_cur, s_end;
   __shared__ unsigned long long s_sum;
@@ -1839,6 +1907,8 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
   const int64_t first = A.tot->n_chunks - A.tot->n_tiny - A.tot->n_small, n_small = A.tot->n_small;
   const uint16_t *a0 = reinterpret_cast<const uint16_t *>(A.tarena0);
   const uint32_t *a1 = reinterpret_cast<const uint32_t *>(A.tarena);
+  int bits = 1;
+  while (bits < 32 && (uint32_t(A.M) - 1u) >> bits) bits++;
   if (tid == 0) s_cur = s_end = 0;
   for (;;) {
     if (tid == 0) {
@@ -1860,29 +1930,16 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
       const int32_t *tbu = A.tb + int64_t(A.vals[k] & kListMask) * (A.T + 2);
       const uint32_t s0 = uint32_t(tbu[0]), n0 = uint32_t(tbu[A.T + 1]) - s0;
       const uint32_t s1 = uint32_t(tbu[1]), n1 = uint32_t(tbu[A.T]) - s1;
-      uint32_t *d = b + (A.epre[k] - e0);
+      uint32_t *d = b0 + (A.epre[k] - e0);
       for (uint32_t q = lane; q < n0; q += 64) d[q] = a0[s0 + q];
       for (uint32_t q = lane; q < n1; q += 64) d[n0 + q] = a1[s1 + q];
     }
-    uint32_t n2 = 64;
-    while (n2 < W) n2 <<= 1;
-    for (uint32_t q = W + tid; q < n2; q += kSmallThreads) b[q] = kSink;
     __syncthreads();
-    // 2. bitonic sort of b[0, n2)
-    for (uint32_t kk = 2; kk <= n2; kk <<= 1) {
-      for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-        for (uint32_t q = tid; q < n2 / 2; q += kSmallThreads) {
-          const uint32_t lo = 2 * q - (q & (jj - 1)), hi = lo + jj;
-          const uint32_t x = b[lo], y = b[hi];
-          if ((x > y) == ((lo & kk) == 0)) {
-            b[lo] = y;
-            b[hi] = x;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    // 3. runs: thread tid owns positions 16 tid .. 16 tid + 15; a head counts its run forward
+    // 2. radix sort
+    const uint32_t *b = block_radix_sort<kSmallThreads>(b0, b1, s_h, s_wt, W, bits);
+    // 3. runs: the heads (a column's first position) among thread tid's kPer positions, ranked by a block
+    //    scan; their positions go to the free buffer (st), then a thread per run
+    uint32_t *st = (b == b0) ? b1 : b0;
     constexpr int kPer = kSmallW / kSmallThreads;
     uint32_t hm = 0;
 #pragma unroll
@@ -1900,22 +1957,16 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
       n_runs += s_wt[w];
     }
     n_runs = uni(n_runs);
-    uint64_t sum = 0;
-    uint32_t cnt[kPer];
 #pragma unroll
-    for (int e = 0; e < kPer; e++) {
-      cnt[e] = 0;
-      if (!((hm >> e) & 1u)) continue;
-      const uint32_t p = uint32_t(tid) * kPer + uint32_t(e), key = b[p];
-      uint32_t q = p + 1;
-      while (q < W && b[q] == key) q++;
-      uint32_t c = q - p;
+    for (int e = 0; e < kPer; e++)
+      if ((hm >> e) & 1u) st[r++] = uint32_t(tid) * kPer + uint32_t(e);
+    if (tid == 0) st[n_runs] = W;
+    __syncthreads();
+    uint64_t sum = 0;
+    for (uint32_t q = uint32_t(tid); q < n_runs; q += kSmallThreads) {
+      const uint32_t p = st[q], c = st[q + 1] - p;
       sum += c;
-      if (key == ra) {
-        c -= self;
-        if (c == 0u) s_drop = int32_t(r + uint32_t(__popc(hm & ((1u << e) - 1u))));
-      }
-      cnt[e] = c;
+      if (b[p] == ra && c == self) s_drop = int32_t(q);
     }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if (lane == 0 && sum) atomicAdd(&s_sum, (unsigned long long)sum);
@@ -1950,16 +2001,12 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
     __syncthreads();
     const int64_t pos = uni(s_pos);
     if (pos >= 0) {
-      uint32_t rr = r;
-#pragma unroll
-      for (int e = 0; e < kPer; e++) {
-        if (!((hm >> e) & 1u)) continue;
-        if (int32_t(rr) != drop) {
-          const int64_t q = pos + rr - (drop >= 0 && int32_t(rr) > drop ? 1 : 0);
-          A.col_out[q] = sp_col(A, b[uint32_t(tid) * kPer + uint32_t(e)]);
-          A.cnt_out[q] = cnt[e];
-        }
-        rr++;
+      for (uint32_t q = uint32_t(tid); q < n_runs; q += kSmallThreads) {
+        if (int32_t(q) == drop) continue;
+        const uint32_t p = st[q], c = st[q + 1] - p, key = b[p];
+        const int64_t o = pos + q - (drop >= 0 && int32_t(q) > drop ? 1 : 0);
+        A.col_out[o] = sp_col(A, key);
+        A.cnt_out[o] = c - (key == ra ? self : 0u);
       }
     }
     __syncthreads();  // (b and the shared scalars are rewritten by the next row)
@@ -2632,7 +2679,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                             sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
                                             order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
-                                            row_base_.as<int64_t>(), tot, spre, sort_rows_ ? 0 : 1);
+                                            row_base_.as<int64_t>(), tot, spre, sort_rows_ ? 0 : small_off_ ? 1 : 3);
   k_sp_totals<<<1, 1, 0, s>>>(tot, epre, spre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
@@ -2710,7 +2757,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   const int64_t n_tiny = h_tot_->n_tiny;
   const int64_t grid_tiny = std::min<int64_t>((n_tiny + kTinyWaves - 1) / kTinyWaves, int64_t(n_cu_) * 8);
   const int64_t n_small = h_tot_->n_small;
-  const int64_t grid_small = std::min<int64_t>(n_small, int64_t(n_cu_) * 8);
+  const int64_t grid_small = std::min<int64_t>(n_small, int64_t(n_cu_) * 4);
   const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0) +
                         (n_small ? grid_small * kSmallSlab : 0);
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
