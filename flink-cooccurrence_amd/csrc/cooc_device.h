@@ -106,6 +106,8 @@ struct PlanTotals {
   int64_t tiny_ctr;       // k_sp_tiny's work counter
   int64_t n_small;        // whole rows of kTinyW < W <= kSmallW pairs (before the tiny ones): a workgroup each (k_sp_small)
   int64_t small_ctr;      // k_sp_small's work counter
+  int64_t srb_ctr;        // k_srb_row's row counter (the deferred rows)
+  int64_t ts_pairs;       // pairs of the tiny and small rows (sorted by k_sp_tiny / k_sp_small)
 };
 
 // One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR

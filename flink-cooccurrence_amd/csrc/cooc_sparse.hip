@@ -48,6 +48,11 @@
 #define STAT_CLOCK() 0ull
 #define STAT_ADD(k, v) do {} while (0)
 #endif
+#ifdef COOC_SP_STATS
+#define SRB_STAT(k, v) do { if (threadIdx.x == 0) atomicAdd(srb_st + (k), (unsigned long long)(v)); } while (0)
+#else
+#define SRB_STAT(k, v) do {} while (0)
+#endif
 #ifdef COOC_SP_TRACE
 #define SPT(msg) do { hipStreamSynchronize(s); fprintf(stderr, "[sp] %s\n", msg); } while (0)
 #else
@@ -600,7 +605,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0, n_tiny = 0,
-           n_small = 0;
+           n_small = 0, ts_pairs = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -617,6 +622,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
       n_active = 1;
       n_tiny = ((tiny_on & 1) && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
       n_small = ((tiny_on & 2) && W > kTinyW && W <= kSmallW) ? 1 : 0;  // (... just before the tiny ones)
+      ts_pairs = (n_tiny || n_small) ? uint64_t(W) : 0u;
       bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
@@ -686,6 +692,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     act += __shfl_xor(act, o, 64);
     n_tiny += __shfl_xor(n_tiny, o, 64);
     n_small += __shfl_xor(n_small, o, 64);
+    ts_pairs += __shfl_xor(ts_pairs, o, 64);
     n_gather += __shfl_xor(n_gather, o, 64);
     max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
   }
@@ -702,6 +709,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
   if (lane == 0 && n_tiny) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_tiny), (unsigned long long)n_tiny);
   if (lane == 0 && n_small) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_small), (unsigned long long)n_small);
+  if (lane == 0 && ts_pairs) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->ts_pairs), (unsigned long long)ts_pairs);
   if (lane == 0 && n_gather)
     atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_gather_rows), (unsigned long long)n_gather);
 }
@@ -1819,6 +1827,37 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_emit(const int32_t *__restric
   }
 }
 
+// One contribution's list -- n0 tile-0 ids of arena0 at s0 (a multiple of 8), then n1 other ids of arena1
+// at s1 (a multiple of 4): the user's parts are 16-B aligned -- copied by one wave to d[0, n0 + n1): 16-B
+// loads (8 or 4 ids), both parts' loads of a step issued before their stores.
+__device__ inline void wave_copy_list(const uint16_t *__restrict__ a0, const uint32_t *__restrict__ a1, uint32_t s0,
+                                      uint32_t n0, uint32_t s1, uint32_t n1, uint32_t *d, int lane) {
+  const uint4 *p0 = reinterpret_cast<const uint4 *>(a0 + s0);
+  const uint4 *p1 = reinterpret_cast<const uint4 *>(a1 + s1);
+  const uint32_t g0 = (n0 + 7u) >> 3, g1 = (n1 + 3u) >> 2, g = max(g0, g1);
+  for (uint32_t q = uint32_t(lane); q < g; q += 64u) {
+    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+    if (q < g0) v0 = p0[q];
+    if (q < g1) v1 = p1[q];
+    if (q < g0) {
+      const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t pos = 8u * q + uint32_t(i);
+        if (pos < n0) d[pos] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+      }
+    }
+    if (q < g1) {
+      const uint32_t w[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t pos = 4u * q + uint32_t(i);
+        if (pos < n1) d[n0 + pos] = w[i];
+      }
+    }
+  }
+}
+
 // ---- small rows: one 512-thread workgroup per row -----------------------------------------------------
 // A whole row of kTinyW < W <= kSmallW pairs -- at C3 the half million rows of the Zipf tail, each one LDS
 // hash chunk over every tile in k_sp_main (~20 us per chunk there, two chunks per CU) -- sorted instead: its
@@ -1925,14 +1964,25 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
     const int64_t k0 = it.k0, k1 = it.k1, e0 = A.epre[k0];
     const uint32_t W = uint32_t(A.epre[k1] - e0);
     const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
-    // 1. the lists, a wave per contribution, at their prefix positions (epre)
-    for (int64_t k = k0 + wave; k < k1; k += kSmallWaves) {
-      const int32_t *tbu = A.tb + int64_t(A.vals[k] & kListMask) * (A.T + 2);
-      const uint32_t s0 = uint32_t(tbu[0]), n0 = uint32_t(tbu[A.T + 1]) - s0;
-      const uint32_t s1 = uint32_t(tbu[1]), n1 = uint32_t(tbu[A.T]) - s1;
-      uint32_t *d = b0 + (A.epre[k] - e0);
-      for (uint32_t q = lane; q < n0; q += 64) d[q] = a0[s0 + q];
-      for (uint32_t q = lane; q < n1; q += 64) d[n0 + q] = a1[s1 + q];
+    // 1. the lists at their prefix positions (epre), a wave per contribution: wave w's contributions are
+    //    k0 + w + 8 j; lane j reads the j-th one's list bounds (all in one round of loads), then the wave
+    //    copies the lists one after another (wave_copy_list)
+    for (int64_t kb = k0 + wave; kb < k1; kb += int64_t(kSmallWaves) * 64) {
+      const int64_t km = kb + int64_t(kSmallWaves) * lane;
+      uint32_t m_s0 = 0, m_n0 = 0, m_s1 = 0, m_n1 = 0, m_d = 0;
+      if (km < k1) {
+        const int32_t *tbu = A.tb + int64_t(A.vals[km] & kListMask) * (A.T + 2);
+        m_s0 = uint32_t(tbu[0]);
+        m_n0 = uint32_t(tbu[A.T + 1]) - m_s0;
+        m_s1 = uint32_t(tbu[1]);
+        m_n1 = uint32_t(tbu[A.T]) - m_s1;
+        m_d = uint32_t(A.epre[km] - e0);
+      }
+      const int cnt = int(min<int64_t>(64, (k1 - kb + kSmallWaves - 1) / kSmallWaves));
+      for (int j = 0; j < cnt; j++)
+        wave_copy_list(a0, a1, uint32_t(__shfl(int(m_s0), j, 64)), uint32_t(__shfl(int(m_n0), j, 64)),
+                       uint32_t(__shfl(int(m_s1), j, 64)), uint32_t(__shfl(int(m_n1), j, 64)),
+                       b0 + uint32_t(__shfl(int(m_d), j, 64)), lane);
     }
     __syncthreads();
     // 2. radix sort
@@ -2169,19 +2219,23 @@ __global__ __launch_bounds__(kTinyThreads) void k_sp_tiny(SpArgs A) {
 // The overflow fallback of the per-row Int2ShortOpenHashMap (ItemRowAggregator.java:21-31) as an MSD radix
 // sort by hand: one 1,024-thread workgroup per deferred row.
 //  1. the first digit: the row's pairs are partitioned by column tile (kTW columns).  The tile histogram
-//     comes from the users' tile tables (tb: a list is already grouped by tile), so the partition is a set
-//     of contiguous segment copies into the row's scratch range; no id is read twice;
-//  2. every tile bucket, in column order, becomes (column, count) runs: a bucket of <= kSrbSort ids is
-//     bitonic-sorted in LDS and its runs counted (the segmented reduce of the +1 increments); a larger one
-//     is counted in kTW LDS counters (a counting sort of the last digit) and compacted in column order.  The
+//     comes from the users' tile tables (tb: a list is already grouped by tile); a wave per contribution
+//     reserves its tile segments in the buckets and copies the list with 16-B loads, every id to the
+//     bucket of its tile (its high bits) in the row's scratch range; no id is read twice;
+//  2. every tile bucket, in column order, becomes (column, count) runs: consecutive buckets of <= kSrbSort
+//     ids together are radix-sorted in LDS (block_radix_sort, by the offset in their tile range: two 7-bit
+//     passes for one tile) and their runs counted (the segmented reduce of the +1 increments); a larger
+//     bucket is counted in kTW LDS counters (a counting sort of the last digit) and compacted in column order.  The
 //     runs are written to the front of the row's scratch range (behind the buckets already consumed); the
 //     diagonal loses the row's self term (dropped at zero);
 //  3. the runs are copied to an exactly sized output slice (relabelled columns mapped back), with the
 //     row-sum check of the other paths.
 // ~16 B of HBM traffic per pair (segment copy 4 + 4, bucket read 4, run copy) against ~40 for the
 // library radix sort of 8-B keys.
-constexpr int kSrbThreads = 1024, kSrbWaves = kSrbThreads / 64, kSrbSort = 4096;
-static_assert(4 * kSrbSort <= kTW, "sort buffer, run starts, counts and columns share the bucket's LDS");
+constexpr int kSrbThreads = 1024, kSrbWaves = kSrbThreads / 64, kSrbSort = kSmallW;
+// buf: sort keys [0, kSrbSort], the other radix buffer from kSrbB, the radix histogram (u16) from kSrbH
+constexpr int kSrbB = kSrbSort + 8, kSrbH = kSrbB + kSrbSort + 8, kSrbUsed = kSrbH + (1 << kRadixBits) * kSrbWaves / 2;
+static_assert(kSrbUsed <= kTW, "the sort areas share the bucket's LDS counters");
 
 __device__ inline uint32_t srb_block_excl_scan(uint32_t x, uint32_t *total, uint32_t *s_wt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2200,27 +2254,31 @@ __device__ inline uint32_t srb_block_excl_scan(uint32_t x, uint32_t *total, uint
   return pre + inc - x;
 }
 
-__global__ __launch_bounds__(kSrbThreads) void k_srb_row(
-    const int32_t *__restrict__ rows, const int64_t *__restrict__ kbase, const int64_t *__restrict__ row_ptr,
+__global__ __launch_bounds__(kSrbThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_srb_row(
+    const int32_t *__restrict__ rows, int64_t n_rows, int64_t scr_stride, const int64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ vals, const int32_t *__restrict__ tb, const uint16_t *__restrict__ arena0,
     const uint32_t *__restrict__ arena1, int32_t T, int32_t Mc, uint32_t *__restrict__ scr_ids,
     uint32_t *__restrict__ scr_cnt, const int64_t *__restrict__ spre, const int64_t *__restrict__ rowsum,
     const int32_t *__restrict__ hot_col, const int32_t *__restrict__ pos_of, int32_t *__restrict__ col_out,
     uint32_t *__restrict__ cnt_out, unsigned long long *__restrict__ bump, int64_t cap,
-    int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, PlanTotals *__restrict__ tot) {
+    int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz, PlanTotals *__restrict__ tot,
+    unsigned long long *__restrict__ srb_st) {
   __shared__ uint32_t buf[kTW];  // dense counters | sorted bucket keys [0, kSrbSort) + run starts above
   __shared__ uint32_t s_hist[kSpMaxTiles + 1], s_off[kSpMaxTiles + 1], s_cur[kSpMaxTiles + 1];
   __shared__ uint32_t s_wt[kSrbWaves];
+  __shared__ int32_t s_wdst[kSrbWaves][kSpMaxTiles];  // per wave: a contribution's bucket positions by tile
   __shared__ uint32_t s_o;        // runs written so far (the row's entries)
   __shared__ int32_t s_drop;      // the bucket's run index of a diagonal that drops to zero (-1: none)
   __shared__ unsigned long long s_sum;
-  __shared__ int64_t s_base;
+  __shared__ int64_t s_base, s_j, s_scur, s_send;  // the row's output base; the dequeued row; the output slab
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int32_t j = blockIdx.x, a = rows[j];
-  const uint32_t ra = uint32_t(relabel_pos(pos_of, uint32_t(a)));
-  const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1], rb = kbase[j];
-  const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
+  // the workgroup's scratch range (every deferred row's pairs fit it); rows dequeued in deferral order
+  const int64_t rb = int64_t(blockIdx.x) * scr_stride;
   for (int i = tid; i < kTW; i += kSrbThreads) buf[i] = 0u;
+  if (tid == 0) s_scur = s_send = 0;
+  bool dirty = false;  // the sort areas of buf hold keys (the counting path needs zero counters)
+  for (;;) {
+  if (tid == 0) s_j = int64_t(atomicAdd(reinterpret_cast<unsigned long long *>(&tot->srb_ctr), 1ull));
   if (tid <= kSpMaxTiles) {
     s_hist[tid] = 0u;
     s_cur[tid] = 0u;
@@ -2230,84 +2288,124 @@ __global__ __launch_bounds__(kSrbThreads) void k_srb_row(
     s_sum = 0ull;
   }
   __syncthreads();
-  // 1a. the tile histogram from the tile tables: one thread per contribution
-  for (int64_t k = k0 + tid; k < k1; k += kSrbThreads) {
-    const int32_t *tbu = tb + int64_t(vals[k] & kListMask) * (T + 2);
-    const uint32_t n0 = uint32_t(tbu[T + 1] - tbu[0]);
-    if (n0) atomicAdd(&s_hist[0], n0);
-    int32_t prev = tbu[1];
-    for (int32_t t = 1; t < T; t++) {
-      const int32_t nx = tbu[t + 1];
-      if (nx > prev) atomicAdd(&s_hist[t], uint32_t(nx - prev));
-      prev = nx;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t run = 0;
-    for (int32_t t = 0; t < T; t++) {
-      s_off[t] = run;
-      run += s_hist[t];
-    }
-    s_off[T] = run;
-  }
-  __syncthreads();
-  // 1b. the partition: a wave per contribution; lane t >= 1 copies its tile's segment (a few ids), the whole
-  // wave the tile-0 segment (the Zipf head: most of the list, u16)
+  const int64_t j = uni(s_j);
+  if (j >= n_rows) break;
+  const int32_t a = rows[j];
+  const uint32_t ra = uint32_t(relabel_pos(pos_of, uint32_t(a)));
+  const int64_t k0 = row_ptr[a], k1 = row_ptr[a + 1];
+  const uint32_t self = uint32_t(spre ? spre[k1] - spre[k0] : k1 - k0);
+  const unsigned long long c_0 = STAT_CLOCK();
+  SRB_STAT(5, 1);
+  SRB_STAT(6, k1 - k0);
+  // 1a. the tile histogram from the tile tables: a wave per contribution, lane t its tile t
   for (int64_t k = k0 + wave; k < k1; k += kSrbWaves) {
     const int32_t *tbu = tb + int64_t(vals[k] & kListMask) * (T + 2);
-    if (lane >= 1 && lane < T) {
-      const int32_t s1 = tbu[lane], e1 = tbu[lane + 1];
-      if (e1 > s1) {
-        const uint32_t d = atomicAdd(&s_cur[lane], uint32_t(e1 - s1));
-        uint32_t *dst = scr_ids + rb + s_off[lane] + d;
-        for (int32_t q = s1; q < e1; q++) dst[q - s1] = arena1[q];
+    if (lane < T) {
+      const int32_t n_t = lane == 0 ? tbu[T + 1] - tbu[0] : tbu[lane + 1] - tbu[lane];
+      if (n_t > 0) atomicAdd(&s_hist[lane], uint32_t(n_t));
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {  // bucket starts: a wave scan of the T <= 64 tile counts
+    const uint32_t h = lane < T ? s_hist[lane] : 0u, inc = wave_incl_scan(h);
+    if (lane < T) s_off[lane] = inc - h;
+    if (lane == T - 1) s_off[T] = inc;
+  }
+  __syncthreads();
+  const unsigned long long c_1 = STAT_CLOCK();
+  SRB_STAT(0, c_1 - c_0);
+  // 1b. the partition, a wave per contribution: lane t reserves its tile's segment in bucket t; then the
+  // wave copies the list with 16-B loads -- the tile-0 part (u16) to bucket 0, the other part (u32, tiles
+  // in order) id by id to the bucket of the id's tile (the tile is the id's high bits)
+  int32_t *wdst = s_wdst[wave];
+  for (int64_t k = k0 + wave; k < k1; k += kSrbWaves) {
+    const int32_t *tbu = tb + int64_t(vals[k] & kListMask) * (T + 2);
+    const int32_t s0 = tbu[0], n0 = tbu[T + 1] - s0, s1 = tbu[1], n1 = tbu[T] - s1;
+    if (lane < T) {
+      const int32_t st = lane == 0 ? s0 : tbu[lane];
+      const int32_t n_t = lane == 0 ? n0 : tbu[lane + 1] - st;
+      const uint32_t d = n_t > 0 ? atomicAdd(&s_cur[lane], uint32_t(n_t)) : 0u;
+      // bucket position of the part's position q: wdst[t] + q
+      wdst[lane] = int32_t(s_off[lane] + d) - (lane == 0 ? 0 : st - s1);
+    }
+    tiny_sync();
+    const uint4 *p0 = reinterpret_cast<const uint4 *>(arena0 + s0);
+    const uint4 *p1 = reinterpret_cast<const uint4 *>(arena1 + s1);
+    const uint32_t g0 = (uint32_t(n0) + 7u) >> 3, g1 = (uint32_t(n1) + 3u) >> 2, g = max(g0, g1);
+    uint32_t *dst0 = scr_ids + rb + wdst[0];
+    for (uint32_t q = uint32_t(lane); q < g; q += 64u) {
+      uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+      if (q < g0) v0 = p0[q];
+      if (q < g1) v1 = p1[q];
+      if (q < g0) {
+        const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint32_t pos = 8u * q + uint32_t(i);
+          if (pos < uint32_t(n0)) dst0[pos] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        }
+      }
+      if (q < g1) {
+        const uint32_t w[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t pos = 4u * q + uint32_t(i);
+          if (pos < uint32_t(n1)) scr_ids[rb + wdst[w[i] >> kTShift] + int32_t(pos)] = w[i];
+        }
       }
     }
-    const int32_t s0 = tbu[0], n0 = tbu[T + 1] - s0;
-    if (n0 > 0) {
-      uint32_t d = 0;
-      if (lane == 0) d = atomicAdd(&s_cur[0], uint32_t(n0));
-      d = __shfl(d, 0, 64);
-      uint32_t *dst = scr_ids + rb + s_off[0] + d;
-      for (int32_t q = lane; q < n0; q += 64) dst[q] = arena0[s0 + q];
-    }
+    tiny_sync();  // (wdst is rewritten for the wave's next contribution)
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the buckets are read back by other waves)
+  const unsigned long long c_2 = STAT_CLOCK();
+  SRB_STAT(1, c_2 - c_1);
+  SRB_STAT(7, s_off[T]);
   // 2. the buckets in column order
   uint64_t sum = 0;
-  for (int32_t t = 0; t < T; t++) {
+  for (int32_t t = 0; t < T;) {
     const uint32_t n = uni(s_hist[t]);
-    if (n == 0) continue;
-    const uint32_t *src = scr_ids + rb + s_off[t];
+    if (n == 0) {
+      t++;
+      continue;
+    }
     const uint32_t o = uni(s_o);
     const uint32_t c0 = uint32_t(t) * uint32_t(kTW);
     if (n <= uint32_t(kSrbSort)) {
-      // bitonic sort of the bucket in LDS, then its runs
-      uint32_t P = 64;
-      while (P < n) P <<= 1;
-      for (uint32_t i = tid; i < P; i += kSrbThreads) buf[i] = i < n ? src[i] : 0xFFFFFFFFu;
-      __syncthreads();
-      for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-          for (uint32_t q = tid; q < P / 2; q += kSrbThreads) {
-            const uint32_t lo = 2 * q - (q & (jj - 1)), hi = lo + jj;
-            const uint32_t x = buf[lo], y = buf[hi];
-            if ((x > y) == ((lo & kk) == 0)) {
-              buf[lo] = y;
-              buf[hi] = x;
-            }
-          }
-          __syncthreads();
+      // a group: this bucket and the next ones while they fit kSrbSort ids together (contiguous in the
+      // scratch), radix-sorted in LDS by their offset in the group's tile range, then its runs
+      const unsigned long long c_g = STAT_CLOCK();
+      uint32_t g = n;
+      int32_t t1 = t + 1;
+      while (t1 < T && g + uni(s_hist[t1]) <= uint32_t(kSrbSort)) g += uni(s_hist[t1++]);
+      const uint32_t *src = scr_ids + rb + s_off[t];
+      uint32_t *ka = buf, *kb = buf + kSrbB;
+      {
+        static_assert(kSrbSort == 4 * kSrbThreads, "four keys per thread");
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t i = uint32_t(tid) + uint32_t(u) * kSrbThreads;
+          v[u] = i < g ? src[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t i = uint32_t(tid) + uint32_t(u) * kSrbThreads;
+          if (i < g) ka[i] = v[u] - c0;
         }
       }
-      // run heads: thread tid owns positions 4 tid .. 4 tid + 3 (n <= 4096)
+      __syncthreads();
+      int bits = kTShift;
+      while ((uint32_t(t1 - t) << kTShift) > (1u << bits)) bits++;
+      const uint32_t *ks = block_radix_sort<kSrbThreads>(ka, kb, reinterpret_cast<uint16_t *>(buf + kSrbH), s_wt, g,
+                                                         bits);
+      uint32_t *st = ks == ka ? kb : ka;  // run starts in the free area (+1: the end marker)
+      dirty = true;
       uint32_t hm = 0;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         const uint32_t i = 4u * uint32_t(tid) + uint32_t(e);
-        if (i < n && (i == 0 || buf[i] != buf[i - 1])) hm |= 1u << e;
+        if (i < g && (i == 0 || ks[i] != ks[i - 1])) hm |= 1u << e;
       }
       uint32_t n_runs;
       const uint32_t r0 = srb_block_excl_scan(uint32_t(__popc(hm)), &n_runs, s_wt);
@@ -2316,37 +2414,50 @@ __global__ __launch_bounds__(kSrbThreads) void k_srb_row(
         uint32_t r = r0;
 #pragma unroll
         for (int e = 0; e < 4; e++)
-          if ((hm >> e) & 1u) buf[kSrbSort + r++] = 4u * uint32_t(tid) + uint32_t(e);
+          if ((hm >> e) & 1u) st[r++] = 4u * uint32_t(tid) + uint32_t(e);
       }
+      if (tid == 0) st[n_runs] = g;
       __syncthreads();
       for (uint32_t r = tid; r < n_runs; r += kSrbThreads) {
-        const uint32_t st = buf[kSrbSort + r], en = r + 1 < n_runs ? buf[kSrbSort + r + 1] : n;
-        const uint32_t col = buf[st];
-        uint32_t c = en - st;
+        const uint32_t p = st[r], c = st[r + 1] - p;
         sum += c;
-        if (col == ra) {
-          c -= self;
-          if (c == 0u) s_drop = int32_t(r);
-        }
-        buf[2 * kSrbSort + r] = c;    // (n_runs <= kSrbSort: counts and columns in the areas above the starts)
-        buf[3 * kSrbSort + r] = col;
+        if (ks[p] + c0 == ra && c == self) s_drop = int32_t(r);
       }
       __syncthreads();
       const int32_t drop = uni(s_drop);
       for (uint32_t r = tid; r < n_runs; r += kSrbThreads) {
         if (int32_t(r) == drop) continue;
+        const uint32_t p = st[r], c = st[r + 1] - p, col = ks[p] + c0;
         const uint32_t q = o + r - (drop >= 0 && int32_t(r) > drop ? 1u : 0u);
-        scr_ids[rb + q] = buf[3 * kSrbSort + r];
-        scr_cnt[rb + q] = buf[2 * kSrbSort + r];
+        scr_ids[rb + q] = col;
+        scr_cnt[rb + q] = c - (col == ra ? self : 0u);
       }
-      __syncthreads();
-      for (uint32_t i = tid; i < uint32_t(kTW); i += kSrbThreads) buf[i] = 0u;
       if (tid == 0) s_o = o + n_runs - (drop >= 0 ? 1u : 0u);
       __syncthreads();
+      SRB_STAT(2, STAT_CLOCK() - c_g);
+      SRB_STAT(8, 1);
+      t = t1;
     } else {
       // counting sort of the bucket's last digit: kTW LDS counters, then a column-order compaction
+      const unsigned long long c_c = STAT_CLOCK();
+      if (dirty) {
+        for (uint32_t i = tid; i < uint32_t(kSrbUsed); i += kSrbThreads) buf[i] = 0u;
+        dirty = false;
+        __syncthreads();
+      }
+      const uint32_t *src = scr_ids + rb + s_off[t];
       const uint32_t w = uint32_t(min(int64_t(kTW), int64_t(Mc) - int64_t(c0)));
-      for (uint32_t i = tid; i < n; i += kSrbThreads) atomicAdd(&buf[src[i] - c0], 1u);
+      for (uint32_t i0 = 0; i0 < n; i0 += 8u * kSrbThreads) {  // (8 loads in flight per thread)
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t i = i0 + uint32_t(tid) + uint32_t(u) * kSrbThreads;
+          v[u] = i < n ? src[i] : kSink;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (v[u] != kSink) atomicAdd(&buf[v[u] - c0], 1u);
+      }
       __syncthreads();
       if (tid == 0 && ra >= c0 && ra < c0 + w) buf[ra - c0] -= self;  // (the self pairs were counted too)
       __syncthreads();
@@ -2377,21 +2488,37 @@ __global__ __launch_bounds__(kSrbThreads) void k_srb_row(
         if (ra >= c0 && ra < c0 + w) sum += self;  // (sum counts the self pairs on both paths)
       }
       __syncthreads();
+      SRB_STAT(3, STAT_CLOCK() - c_c);
+      SRB_STAT(9, 1);
+      t++;
     }
   }
+  const unsigned long long c_3 = STAT_CLOCK();
   // 3. the exact output slice; the row-sum check
   for (int x = 32; x > 0; x >>= 1) sum += __shfl_xor(sum, x, 64);
   if (lane == 0 && sum) atomicAdd(&s_sum, (unsigned long long)sum);
   __syncthreads();
   const uint32_t d = s_o;
   if (tid == 0) {
-    int64_t b = d ? int64_t(atomicAdd(bump, (unsigned long long)d)) : 0;
-    if (b + int64_t(d) > cap) {
-      atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 4ull);
-      b = -1;
+    // the row's slice from the workgroup's output slab (a new slab of >= kSmallSlab entries when it is short)
+    int64_t b = -1;
+    if (s_scur + int64_t(d) > s_send) {
+      const int64_t take = max<int64_t>(kSmallSlab, int64_t(d));
+      const int64_t nb = int64_t(atomicAdd(bump, (unsigned long long)take));
+      if (nb + take > cap) {
+        atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 4ull);
+        s_scur = s_send = 0;
+      } else {
+        s_scur = nb;
+        s_send = nb + take;
+      }
+    }
+    if (s_scur + int64_t(d) <= s_send) {
+      b = s_scur;
+      s_scur += d;
     }
     s_base = b;
-    row_base[a] = b < 0 ? 0 : b;
+    row_base[a] = (b < 0 || d == 0) ? 0 : b;
     row_nnz[a] = b < 0 ? 0 : int32_t(d);
     if (s_sum != (unsigned long long)(rowsum[a] + self)) {
       atomicOr(reinterpret_cast<unsigned long long *>(&tot->err), 2ull);
@@ -2401,10 +2528,28 @@ __global__ __launch_bounds__(kSrbThreads) void k_srb_row(
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int64_t base = s_base;
-  if (base < 0) return;
-  for (uint32_t i = tid; i < d; i += kSrbThreads) {
-    col_out[base + i] = relabel_col(hot_col, scr_ids[rb + i]);
-    cnt_out[base + i] = scr_cnt[rb + i];
+  (void)c_3;
+  for (uint32_t i0 = 0; base >= 0 && i0 < d; i0 += 4u * kSrbThreads) {  // (4 entries' loads in flight per thread)
+    uint32_t c[4], n[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t i = i0 + uint32_t(tid) + uint32_t(u) * kSrbThreads;
+      c[u] = i < d ? scr_ids[rb + i] : 0u;
+      n[u] = i < d ? scr_cnt[rb + i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t i = i0 + uint32_t(tid) + uint32_t(u) * kSrbThreads;
+      if (i < d) {
+        col_out[base + i] = relabel_col(hot_col, c[u]);
+        cnt_out[base + i] = n[u];
+      }
+    }
+  }
+  SRB_STAT(4, STAT_CLOCK() - c_3);
+  SRB_STAT(10, STAT_CLOCK() - c_0);
+  __builtin_amdgcn_s_waitcnt(0);  // (the next row's partition rewrites the scratch these loads read)
+  __syncthreads();
   }
 }
 
@@ -2679,7 +2824,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                             sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
                                             order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
-                                            row_base_.as<int64_t>(), tot, spre, sort_rows_ ? 0 : small_off_ ? 1 : 3);
+                                            row_base_.as<int64_t>(), tot, spre, small_off_ ? 1 : 3);
   k_sp_totals<<<1, 1, 0, s>>>(tot, epre, spre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
@@ -2759,7 +2904,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   const int64_t n_small = h_tot_->n_small;
   const int64_t grid_small = std::min<int64_t>(n_small, int64_t(n_cu_) * 4);
   const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0) +
-                        (n_small ? grid_small * kSmallSlab : 0);
+                        (n_small ? grid_small * kSmallSlab : 0) + 2 * int64_t(n_cu_) * kSmallSlab;  // (+ k_srb_row)
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
   cap = std::max<int64_t>(1, std::min(cap, budget));
@@ -2876,8 +3021,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipStreamSynchronize(s));
     int64_t err = h_tot_->err;
     const int64_t n_def = h_tot_->n_deferred;
-    last_deferred_ = n_def;
-    last_deferred_pairs_ = 0;
+    // (COOC_FLAG_SORT_ROWS: every whole row is sorted -- the tiny and small rows by k_sp_tiny / k_sp_small, the
+    // others by the sort path)
+    last_deferred_ = n_def + (sort_rows_ ? h_tot_->n_tiny + h_tot_->n_small : 0);
+    last_deferred_pairs_ = sort_rows_ ? h_tot_->ts_pairs : 0;
     if (n_def > 0 && !(err & 4)) {  // rows whose hash table overflowed (all whole rows: COOC_FLAG_SORT_ROWS)
       COOC_TRY(run_deferred(n_def, T, row_ptr, epre, vals, spre, cap, s));
       COOC_HIP_TRY(hipMemcpyAsync(&err, &tot->err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -2975,30 +3122,43 @@ Status Counter::run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, c
   }
   const int64_t nk = std::max<int64_t>(max_batch, 1);
   if (!srb_hipcub_) {
-    // the hand-written path (k_srb_row): the batch's pairs as u32 ids + u32 run counts in scratch
-    COOC_TRY(sr_keys_.reserve(sizeof(uint32_t) * size_t(2 * nk)));
-    uint32_t *ids = sr_keys_.as<uint32_t>(), *cn = ids + nk;
-    std::vector<int64_t> kb;
-    for (int64_t j0 = 0; j0 < n_def;) {
-      int64_t j1 = j0, acc = 0;
-      kb.assign(1, 0);
-      while (j1 < n_def && (j1 == j0 || acc + w[size_t(j1)] <= budget)) {
-        acc += w[size_t(j1)];
-        kb.push_back(acc);
-        j1++;
-      }
-      last_deferred_pairs_ += acc;
-      int64_t *kbase = d_w + n_def + 2;
-      COOC_HIP_TRY(hipMemcpyAsync(kbase, kb.data(), sizeof(int64_t) * kb.size(), hipMemcpyHostToDevice, s));
-      k_srb_row<<<unsigned(j1 - j0), kSrbThreads, 0, s>>>(
-          rows + j0, kbase, row_ptr, vals, sp_tb_.as<int32_t>(), sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), T,
-          last_mc_, ids, cn, spre, rowsum_.as<int64_t>(), last_hot_col_, last_pos_of_, col_.as<int32_t>(),
-          cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
-          tot_.as<PlanTotals>());
-      COOC_HIP_TRY(hipGetLastError());
-      COOC_HIP_TRY(hipStreamSynchronize(s));  // (kb is reused by the next batch's upload)
-      j0 = j1;
+    // the hand-written path (k_srb_row): persistent workgroups (two per CU) take the rows in deferral order;
+    // each has a scratch range for the largest row's pairs as u32 ids + u32 run counts
+    int64_t max_w = 1;
+    for (int64_t j = 0; j < n_def; j++) {
+      max_w = std::max(max_w, w[size_t(j)]);
+      last_deferred_pairs_ += w[size_t(j)];
     }
+    const int64_t stride = (max_w + 63) & ~int64_t(63);
+    int64_t grid = std::min<int64_t>(n_def, 2 * int64_t(n_cu_));
+    grid = std::max<int64_t>(1, std::min<int64_t>(grid, int64_t(f0 / 2) / (8 * stride)));
+    COOC_TRY(sr_keys_.reserve(sizeof(uint32_t) * size_t(2 * grid * stride)));
+    uint32_t *ids = sr_keys_.as<uint32_t>(), *cn = ids + grid * stride;
+    unsigned long long *srb_st = nullptr;
+#ifdef COOC_SP_STATS
+    static unsigned long long *d_srb = nullptr;
+    if (!d_srb) COOC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_srb), 16 * 8));
+    COOC_HIP_TRY(hipMemsetAsync(d_srb, 0, 16 * 8, s));
+    srb_st = d_srb;
+#endif
+    PlanTotals *tot = tot_.as<PlanTotals>();
+    COOC_HIP_TRY(hipMemsetAsync(&tot->srb_ctr, 0, sizeof(int64_t), s));
+    k_srb_row<<<unsigned(grid), kSrbThreads, 0, s>>>(
+        rows, n_def, stride, row_ptr, vals, sp_tb_.as<int32_t>(), sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), T,
+        last_mc_, ids, cn, spre, rowsum_.as<int64_t>(), last_hot_col_, last_pos_of_, col_.as<int32_t>(),
+        cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), tot,
+        srb_st);
+    COOC_HIP_TRY(hipGetLastError());
+#ifdef COOC_SP_STATS
+    {
+      unsigned long long h[16];
+      COOC_HIP_TRY(hipMemcpy(h, srb_st, sizeof(h), hipMemcpyDeviceToHost));
+      const double r = h[5] ? double(h[5]) : 1.0;
+      fprintf(stderr, "[srb stats] rows %llu contributions %llu pairs %llu | per row (us): hist %.1f partition %.1f "
+              "sort groups %.1f (%llu) counting %.1f (%llu) output %.1f total %.1f\n", h[5], h[6], h[7], h[0] / 100.0 / r,
+              h[1] / 100.0 / r, h[2] / 100.0 / r, h[8], h[3] / 100.0 / r, h[9], h[4] / 100.0 / r, h[10] / 100.0 / r);
+    }
+#endif
     return Status::Ok();
   }
   COOC_TRY(sr_keys_.reserve(sizeof(uint64_t) * size_t(2 * nk)));
