@@ -333,7 +333,31 @@ def main():
     if args.config == "c5":
         out["config"]["topk"] = args.topk
         out["config"]["output"] += f"; top-{args.topk} heaps (sizes, values, scores) per row in HBM"
-        out["topk_ms"] = float(np.median(topk_ms))
+        out["topk_ms"] = tk = float(np.median(topk_ms))
+        # the rescoring pass (cooc_topk_batch_device: k_col_terms + k_rescore) against its own bytes: every
+        # entry streamed once (col + cnt, 8 B), the per-row CSR header and row sums (20 B per row), the heaps
+        # written (sizes 4 B + k x (value 4 B + score 8 B) per row); the per-column LLR terms it gathers are
+        # counted once (32 B per column) -- their re-reads hit L2 / the Infinity Cache
+        pmc_rs = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_rescore.json"))
+        rs_stale = bool(pmc_rs) and pmc_rs.get("source_digest") != digest
+        if rs_stale:
+            pmc_rs = {"kernel": "k_rescore", "stale_source_digest": pmc_rs.get("source_digest")}
+        b_rs = 8.0 * D + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
+        a_rs = b_rs / (tk * 1e-3) / 1e9
+        t_rs = pmc_rs.get("hbm_bytes_per_launch")
+        out["roofline_rescore"] = {
+            "bound": "hbm", "kernel": "k_col_terms+k_rescore", "achieved": a_rs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": a_rs / HBM_PEAK_GBPS, "traffic": t_rs, "kernel_ms": tk, "algorithmic_bytes_per_launch": b_rs,
+            "units_per_launch": {"entries": D, "rows": M, "topk": args.topk},
+            "traffic_gbps": (t_rs / (tk * 1e-3) / 1e9) if t_rs else None,
+            "l2_hit_rate": pmc_rs.get("l2_hit_rate"), "wave_wait_frac": pmc_rs.get("wave_wait_frac"),
+            "valu_busy": pmc_rs.get("valu_busy"), "limiter": limiter(pmc_rs, t_rs, tk),
+            "pmc_source_digest": pmc_rs.get("source_digest") or pmc_rs.get("stale_source_digest"),
+            "pmc_stale": rs_stale,
+            "note": "B = 8D + 20M + M(4 + 12k) + 32M per launch (entries streamed, row headers and sums, heaps, "
+                    "column terms), over the HIP-event time of the rescoring call; its limiter is f64 log "
+                    "throughput (DESIGN.md §4), so frac is low by construction",
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if large:
             bu, bi = datagen.c3_users(0, 200_000, permute=args.permute_items)

@@ -247,7 +247,7 @@ class Counter {
   // batch windows of the large-universe path: columns relabelled by descending frequency (off: column ids,
   // COOC_FLAG_COLUMN_ORDER); the last run's maps (NULL without a relabel)
   bool relabel_ = true;
-  DevBuf sp_rank_, sp_rkeys_;
+  DevBuf sp_rank_, sp_rkeys_, sp_bits_;  // (sp_bits_: the hot-column and owned-row bitmaps of the user passes)
   const int32_t *last_hot_col_ = nullptr, *last_pos_of_ = nullptr;
   int32_t last_mc_ = 0;       // columns of the last run's (relabelled) space
   // deferred rows through the library radix sort (COOC_SR_HIPCUB=1, A/B) instead of k_srb_row

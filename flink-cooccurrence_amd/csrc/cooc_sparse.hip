@@ -261,6 +261,15 @@ __device__ inline int32_t sp_split_shares(int64_t W, float g0) {
 constexpr uint32_t kSink = 0xFFFFFFFFu;
 constexpr uint32_t kSink16 = 0xFFFFu;  // (arena0 pads; never a tile-0 id)
 
+__device__ inline bool bit_of(const uint32_t *__restrict__ bits, uint32_t i) { return (bits[i >> 5] >> (i & 31u)) & 1u; }
+
+// An id's column after the relabel: a hot id's position in tile 0 (pos_of, gathered), any other id + kTW
+// (arithmetic); without a relabel the id itself.
+__device__ inline int32_t planner_rank(const int32_t *__restrict__ pos_of, const uint32_t *__restrict__ hotbm, uint32_t it) {
+  if (!pos_of) return int32_t(it);
+  return bit_of(hotbm, it) ? pos_of[it] : int32_t(it) + kTW;
+}
+
 // The arenas' user regions, packed and dense: one wave per user counts its tile-0 ids (ballots) and
 // writes len[j] = round8(tile-0 ids) << 32 | round4(other ids); their inclusive prefix (one scan) gives
 // every user's base in arena0 (high half) and arena1 (low half).
@@ -268,7 +277,9 @@ __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t
                                                         const int32_t *__restrict__ items, int32_t M,
                                                         uint64_t *__restrict__ len, const int32_t *__restrict__ owner,
                                                         int32_t part, int32_t *__restrict__ ownc,
-                                                        const int32_t *__restrict__ rank_of) {
+                                                        const int32_t *__restrict__ rank_of,
+                                                        const uint32_t *__restrict__ hotbm,
+                                                        const uint32_t *__restrict__ minebm) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -284,9 +295,10 @@ __global__ __launch_bounds__(256) void k_sp_tile_counts(int64_t U, const int64_t
       for (int k = 0; k < 4; k++) {  // (an invalid id goes to tile 0 in k_sp_tile_lists, which reports it)
         const bool in = p0 + 64 * k + lane < n;
         const bool valid = uint32_t(it[k]) < uint32_t(M);
-        const uint32_t rk = valid ? uint32_t(relabel_pos(rank_of, uint32_t(it[k]))) : uint32_t(it[k]);
-        n0 += int32_t(__popcll(__ballot(in && (rk < uint32_t(kTW) || !valid))));
-        if (owner) mine += int32_t(__popcll(__ballot(valid && owner[it[k]] == part)));
+        // (tile 0: a hot id after a relabel -- a bit -- else an id below kTW)
+        const bool t0 = !valid || (rank_of ? bit_of(hotbm, uint32_t(it[k])) : uint32_t(it[k]) < uint32_t(kTW));
+        n0 += int32_t(__popcll(__ballot(in && t0)));
+        if (owner) mine += int32_t(__popcll(__ballot(valid && bit_of(minebm, uint32_t(it[k])))));
       }
     }
     if (lane == 0) {
@@ -311,7 +323,9 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
                                                        uint32_t *__restrict__ keys,
                                                        uint32_t *__restrict__ vals, const int32_t *__restrict__ owner,
                                                        int32_t part, const int64_t *__restrict__ ownoff,
-                                                       PlanTotals *__restrict__ tot, const int32_t *__restrict__ rank_of) {
+                                                       PlanTotals *__restrict__ tot, const int32_t *__restrict__ rank_of,
+                                                       const uint32_t *__restrict__ hotbm,
+                                                       const uint32_t *__restrict__ minebm) {
   __shared__ int32_t cur[4][kSpMaxTiles + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int32_t *c = cur[wave];
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
           vals[s + p] = uint32_t(j);
         }
       } else {
-        const bool m = in && valid && owner[it] == part;
+        const bool m = in && valid && bit_of(minebm, uint32_t(it));
         const uint64_t bal = __ballot(m);
         if (m && keys) {
           keys[o + __popcll(bal & lt)] = uint32_t(it);
@@ -369,7 +383,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
     for (int k = 0; k < kTlR; k++) {
       valid[k] = uint32_t(r[k]) < uint32_t(M);
       if (!valid[k]) r[k] = 0;
-      rk[k] = lane + 64 * k < n ? relabel_pos(rank_of, uint32_t(r[k])) : r[k];
+      rk[k] = lane + 64 * k < n ? planner_rank(rank_of, hotbm, uint32_t(r[k])) : r[k];
     }
 #pragma unroll
     for (int k = 0; k < kTlR; k++) count(lane + 64 * k < n, lane + 64 * k, r[k], rk[k], valid[k]);
@@ -381,7 +395,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
         bad = true;
         it = 0;
       }
-      count(p < n, p, it, p < n ? relabel_pos(rank_of, uint32_t(it)) : it, v);
+      count(p < n, p, it, p < n ? planner_rank(rank_of, hotbm, uint32_t(it)) : it, v);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -430,7 +444,7 @@ __global__ __launch_bounds__(256) void k_sp_tile_lists(int64_t U, const int64_t 
       const int32_t p = p0 + lane;
       int32_t it = p < n ? items[s + p] : 0;
       if (uint32_t(it) >= uint32_t(M)) it = 0;
-      place(p < n, p < n ? relabel_pos(rank_of, uint32_t(it)) : it);
+      place(p < n, p < n ? planner_rank(rank_of, hotbm, uint32_t(it)) : it);
     }
     if (lane < ((n0 + 7) & ~7) - n0) o0[n0 + lane] = uint16_t(kSink16);  // (<= 7 pads)
     if (lane < ((n1 + 3) & ~3) - n1) o1[n1 + lane] = kSink;              // (<= 3 pads)
@@ -508,6 +522,26 @@ __global__ void k_rank_keys(const int64_t *__restrict__ row_ptr, const int64_t *
 __global__ void k_hot_mark(const int32_t *__restrict__ order, int32_t h, uint8_t *__restrict__ hot) {
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < h) hot[order[r]] = 1;
+}
+
+// Bitmaps over item ids for the planner's per-interaction passes: a 4-B gather per interaction into an
+// M-entry table is one L2 request per lane (the passes over a whole 1e9-interaction log are bound by that
+// request rate), a bit lookup into an M-bit table shares lines between the lanes (the hot ids' bits sit in
+// few lines).  hot: the ids of tile 0 after a relabel; mine: the rows a part owns.
+__global__ void k_bits_hot(const uint8_t *__restrict__ hot, int32_t M, uint32_t *__restrict__ bits) {
+  const int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w * 32 >= M) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 32 && w * 32 + b < M; b++) v |= uint32_t(hot[w * 32 + b] != 0) << b;
+  bits[w] = v;
+}
+
+__global__ void k_bits_owner(const int32_t *__restrict__ owner, int32_t part, int32_t M, uint32_t *__restrict__ bits) {
+  const int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w * 32 >= M) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 32 && w * 32 + b < M; b++) v |= uint32_t(owner[w * 32 + b] == part) << b;
+  bits[w] = v;
 }
 
 struct IsHot {
@@ -2700,6 +2734,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 
   const int64_t waves = std::min<int64_t>(std::max<int64_t>(U, 1), 65536);
   int32_t *hot_col = nullptr, *pos_of = nullptr;
+  const uint8_t *hot_u8 = nullptr;    // 1 per hot id (tile 0 after the relabel)
   const int64_t *freq_col = nullptr;  // the frequencies in relabelled column order (the planner's estimate)
   bool sorted_early = false;          // contributions sorted ahead of the relabel (no owner)
   if (relabel) {
@@ -2738,6 +2773,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceSelect::If(sort_tmp_.p, b, from0, hot_col, n_sel, M, IsHot{hot}, s));  // kTW of them
     k_relabel_pos<<<nblocks(M, 256), 256, 0, s>>>(hot, rk_in, M, pos_of, fc);
+    hot_u8 = hot;
     k_relabel_hot<<<nblocks(kTW, 256), 256, 0, s>>>(hot_col, rk_in, pos_of, fc);
     COOC_HIP_TRY(hipGetLastError());
     freq_col = fc;
@@ -2745,6 +2781,13 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   last_hot_col_ = hot_col;
   last_pos_of_ = pos_of;
   last_mc_ = Mc;
+  // the bitmaps of the user passes (hot ids after a relabel; the part's rows)
+  const int64_t n_words = (int64_t(M) + 31) / 32;
+  COOC_TRY(sp_bits_.reserve(sizeof(uint32_t) * size_t(2 * n_words + 2)));
+  uint32_t *hotbm = relabel ? sp_bits_.as<uint32_t>() : nullptr;
+  uint32_t *minebm = owner ? sp_bits_.as<uint32_t>() + n_words : nullptr;
+  if (hotbm) k_bits_hot<<<nblocks(n_words, 256), 256, 0, s>>>(hot_u8, M, hotbm);
+  if (minebm) k_bits_owner<<<nblocks(n_words, 256), 256, 0, s>>>(owner, part, M, minebm);
   // 1. per-user tile regrouping + the (item, user) contributions (owner != NULL: of this part's rows)
   if (owner) {
     COOC_TRY(sp_ownc_.reserve(sizeof(int32_t) * size_t(U1)));
@@ -2753,7 +2796,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_HIP_TRY(hipMemsetAsync(pbase, 0, sizeof(uint64_t), s));
   if (U > 0) {
     k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen, owner, part,
-                                                             sp_ownc_.as<int32_t>(), pos_of);
+                                                             sp_ownc_.as<int32_t>(), pos_of, hotbm, minebm);
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
   }
@@ -2773,7 +2816,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     k_sp_tile_lists<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, T, sp_tb_.as<int32_t>(),
                                                             sp_arena0_.as<uint16_t>(), sp_arena_.as<uint32_t>(), pbase,
                                                             (win || sorted_early) ? nullptr : keys_in, vals_in, owner,
-                                                            part, ownoff, tot, pos_of);
+                                                            part, ownoff, tot, pos_of, hotbm, minebm);
     COOC_HIP_TRY(hipGetLastError());
   }
   int64_t n_c = n;  // contributions: every interaction, or those of the owned rows, or a window's positions

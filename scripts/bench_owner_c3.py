@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--parts", default="0", help="comma-separated ranks to time")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--permute", action="store_true", help="item ids permuted (datagen.c3_item_perm)")
     args = ap.parse_args()
     import torch
 
@@ -35,7 +36,7 @@ def main():
     ups, its = [], []
     base = 0
     for r in range(args.world):
-        up, it = datagen.c3_users(r * U8, (r + 1) * U8, device=dev)
+        up, it = datagen.c3_users(r * U8, (r + 1) * U8, device=dev, permute=args.permute)
         ups.append(up[:-1] + base)
         its.append(it)
         base += int(up[-1].item())
@@ -58,7 +59,8 @@ def main():
     freq = core.item_counts(it)
     owner = sharding.snake_owner(freq, args.world)
     out = {"config": f"C3 rank compute at N={args.world}: all {args.world * U8} users ({N} interactions) after the "
-                     f"all-gather, rows owned by snake_owner(freq, {args.world})", "parts": {}}
+                     f"all-gather, rows owned by snake_owner(freq, {args.world})", "permuted_ids": args.permute,
+           "parts": {}}
     P_all = 0
     for part in [int(x) for x in args.parts.split(",")]:
         ms, kms = [], []

@@ -36,6 +36,9 @@ if "TCC_HIT_sum" in avg:
 if "SQ_LDS_IDX_ACTIVE" in avg and "GRBM_GUI_ACTIVE" in avg:
     res["lds_util"] = avg["SQ_LDS_IDX_ACTIVE"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 256)
     res["lds_bank_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"]
+if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+    # VALU wave-instructions issued per SIMD-cycle (1,024 SIMDs; GRBM_GUI_ACTIVE summed over the 8 XCDs)
+    res["valu_busy"] = avg["SQ_INSTS_VALU"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
 if "SQ_WAIT_ANY" in avg:
     res["wave_wait_frac"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
 # the code the counters belong to: bench.py reports traffic / limiter only when its own source digest matches
