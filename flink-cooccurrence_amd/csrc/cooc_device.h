@@ -243,6 +243,7 @@ class Counter {
   // sort + segmented-reduce path of deferred rows: the deferred list, keys (x2), runs, per-batch tables
   DevBuf sp_defer_, sr_keys_, sr_ukeys_, sr_ucnt_, sr_aux_;
   int64_t last_deferred_ = 0, last_deferred_pairs_ = 0;
+  int32_t last_hot_overlap_ = -1;  // hot items with an id below kTW at the last relabel decision (-1: none)
   bool sort_rows_ = false;  // COOC_FLAG_SORT_ROWS
   // batch windows of the large-universe path: columns relabelled by descending frequency (off: column ids,
   // COOC_FLAG_COLUMN_ORDER); the last run's maps (NULL without a relabel)
