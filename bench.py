@@ -198,6 +198,11 @@ def main():
 
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
     core.set_kernel_timing(True)
+    # N > 1, C3/C5: the exchange runs inside the library (cooc_count_owned / cooc_topk_owned) over its own RCCL
+    # communicator; COOC_BENCH_EXCHANGE=torch keeps the torch.distributed orchestration of sharding.py
+    lib_exchange = world > 1 and large and os.environ.get("COOC_BENCH_EXCHANGE", "library") != "torch"
+    if lib_exchange:
+        sharding.init_comm(core)
 
     topk_ms = []
     if args.config == "c5":
@@ -296,8 +301,9 @@ def main():
             "distinct_keys_total": int(d_total),
             "output": "padded CSR (row_base, row_nnz, col int32, cnt uint32) in HBM, exact counts",
             "parallelism": f"users sharded over {world} GPU(s)" + (
-                "; rows owned by frequency-snake order, histories all-gathered over RCCL" if world > 1 and
-                large else "; rows owned by a mod N, records exchange over RCCL" if world > 1 else ""),
+                "; rows owned by frequency-snake order, histories all-gathered over RCCL" + (
+                    " inside the library (cooc_count_owned)" if lib_exchange else " (torch.distributed)")
+                if world > 1 and large else "; rows owned by a mod N, records exchange over RCCL" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm",
