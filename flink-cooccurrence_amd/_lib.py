@@ -147,6 +147,8 @@ _SIGS = {
     "cooc_count_owned": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.POINTER(CoocOwnedInfo),
                                         ctypes.POINTER(CoocDeviceResult)]),
     "cooc_topk_owned": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "cooc_count_owned_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocOwnedInfo),
+                                             ctypes.POINTER(CoocWindowInfo)]),
     "cooc_snake_owner": (ctypes.c_int, [i64p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p]),
     "cooc_shard_plan": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp,
                                        ctypes.c_int64, vp, i64p, i64p]),

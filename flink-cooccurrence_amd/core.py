@@ -348,6 +348,17 @@ class CooccurrenceCore:
         self._comm_ops = ops
         self.comm_world = int(world)
 
+    def count_owned_host(self, user_ptr, items):
+        """cooc_count_owned_host: count_owned from host arrays (a JVM subtask's buffered shard); the owned
+        rows become this context's batch result.  Returns (BatchResult of the owned rows, CoocOwnedInfo)."""
+        up = np.ascontiguousarray(user_ptr, np.int64)
+        it = np.ascontiguousarray(items, np.int32)
+        info, winfo = CoocOwnedInfo(), CoocWindowInfo()
+        L = _lib.load()
+        check(L.cooc_count_owned_host(self._h, len(up) - 1, _p(up, i64p), _p(it, i32p), ctypes.byref(info),
+                                      ctypes.byref(winfo)), self._h)
+        return self.copy_batch(winfo.nnz, winfo.observed), info
+
     def count_owned(self, user_ptr, items, stream=None):
         """cooc_count_owned: this rank's users -> the rows it owns over the whole job's users (item
         counts all-reduced, owner map, histories all-gathered, owned rows counted, pairs all-reduced),

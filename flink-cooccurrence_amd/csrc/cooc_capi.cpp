@@ -441,6 +441,16 @@ int cooc_count_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, 
   });
 }
 
+int cooc_count_owned_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
+                          cooc_owned_info *info, cooc_window_info *winfo) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !info) return COOC_ERR_ARG;
+    if (n_users < 0 || (n_users > 0 && !user_ptr)) return fail(ctx, COOC_ERR_ARG, "bad CSR arguments");
+    Status s = ctx->count_owned_host(n_users, user_ptr, items, info, winfo);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
 int cooc_topk_owned(cooc_ctx *ctx, int32_t topk, int32_t flags, int32_t *d_sizes, int32_t *d_values, double *d_scores,
                     int64_t *d_rowsum_global, void *hip_stream) {
   return guarded(ctx, [&]() -> int {

@@ -166,6 +166,34 @@ Status cooc_ctx::count_host(int64_t n_users, const int64_t *user_ptr, const int3
   return Status::Ok();
 }
 
+Status cooc_ctx::count_owned_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_owned_info *info,
+                                  cooc_window_info *winfo) {
+  COOC_HIP_TRY(hipSetDevice(device));
+  if (user_ptr && n_users > 0 && user_ptr[0] != 0) return Status{COOC_ERR_ARG, "user_ptr[0] must be 0"};
+  for (int64_t u = 0; u < n_users; u++)
+    if (user_ptr[u + 1] < user_ptr[u]) return Status{COOC_ERR_ARG, "user_ptr must be non-decreasing"};
+  const int64_t n = n_users > 0 ? user_ptr[n_users] : 0;
+  if (n > 0 && !items) return Status{COOC_ERR_ARG, "items is NULL"};
+  COOC_TRY(b_user_ptr.reserve(sizeof(int64_t) * (n_users + 1)));
+  COOC_TRY(b_items.reserve(sizeof(int32_t) * (n + 1)));
+  if (n_users > 0)
+    COOC_HIP_TRY(hipMemcpyAsync(b_user_ptr.p, user_ptr, sizeof(int64_t) * (n_users + 1), hipMemcpyHostToDevice, stream));
+  else
+    COOC_HIP_TRY(hipMemsetAsync(b_user_ptr.p, 0, sizeof(int64_t), stream));
+  if (n > 0) COOC_HIP_TRY(hipMemcpyAsync(b_items.p, items, sizeof(int32_t) * n, hipMemcpyHostToDevice, stream));
+  cooc_device_result r;
+  COOC_TRY(count_owned(n_users, b_user_ptr.as<int64_t>(), b_items.as<int32_t>(), n, stream, info, &r));
+  if (winfo) {
+    std::vector<int32_t> nnz_rows(cfg.n_items);
+    COOC_HIP_TRY(hipMemcpy(nnz_rows.data(), r.row_nnz, sizeof(int32_t) * cfg.n_items, hipMemcpyDeviceToHost));
+    std::memset(winfo, 0, sizeof(*winfo));
+    winfo->nnz = r.nnz;
+    winfo->observed = r.observed;
+    winfo->n_rows = int32_t(std::count_if(nnz_rows.begin(), nnz_rows.end(), [](int32_t x) { return x > 0; }));
+  }
+  return Status::Ok();
+}
+
 Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                             int32_t *rowsum32) {
   if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};

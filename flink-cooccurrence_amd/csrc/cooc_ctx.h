@@ -142,6 +142,9 @@ struct cooc_ctx {
   cooc::Status topk_items(int32_t k, int32_t flags, int32_t n, const int32_t *items, int32_t *sizes,
                           int32_t *values, double *scores);
 
+  // the same from host arrays (staged on the context's stream): cooc_count_owned_host
+  cooc::Status count_owned_host(int64_t n_users, const int64_t *user_ptr, const int32_t *items, cooc_owned_info *info,
+                                cooc_window_info *winfo);
   // multi-GPU large-universe window over the communicator (cooc_owned.hip): cooc_count_owned / cooc_topk_owned
   cooc::Status count_owned(int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items, int64_t n_interactions,
                            hipStream_t s, cooc_owned_info *info, cooc_device_result *out);

@@ -214,6 +214,47 @@ JNIEXPORT jlongArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_c
   return out;
 }
 
+/* ---- multi-GPU (p > 1, one window): the exchange inside the library over RCCL ---- */
+JNIEXPORT jbyteArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_commUniqueId(JNIEnv *env, jclass cls) {
+  uint8_t id[COOC_COMM_ID_BYTES];
+  if (check(env, NULL, cooc_comm_unique_id(id))) return NULL;
+  jbyteArray out = (*env)->NewByteArray(env, COOC_COMM_ID_BYTES);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, COOC_COMM_ID_BYTES, (const jbyte *)id);
+  return out;
+}
+
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_commInit(
+    JNIEnv *env, jclass cls, jlong h, jbyteArray id, jint rank, jint world) {
+  uint8_t buf[COOC_COMM_ID_BYTES];
+  if (!id || (*env)->GetArrayLength(env, id) != COOC_COMM_ID_BYTES) {
+    throw_class(env, "java/lang/IllegalArgumentException", "the communicator id is COOC_COMM_ID_BYTES bytes");
+    return;
+  }
+  (*env)->GetByteArrayRegion(env, id, 0, COOC_COMM_ID_BYTES, (jbyte *)buf);
+  check(env, H(h), cooc_comm_init(H(h), buf, rank, world));
+}
+
+JNIEXPORT jlongArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_countOwned(
+    JNIEnv *env, jclass cls, jlong h, jlongArray userPtr, jintArray items) {
+  const jsize n_users = (*env)->GetArrayLength(env, userPtr) - 1;
+  cooc_owned_info oi;
+  cooc_window_info wi;
+  scratch p, i;
+  p.p = i.p = NULL;
+  int st = -1;
+  if (!scratch_get(env, &p, userPtr, sizeof(jlong), -1, 1, 'J') && !scratch_get(env, &i, items, sizeof(jint), -1, 1, 'I'))
+    st = check(env, H(h), cooc_count_owned_host(H(h), n_users, (const int64_t *)p.p, (const int32_t *)i.p, &oi, &wi));
+  scratch_put(env, &i, 0, 'I', 0);
+  scratch_put(env, &p, 0, 'J', 0);
+  if (st) return NULL;
+  jlongArray out = (*env)->NewLongArray(env, 4);
+  if (out) {
+    const jlong v[4] = {wi.nnz, wi.observed, wi.n_rows, oi.observed};
+    (*env)->SetLongArrayRegion(env, out, 0, 4, v);
+  }
+  return out;
+}
+
 JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyBatch(
     JNIEnv *env, jclass cls, jlong h, jlongArray rowPtr, jintArray cols, jshortArray cnt16, jintArray rowSums32) {
   scratch p, c, v, r;

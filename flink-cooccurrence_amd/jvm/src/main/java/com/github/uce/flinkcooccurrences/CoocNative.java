@@ -76,6 +76,23 @@ final class CoocNative {
   /** cooc_copy_batch: rowPtr long[nItems + 1], cols int[nnz], cnt16 short[nnz], rowSums32 int[nItems]. */
   static native void copyBatch(long handle, long[] rowPtr, int[] cols, short[] cnt16, int[] rowSums32);
 
+  /**
+   * cooc_comm_unique_id: the 128-byte RCCL id of a new communicator (host only: created once in the job's
+   * main() and handed to every subtask in its operator's constructor).
+   */
+  static native byte[] commUniqueId();
+
+  /** cooc_comm_init: the handle joins the communicator as subtask {@code rank} of {@code world} (open()). */
+  static native void commInit(long handle, byte[] id, int rank, int world);
+
+  /**
+   * cooc_count_owned_host: this subtask's users (userPtr long[nUsers + 1] into items) -> the rows it owns
+   * over every subtask's users (item counts all-reduced, owner map, histories exchanged over RCCL, owned
+   * rows counted).  Returns {nnz, observed, rows with entries} of the owned rows and the job's observed;
+   * the owned rows are then the handle's batch (copyBatch: every other row empty).
+   */
+  static native long[] countOwned(long handle, long[] userPtr, int[] items);
+
   /** cooc_topk_items: topk(handle, items[], k) of the last batch; sizes int[n], values/scores [n * k]. */
   static native void topKItems(long handle, int k, int flags, int[] items, int[] sizes, int[] values,
       double[] scores);

@@ -82,6 +82,31 @@ final class GpuCooccurrenceJob {
             new ItemRowRescorerTwoInputStreamOperator(topK));
   }
 
+  /**
+   * p > 1 subtasks, one window (the C3 / C5 configs): the keyBy(item) merge of partial rows replaced by the
+   * library's exchange over RCCL (GpuOwnedCooccurrenceRowsOperator): the communicator id is created here, in
+   * the job's client, and every subtask joins it in open(); each subtask emits the complete rows it owns,
+   * which feed the reference's rescorer with no ItemRowMerge / RowSumMerge windows.
+   */
+  static DataStream<Tuple2<Integer, IntDoublePriorityQueue>> topKOwned(
+      DataStream<Tuple3<Integer, Integer, Long>> interactionStream, int windowSize, TimeUnit windowUnit, int nItems,
+      int[] devices, short topK, int parallelism) {
+    final byte[] commId = CoocNative.commUniqueId();
+    final SingleOutputStreamOperator<Void> counter = interactionStream
+        .keyBy(0)
+        .transform(
+            "GpuOwnedCooccurrenceRows (" + windowSize + " " + windowUnit + ", " + parallelism + " GPUs)",
+            GpuNonSampledCooccurrenceRowsOperator.getOutputType(),
+            new GpuOwnedCooccurrenceRowsOperator(windowSize, windowUnit, nItems, devices, commId))
+        .setParallelism(parallelism);
+    return counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROWS_TAG)
+        .keyBy(0).connect(counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROW_SUM_TAG).broadcast())
+        .transform(
+            "ItemRowRescorer",
+            ItemRowRescorerTwoInputStreamOperator.getOutputType(),
+            new ItemRowRescorerTwoInputStreamOperator(topK));
+  }
+
   /** Int2ShortOpenHashMap.addTo of every entry (short arithmetic wraps, ItemRowAggregator.java:29). */
   static final class ItemRowMerge implements ReduceFunction<Tuple2<Integer, Int2ShortOpenHashMap>> {
     private static final long serialVersionUID = 1L;

@@ -344,6 +344,14 @@ typedef struct cooc_owned_info {
 COOC_API int cooc_count_owned(cooc_ctx *ctx, int64_t n_users, const int64_t *d_user_ptr, const int32_t *d_items,
                               int64_t n_interactions, void *hip_stream, cooc_owned_info *info,
                               cooc_device_result *out);
+/* The same window from HOST arrays (a JVM subtask's buffered user shard: user_ptr int64[n_users+1] into
+ * items), staged on the context's stream; *winfo as cooc_count_host (nnz, observed and rows with entries of
+ * the OWNED rows).  The owned rows are then this context's batch result: cooc_copy_batch packs them (every
+ * other row empty), cooc_topk_batch / cooc_topk_owned score them.  Replaces the p > 1 merge of partial
+ * rows (ItemRowAggregator / RowSumAggregator windows keyed by item, FlinkCooccurrences.java:138-157) for a
+ * one-window job. */
+COOC_API int cooc_count_owned_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
+                                   cooc_owned_info *info, cooc_window_info *winfo);
 /* C5 after cooc_count_owned: the owned rows' row sums all-reduced (the broadcast row-sum stream,
  * FlinkCooccurrences.java:163), then every owned row's LLR top-k against them (cooc_topk_batch_device).
  * d_rowsum_global (device int64[n_items], may be NULL) receives the all-reduced row sums. */

@@ -97,14 +97,24 @@ def _worker(rank, world, port, out_dir, n_users, topk, exchange):
     up_r = torch.from_numpy(up[u0:u1 + 1] - lo).to(dev)
     it_r = torch.from_numpy(it[lo:hi]).to(dev)
     with pkg.CooccurrenceCore(n_items=M, device=0) as core:
-        if exchange == "library":  # cooc_count_owned / cooc_topk_owned: the exchange inside the library
+        if exchange in ("library", "library_host"):  # cooc_count_owned(_host): the exchange inside the library
             sharding.init_comm_torch_ops(core)
-        res = sharding.count_owned(core, up_r, it_r)
-        torch.cuda.current_stream().synchronize()
-        rp, cols, cnt, rowsum = _rows(res.owned, M)
-        out.update(c3_rp=rp, c3_cols=cols, c3_cnt=cnt, c3_rowsum=rowsum, c3_owner=res.owner.cpu().numpy(),
-                   c3_observed=np.int64(res.observed), c3_local_observed=np.int64(res.local_observed),
-                   c3_n_all=np.int64(res.n_interactions_all))
+        if exchange == "library_host":  # a JVM subtask's call: host arrays in, the owned rows copied out
+            b, info = core.count_owned_host(up[u0:u1 + 1] - lo, it[lo:hi])
+            out.update(c3_rp=b.row_ptr, c3_cols=b.cols, c3_cnt=b.cnt, c3_rowsum=b.rowsum,
+                       c3_owner=_d2h(info.owner, M, np.int32), c3_observed=np.int64(info.observed),
+                       c3_local_observed=np.int64(info.local_observed), c3_n_all=np.int64(info.n_interactions_all))
+            res = sharding.OwnedResult(info.part, info.n_parts, None, None, int(info.observed),
+                                       int(info.local_observed), int(info.n_users_all),
+                                       int(info.n_interactions_all), int(info.gathered_bytes))
+            res.owner = torch.from_numpy(out["c3_owner"]).to(dev)
+        else:
+            res = sharding.count_owned(core, up_r, it_r)
+            torch.cuda.current_stream().synchronize()
+            rp, cols, cnt, rowsum = _rows(res.owned, M)
+            out.update(c3_rp=rp, c3_cols=cols, c3_cnt=cnt, c3_rowsum=rowsum, c3_owner=res.owner.cpu().numpy(),
+                       c3_observed=np.int64(res.observed), c3_local_observed=np.int64(res.local_observed),
+                       c3_n_all=np.int64(res.n_interactions_all))
         tk = sharding.topk_owned(core, res, topk)
         torch.cuda.current_stream().synchronize()
         out.update(tk_sizes=tk.sizes.cpu().numpy(), tk_values=tk.values.cpu().numpy(),
@@ -125,11 +135,12 @@ def _worker(rank, world, port, out_dir, n_users, topk, exchange):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["torch", "library"])
+@pytest.mark.parametrize("exchange", ["torch", "library", "library_host"])
 def test_two_ranks_real_core_vs_one_process(pkg, torch_cuda, tmp_path, exchange):
     """exchange "torch": sharding.py moves the buffers over torch.distributed; "library": the whole C3 step
     is cooc_count_owned / cooc_topk_owned, the library's exchange over cooc_comm_ops callbacks (gloo here,
-    RCCL in production: the same orchestration code)."""
+    RCCL in production: the same orchestration code); "library_host": cooc_count_owned_host from host
+    arrays and cooc_copy_batch of the owned rows, the calls a JVM subtask makes."""
     import torch
     import torch.multiprocessing as mp
 
@@ -165,7 +176,10 @@ def test_two_ranks_real_core_vs_one_process(pkg, torch_cuda, tmp_path, exchange)
         assert np.array_equal(nnz[mine], w_nnz[mine]) and np.array_equal(p["c3_rowsum"][mine], w_rowsum[mine])
         for a in np.flatnonzero(mine & (w_nnz > 0)):
             sl, ws = slice(p["c3_rp"][a], p["c3_rp"][a + 1]), slice(w_rp[a], w_rp[a + 1])
-            assert np.array_equal(p["c3_cols"][sl], w_cols[ws]) and np.array_equal(p["c3_cnt"][sl], w_cnt[ws]), f"row {a}"
+            # (device rows are in column order, cooc_copy_batch's in ascending ids: compared as sorted rows)
+            o1, o2 = np.argsort(p["c3_cols"][sl], kind="stable"), np.argsort(w_cols[ws], kind="stable")
+            assert np.array_equal(p["c3_cols"][sl][o1], w_cols[ws][o2]), f"row {a}"
+            assert np.array_equal(p["c3_cnt"][sl][o1], w_cnt[ws][o2]), f"row {a}"
         # top-k: the all-reduced row sums are the whole log's, so the owned heaps are the whole log's heaps
         assert np.array_equal(p["tk_rowsum"], w_rowsum)
         sz = p["tk_sizes"]
