@@ -124,13 +124,15 @@ def test_gather_and_split_rows_vs_brute(pkg, torch_cuda, planner):
             assert core.last_sort_rows()[0] == int(np.count_nonzero(rows.nnz)) - 200  # all but the 200 split rows
 
 
+@pytest.mark.parametrize("permute", [False, True])
 @pytest.mark.parametrize("planner", ["auto", "sort"])
-def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda, planner):
+def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda, planner, permute):
     """The first 1,500 users of the shard-invariant C3 log (1e6 items): the whole CSR vs scipy, through the
-    LDS hash / dense-tile chunks and through the sort + segmented-reduce path."""
+    LDS hash / dense-tile chunks and through the sort + segmented-reduce path (k_srb_row, k_sp_small,
+    k_sp_tiny); with item ids permuted, through the column relabel as well."""
     from flink_cooccurrence_amd import datagen
 
-    up, it = datagen.c3_users(0, 1500)
+    up, it = datagen.c3_users(0, 1500, permute=permute)
     M = datagen.C3_ITEMS
     with pkg.CooccurrenceCore(n_items=M, planner=planner) as core:
         got = core.count(up, it)
