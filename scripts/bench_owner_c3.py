@@ -23,12 +23,15 @@ def main():
     ap.add_argument("--parts", default="0", help="comma-separated ranks to time")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--permute", action="store_true", help="item ids permuted (datagen.c3_item_perm)")
+    ap.add_argument("--lib", default=None, help="another build of libcooc_hip.so")
     args = ap.parse_args()
     import torch
 
     import __graft_entry__
 
     pkg = __graft_entry__.load_package()
+    if args.lib:  # before the first call loads the library
+        sys.modules["flink_cooccurrence_amd._lib"].LIB_PATH = os.path.abspath(args.lib)
     from flink_cooccurrence_amd import datagen, sharding
 
     dev = torch.device("cuda", 0)
