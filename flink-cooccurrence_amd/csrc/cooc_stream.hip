@@ -214,9 +214,10 @@ struct DenseRows {
   const uint32_t *G;
   int32_t M;
   __device__ int64_t size(int32_t) const { return M; }
-  __device__ void get(int32_t a, int64_t i, int32_t &c, uint32_t &v) const {
+  __device__ int64_t base(int32_t a) const { return int64_t(a) * M; }
+  __device__ void get_at(int64_t b, int64_t i, int32_t &c, uint32_t &v) const {
     c = int32_t(i);
-    v = G[int64_t(a) * M + i];
+    v = G[b + i];
   }
 };
 
@@ -226,10 +227,10 @@ struct CsrRows {
   const int32_t *col;
   const uint32_t *cnt;
   __device__ int64_t size(int32_t a) const { return row_nnz[a]; }
-  __device__ void get(int32_t a, int64_t i, int32_t &c, uint32_t &v) const {
-    const int64_t k = row_base[a] + i;
-    c = col[k];
-    v = cnt[k];
+  __device__ int64_t base(int32_t a) const { return row_base[a]; }
+  __device__ void get_at(int64_t b, int64_t i, int32_t &c, uint32_t &v) const {
+    c = col[b + i];
+    v = cnt[b + i];
   }
 };
 
@@ -254,7 +255,7 @@ struct RowTerms {
 // full formula (5 logs; the two terms that depend on k11 alone come from k_k11_terms' tables).  Both
 // are LogLikelihood.java:41-57 in Java's operation order, bit for bit.
 template <class Rows>
-__device__ inline void rs_score_chunk(const Rows &src, int32_t a, int64_t i0, int64_t n, const RowTerms &R,
+__device__ inline void rs_score_chunk(const Rows &src, int64_t rb, int64_t i0, int64_t n, const RowTerms &R,
                                       int32_t exact, const ColTerms *__restrict__ cterm,
                                       const double *__restrict__ k11t, double *rscore, int32_t *rcol, int32_t *rq) {
   const int lane = threadIdx.x & 63;
@@ -263,29 +264,42 @@ __device__ inline void rs_score_chunk(const Rows &src, int32_t a, int64_t i0, in
   int32_t cj[kRsR];
   uint32_t vj[kRsR];
 #pragma unroll
-  for (int j = 0; j < kRsR; j++) {  // all kRsR steps' loads in flight at once
+  for (int j = 0; j < kRsR; j++) {  // all kRsR steps' loads in flight at once (the row base hoisted by the caller)
     cj[j] = 0;
     vj[j] = 0u;
-    if (i0 + j * 64 + lane < n) src.get(a, i0 + j * 64 + lane, cj[j], vj[j]);
+    if (i0 + j * 64 + lane < n) src.get_at(rb, i0 + j * 64 + lane, cj[j], vj[j]);
   }
+  // the per-column terms of kRsG steps gathered before any of them is scored (their latency overlaps)
+  constexpr int kRsG = 4;
 #pragma unroll
-  for (int j = 0; j < kRsR; j++) {
-    const int32_t c = cj[j];
-    const uint32_t v = vj[j];
-    const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
-    const bool fast = v != 0u && k11 == 1;
-    double score = 0.0;
-    if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
-      const ColTerms t = cterm[c];
-      const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (t.rs - k11);
-      score = llr_terms(R.x_all1, R.x_a, R.x_r1, t.x_rs, t.x_or2, 0.0, R.x_a1, t.x_rs1, xlogx(k22));
+  for (int j0 = 0; j0 < kRsR; j0 += kRsG) {
+    ColTerms tg[kRsG];
+#pragma unroll
+    for (int g = 0; g < kRsG; g++) {
+      const uint32_t v = vj[j0 + g];
+      const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+      if (v != 0u && k11 == 1) tg[g] = cterm[cj[j0 + g]];
     }
-    const bool slow = v != 0u && !fast;
-    const uint64_t sm = __ballot(slow);
-    if (slow) rq[npend + uint32_t(__popcll(sm & lt))] = j * 64 + lane;
-    npend += uint32_t(__popcll(sm));
-    rscore[j * 64 + lane] = slow ? __longlong_as_double(k11) : score;  // slow: k11 parked until scored
-    rcol[j * 64 + lane] = v != 0u ? c : -1;
+#pragma unroll
+    for (int g = 0; g < kRsG; g++) {
+      const int j = j0 + g;
+      const int32_t c = cj[j];
+      const uint32_t v = vj[j];
+      const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+      const bool fast = v != 0u && k11 == 1;
+      double score = 0.0;
+      if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+        const ColTerms &t = tg[g];
+        const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (t.rs - k11);
+        score = llr_terms(R.x_all1, R.x_a, R.x_r1, t.x_rs, t.x_or2, 0.0, R.x_a1, t.x_rs1, xlogx(k22));
+      }
+      const bool slow = v != 0u && !fast;
+      const uint64_t sm = __ballot(slow);
+      if (slow) rq[npend + uint32_t(__popcll(sm & lt))] = j * 64 + lane;
+      npend += uint32_t(__popcll(sm));
+      rscore[j * 64 + lane] = slow ? __longlong_as_double(k11) : score;  // slow: k11 parked until scored
+      rcol[j * 64 + lane] = v != 0u ? c : -1;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -343,8 +357,9 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
     const int64_t n = src.size(a);
     int32_t size = 0;
     double least = 0.0;
+    const int64_t rb = n > 0 ? src.base(a) : 0;
     for (int64_t i0 = 0; i0 < n; i0 += kRsChunk) {
-      rs_score_chunk(src, a, i0, n, R, exact, cterm, k11t, rscore, rcol, rq);
+      rs_score_chunk(src, rb, i0, n, R, exact, cterm, k11t, rscore, rcol, rq);
       for (int j = 0; j < kRsR && i0 + j * 64 < n; j++) {
         const int32_t c = rcol[j * 64 + lane];
         const double score = rscore[j * 64 + lane];
