@@ -42,10 +42,11 @@ def algorithmic_bytes(P: int, N: int, U: int, D: int) -> int:
     return 4 * P + 4 * N + 8 * (U + 1) + 12 * D
 
 
-def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: str, target_s: float = 12.0) -> dict:
+def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: str, target_s: float = 20.0) -> dict:
     """The oracle's multithreaded record-by-record restatement (threads own rows a mod T, every
     thread expands every user's records, NonSampled...java:129-161 -> ItemRowAggregator addTo) on
-    the first users of the same log: a calibration run sizes a sample of ~target_s seconds."""
+    the first users of the same log: a calibration run sizes the sample (its small size underestimates the
+    rate, so a target of 20 s gives a run of ~10-15 s)."""
     from oracle import oracle
 
     threads, nproc, avail = cpu_threads()
