@@ -99,7 +99,7 @@ constexpr int64_t kSubWork = int64_t(1) << COOC_SP_SUB_LG;  // pairs per split w
 constexpr int64_t kScrGroups = int64_t(1) << 21;       // gather scratch per workgroup (16-B groups of 4 ids)
 constexpr int kGatherMinChunks = COOC_SP_GATHER_MIN;   // rows with this many chunks gather their tails
 #ifndef COOC_SP_FILL
-#define COOC_SP_FILL 0.375f  // A/B at C3: 0.375 with 4x tables 4.5% faster than 0.5 with 3x
+#define COOC_SP_FILL 0.45f  // A/B at C3 (round 4, small rows in k_sp_small): 0.45 126.7, 0.5 126.9 (a row overflows), 0.375 130.3, 0.55 133 ms
 #endif
 #ifndef COOC_SP_DENSE
 #define COOC_SP_DENSE 2.f
