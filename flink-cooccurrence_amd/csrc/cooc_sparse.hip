@@ -89,7 +89,7 @@ constexpr int kSmallW = 4096;                          // ... of at most this ma
 #define COOC_SP_SPLIT_LG 23
 #endif
 #ifndef COOC_SP_GATHER_MIN
-#define COOC_SP_GATHER_MIN 3
+#define COOC_SP_GATHER_MIN 4  // rows of >= 4 chunks gather (A/B at round-4 HEAD: 125.2-125.5 vs 127.3-127.4 ms with 3)
 #endif
 constexpr int64_t kSplitWork = int64_t(1) << COOC_SP_SPLIT_LG;  // rows above this pair work are split
 #ifndef COOC_SP_SUB_LG
