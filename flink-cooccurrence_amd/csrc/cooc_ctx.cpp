@@ -121,6 +121,8 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
     err = h.err;
     bad_row = counter.sparse() ? h.bad_row : -1;
   }
+  if (err & 8)
+    return Status{COOC_ERR_STATE, "internal bounds check failed" + (bad_row >= 0 ? " (row " + std::to_string(bad_row) + ")" : std::string())};
   if (err & 2)
     return Status{COOC_ERR_OVERFLOW, "row-sum check failed" + (bad_row >= 0 ? " (row " + std::to_string(bad_row) + ")" : std::string()) +
                                          ": a row's exact counts do not add up to its closed-form row sum (a co-occurrence "

@@ -179,6 +179,14 @@ __device__ inline int32_t sp_rank(const SpArgs &A, int32_t a) { return relabel_p
 #define WPROG(A, v) do {} while (0)
 #endif
 
+// Bounds checks of the global index math (COOC_SP_CHECK builds, for fault hunting): a failed check sets err
+// bit 8 (COOC_ERR_STATE "internal bounds check") and skips the access; release builds compile them out.
+#ifdef COOC_SP_CHECK
+#define SP_CHECK(A, cond) ((cond) ? true : (atomicOr(reinterpret_cast<unsigned long long *>(&(A).tot->err), 8ull), false))
+#else
+#define SP_CHECK(A, cond) true
+#endif
+
 // Values every thread of the workgroup holds identically (read from LDS after a barrier): made
 // explicitly uniform so that the branches on them are scalar and no barrier sits in exec-masked code.
 __device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1919,6 +1927,9 @@ template <int kThreads>
 __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uint32_t *s_wt, uint32_t n, int bits) {
   constexpr int kWaves = kThreads / 64, kE = kSmallW / kThreads, kD = 1 << kRadixBits;
   static_assert(kD * kWaves == 2 * kThreads, "two scan entries per thread");
+  // a wave ranks kE * 64 positions: the rank (< kE * 64 <= 512, 9 bits) and the digit (7 bits) fill all 16 bits,
+  // so no 16-bit value is free to mark "no key" -- a position holds a key iff it is below n (checked by position
+  // in the scatter; the former 0xffff marker was also digit 127 at rank 511, and that key was never scattered)
   static_assert(kE * 64 <= 512 && kRadixBits <= 7, "rank and digit pack into 16 bits");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t below_mask = (1ull << lane) - 1ull;
@@ -1926,9 +1937,9 @@ __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uin
   for (int sh = 0; sh < bits; sh += kRadixBits) {
     reinterpret_cast<uint32_t *>(h)[tid] = 0u;
     __syncthreads();
-    uint32_t pk[kE / 2];  // (digit << 9 | rank), two per register; 0xffff: no key
+    uint32_t pk[kE / 2];  // (digit << 9 | rank), two per register; meaningful only at positions below n
 #pragma unroll
-    for (int e = 0; e < kE / 2; e++) pk[e] = 0xffffffffu;
+    for (int e = 0; e < kE / 2; e++) pk[e] = 0u;
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const uint32_t p0 = base + uint32_t(e) * 64u;
@@ -1963,9 +1974,9 @@ __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uin
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < kE; e++) {
-      const uint32_t x = (pk[e / 2] >> ((e & 1) * 16)) & 0xffffu;
-      if (x == 0xffffu) continue;
-      const uint32_t p = base + uint32_t(e) * 64u + uint32_t(lane), d = x >> 9;
+      const uint32_t p = base + uint32_t(e) * 64u + uint32_t(lane);
+      if (p >= n) continue;
+      const uint32_t x = (pk[e / 2] >> ((e & 1) * 16)) & 0xffffu, d = x >> 9;
       t[uint32_t(h[d * kWaves + uint32_t(wave)]) + (x & 511u)] = k[p];
     }
     __syncthreads();
@@ -1999,11 +2010,25 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
     __syncthreads();
     const int64_t i = uni(s_i);
     if (i >= n_small) break;
+    if (!SP_CHECK(A, first + i >= 0 && first + i < A.tot->n_chunks)) break;
     const SpWork it = A.queue[first + i];
     const int32_t a = it.row;
+    if (!SP_CHECK(A, a >= 0 && a < A.M && it.k0 >= 0 && it.k0 < it.k1 && it.k1 <= A.n_contrib)) continue;
     const uint32_t ra = uint32_t(sp_rank(A, a));
     const int64_t k0 = it.k0, k1 = it.k1, e0 = A.epre[k0];
-    const uint32_t W = uint32_t(A.epre[k1] - e0);
+    const int64_t W64 = uni(int64_t(A.epre[k1] - e0));
+    // the planner sends rows of kTinyW < W <= kSmallW pairs here; a larger W would overrun the LDS buffers
+    // (as k_sp_tiny, the row is refused and the run fails its row-sum check instead)
+    if (W64 > int64_t(kSmallW) || W64 <= 0) {
+      if (tid == 0) {
+        atomicOr(reinterpret_cast<unsigned long long *>(&A.tot->err), 2ull | 8ull);
+        A.tot->bad_row = a;
+        A.row_nnz[a] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t W = uint32_t(W64);
     const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
     // 1. the lists at their prefix positions (epre), a wave per contribution: wave w's contributions are
     //    k0 + w + 8 j; lane j reads the j-th one's list bounds (all in one round of loads), then the wave
@@ -2012,12 +2037,17 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
       const int64_t km = kb + int64_t(kSmallWaves) * lane;
       uint32_t m_s0 = 0, m_n0 = 0, m_s1 = 0, m_n1 = 0, m_d = 0;
       if (km < k1) {
-        const int32_t *tbu = A.tb + int64_t(A.vals[km] & kListMask) * (A.T + 2);
+        const uint32_t u = A.vals[km] & kListMask;
+        const int32_t *tbu = A.tb + int64_t(SP_CHECK(A, u < A.n_users) ? u : 0u) * (A.T + 2);
         m_s0 = uint32_t(tbu[0]);
         m_n0 = uint32_t(tbu[A.T + 1]) - m_s0;
         m_s1 = uint32_t(tbu[1]);
         m_n1 = uint32_t(tbu[A.T]) - m_s1;
         m_d = uint32_t(A.epre[km] - e0);
+        // the list lands inside the row's W ids; its 16-B groups inside the arenas
+        if (!SP_CHECK(A, m_d + m_n0 + m_n1 <= W && (int64_t(m_s0) + m_n0 + 7) / 8 <= A.n_groups0 &&
+                             (int64_t(m_s1) + m_n1 + 3) / 4 <= A.n_groups))
+          m_n0 = m_n1 = 0;
       }
       const int cnt = int(min<int64_t>(64, (k1 - kb + kSmallWaves - 1) / kSmallWaves));
       for (int j = 0; j < cnt; j++)
@@ -2091,7 +2121,7 @@ __global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(8
     }
     __syncthreads();
     const int64_t pos = uni(s_pos);
-    if (pos >= 0) {
+    if (pos >= 0 && SP_CHECK(A, pos + int64_t(n_keep) <= A.cap && n_runs <= W)) {
       for (uint32_t q = uint32_t(tid); q < n_runs; q += kSmallThreads) {
         if (int32_t(q) == drop) continue;
         const uint32_t p = st[q], c = st[q + 1] - p, key = b[p];

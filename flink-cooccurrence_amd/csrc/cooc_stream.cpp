@@ -314,6 +314,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   COOC_HIP_TRY(hipStreamSynchronize(s));
   PlanTotals t;
   COOC_TRY(ctx.counter.read_totals(&t));
+  if (t.err & 8) return Status{COOC_ERR_STATE, "internal bounds check failed"};
   if (t.err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
   if (t.err & 4) return Status{COOC_ERR_OOM, "the sparse output region is exhausted"};
 

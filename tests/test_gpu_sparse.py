@@ -124,6 +124,32 @@ def test_gather_and_split_rows_vs_brute(pkg, torch_cuda, planner):
             assert core.last_sort_rows()[0] == int(np.count_nonzero(rows.nnz)) - 200  # all but the 200 split rows
 
 
+def test_small_row_full_radix_blocks_vs_closed_form(pkg, oracle, torch_cuda):
+    """k_sp_small's LSD radix sort (rows of 257..4,096 pairs, 512-thread workgroups: a wave ranks 512 positions)
+    when whole 512-position blocks share one digit: row a = 0x3F80 (digit 0 in pass 0, digit 127 = bits 7..13
+    in pass 1) holds 2,200 copies of its own column (600 users [a, x], 400 users [a, a, x]), so in pass 1 the
+    last key of a full wave block has digit 127 at rank 511 -- the value the sort once used as its "no key"
+    marker, which left a stale LDS word in the sorted row.  The whole CSR against the closed form."""
+    rng = np.random.default_rng(5)
+    M, a = 100_000, 0x3F80
+    xs = rng.choice(np.arange(20_000, M), 1000, replace=False)
+    xs = xs[(xs & 127) != 0][:1000]
+    lists = [[a, int(x)] for x in xs[:600]] + [[a, a, int(x)] for x in xs[600:]]
+    up = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+    it = np.concatenate([np.array(x, np.int32) for x in lists])
+    lens = np.diff(up)
+    W_a = int(np.sum(lens[[a in x for x in lists]] * np.array([x.count(a) for x in lists])))
+    assert 256 < W_a <= 4096  # k_sp_small's row size
+    with pkg.CooccurrenceCore(n_items=M) as core:
+        got = core.count(up, it)
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    assert got.observed == observed
+    assert np.array_equal(got.row_ptr, rp)
+    assert np.array_equal(got.cols, cols)
+    assert np.array_equal(got.cnt.astype(np.int64), data)
+    assert np.array_equal(got.rowsum, rowsums)
+
+
 @pytest.mark.parametrize("permute", [False, True])
 @pytest.mark.parametrize("planner", ["auto", "sort"])
 def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda, planner, permute):
