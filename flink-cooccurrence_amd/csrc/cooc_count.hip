@@ -1115,7 +1115,7 @@ void Counter::release() {
                    &order_, &ord_nch_, &ord_cbase_, &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_,
                    &col_, &cnt_, &staging_, &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_,
                    &split_sum_, &tarena_, &bump_, &seg_off_, &plen_, &poff_, &send_, &witems_, &sp_arena_, &sp_arena0_, &sp_defer_, &sr_keys_, &sr_ukeys_, &sr_ucnt_, &sr_aux_, &sp_tb_,
-                   &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_, &sp_pbase_, &sp_scr_, &sp_hz_, &sp_spre_};
+                   &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_, &sp_pbase_, &sp_scr_, &sp_scr_mid_, &sp_hz_, &sp_spre_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;

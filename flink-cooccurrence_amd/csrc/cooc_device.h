@@ -108,6 +108,8 @@ struct PlanTotals {
   int64_t small_ctr;      // k_sp_small's work counter
   int64_t srb_ctr;        // k_srb_row's row counter (the deferred rows)
   int64_t ts_pairs;       // pairs of the tiny and small rows (sorted by k_sp_tiny / k_sp_small)
+  int64_t n_mid;          // whole rows of at most kMidW pairs above the small ones: k_sp_main's mid shape
+  int64_t max_tail_mid;   // largest expected gather tail of a mid row (sizes the mid launch's scratch)
 };
 
 // One streaming window through the large-universe path in one pass (NonSampled...java:129-161): the CSR
@@ -254,6 +256,9 @@ class Counter {
   // deferred rows through the library radix sort (COOC_SR_HIPCUB=1, A/B) instead of k_srb_row
   bool srb_hipcub_ = getenv("COOC_SR_HIPCUB") && getenv("COOC_SR_HIPCUB")[0] == '1';
   bool small_off_ = getenv("COOC_SP_SMALL") && getenv("COOC_SP_SMALL")[0] == '0';  // (A/B: small rows in k_sp_main)
+  bool mid_off_ = getenv("COOC_SP_MID") && getenv("COOC_SP_MID")[0] == '0';  // (A/B: mid rows in the big shape)
+  DevBuf sp_scr_mid_;      // the mid launch's gather scratch
+  int64_t last_mid_grid_ = 0;
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,
                       const int64_t *spre, int64_t cap, hipStream_t s);
   bool general_only_ = false;

@@ -108,6 +108,36 @@ constexpr float kHashFill = COOC_SP_FILL * kHashMax;     // expected distinct ke
 constexpr float kDensePairs = COOC_SP_DENSE * kTW;       // a tile with more expected pairs is dense
 constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 + kSpThreads;  // (gb + info: 8 B per descriptor)
 
+// Two shapes of the accumulate kernel, one queue.  Rows of at most kMidW pairs ("mid rows": at C3 the half
+// million rows of 4K..64K pairs, mostly one dense tile 0 plus a sparse tail) run with FOUR 256-thread
+// workgroups per CU instead of two 512-thread ones: their chunks are short latency chains (walk, barrier,
+// compaction), so more independent chunks per CU hide more of them.  The LDS budget (40 KB per workgroup)
+// holds because a count never exceeds its row's pair work W <= 65,535: the dense tile's counters are u16,
+// two per LDS word (a ds_add of 1 << 16 for the odd column never carries), and hash tables have 4K slots
+// (chunks of half the expected keys) over column spans of at most 2^19 (a 512-word block bitmap).
+#ifndef COOC_SP_MID_W
+#define COOC_SP_MID_W 65535
+#endif
+constexpr int64_t kMidW = COOC_SP_MID_W;
+static_assert(kMidW <= 65535, "mid rows count in u16");
+template <int Threads, int HashMax, int L1Words, int Db, bool U16>
+struct SpShape {
+  static constexpr int kThreads = Threads, kWaves = Threads / 64;
+  static constexpr int kHashMax = HashMax;            // hash slots: keys [0, H) + counts [HashMax, HashMax + H)
+  static constexpr int kWStage = HashMax / 2;         // compaction staging (entries) in the emptied table
+  static constexpr int kL1Words = L1Words;            // block bitmap words: chunk spans <= L1Words * 1024 columns
+  static constexpr int kHashMaxTiles = L1Words * 1024 / kTW;
+  static constexpr int kDb = Db;                      // contribution descriptors per walk batch
+  static constexpr bool kU16 = U16;                   // dense counters: u16 pairs (true) or u32
+  static constexpr int kPer = U16 ? 8 : 4;            // dense counters per 16-B LDS word
+  static constexpr int kRWords = (U16 ? kTW / 2 : kTW) > 2 * HashMax ? (U16 ? kTW / 2 : kTW) : 2 * HashMax;
+  static constexpr int kLds = kRWords * 4 + 2 * L1Words * 4 + Db * 8 + (Db + 4) * 4 + Threads;
+};
+using SpBig = SpShape<kSpThreads, kHashMax, kL1Words, kSpDb, false>;
+using SpMid = SpShape<256, 4096, 512, 256, true>;
+static_assert(SpBig::kLds == kSpLds, "the big shape is the original kernel");
+constexpr float kHashFillMid = COOC_SP_FILL * SpMid::kHashMax;
+
 // One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
 struct SpWork {
   int64_t k0, k1;   // contribution range (row-sorted)
@@ -122,7 +152,8 @@ struct SpWork {
 struct SpArgs {
   const SpWork *queue;
   PlanTotals *tot;
-  int32_t *qctr;
+  int32_t *qctr;            // this launch's work counter (k_sp_main: the queue range [q_begin, q_end))
+  int64_t q_begin, q_end;
   const uint32_t *vals;     // contributions: user index, item-sorted
   const int32_t *tb;        // [U x (T + 2)] a user's tile-0 range in arena0, its tile starts in arena1
   const uint4 *tarena;      // arena1: the lists' ids of tiles >= 1 (u32), in 16-B groups
@@ -210,7 +241,8 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// Block-wide exclusive scan (kSpThreads threads); *total = the block sum.  Two barriers.
+// Block-wide exclusive scan (kWaves waves); *total = the block sum.  Two barriers.
+template <int kWaves>
 __device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t *total, uint32_t *s_wtot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t inc = wave_incl_scan(x);
@@ -218,7 +250,7 @@ __device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t *total, uint32_t
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kSpWaves; w++) {
+  for (int w = 0; w < kWaves; w++) {
     const uint32_t v = s_wtot[w];
     pre += w < wave ? v : 0u;
     tot += v;
@@ -654,7 +686,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   __shared__ uint64_t s_red[4][4];
   const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t est_sum = 0, bound = 0, n_split = 0, split_work = 0, n_active = 0, max_tail = 0, n_gather = 0, n_tiny = 0,
-           n_small = 0, ts_pairs = 0;
+           n_small = 0, ts_pairs = 0, n_mid = 0, max_tail_mid = 0;
   if (a < M) {
     const int64_t k0 = row_ptr[a], c = row_ptr[a + 1] - k0;
     const int64_t W = epre[k0 + c] - epre[k0];
@@ -672,6 +704,12 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
       n_tiny = ((tiny_on & 1) && W <= kTinyW) ? 1 : 0;  // (the W-descending queue puts them last)
       n_small = ((tiny_on & 2) && W > kTinyW && W <= kSmallW) ? 1 : 0;  // (... just before the tiny ones)
       ts_pairs = (n_tiny || n_small) ? uint64_t(W) : 0u;
+      // a mid row (k_sp_main's 256-thread shape): its chunks are planned for 4K-slot tables over <= 2^19 columns
+      const bool mid = (tiny_on & 4) && !n_tiny && !n_small && W <= kMidW;
+      n_mid = mid ? 1 : 0;
+      const float hfill = mid ? kHashFillMid : kHashFill;
+      const int hmax = mid ? SpMid::kHashMax : kHashMax;
+      const int hmaxtiles = mid ? SpMid::kHashMaxTiles : kHashMaxTiles;
       bound = uint64_t(min<int64_t>(W - self, M));
       float e_tot = 0.f;
       if (W > kSplitWork) {
@@ -690,7 +728,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
 #ifndef COOC_SP_HASH_SLACK
 #define COOC_SP_HASH_SLACK 4.f  // table >= 4x the estimated distinct count (A/B)
 #endif
-          for (int H = kHashMin; H < kHashMax && float(H) < COOC_SP_HASH_SLACK * cur + 64.f; H <<= 1) code++;
+          for (int H = kHashMin; H < hmax && float(H) < COOC_SP_HASH_SLACK * cur + 64.f; H <<= 1) code++;
           if (cs < 32) h0 |= code << (2 * cs); else h1 |= code << (2 * (cs - 32));
           cs = -1;
         };
@@ -698,12 +736,12 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
           const float d = est_distinct(est, t, W);
           const float e = float(W) * gmass[t];
           e_tot += d;
-          if (d > kHashFill || e > kDensePairs) {
+          if (d > hfill || e > kDensePairs) {
             close();
             st |= uint64_t(1) << t;
             dn |= uint64_t(1) << t;
           } else {
-            if (cs < 0 || cur + d > kHashFill || n_in == kHashMaxTiles) {
+            if (cs < 0 || cur + d > hfill || n_in == hmaxtiles) {
               close();
               st |= uint64_t(1) << t;
               cs = t;
@@ -718,6 +756,10 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
         if (T < 64 && (dn & 1ull) && __popcll(st) >= kGatherMinChunks) {  // gather mode (k_sp_main)
           dn |= uint64_t(1) << 63;
           max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]));
+          if (mid) {
+            max_tail_mid = max_tail;
+            max_tail = 0;
+          }
           n_gather = 1;
         }
       }
@@ -741,6 +783,8 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
     act += __shfl_xor(act, o, 64);
     n_tiny += __shfl_xor(n_tiny, o, 64);
     n_small += __shfl_xor(n_small, o, 64);
+    n_mid += __shfl_xor(n_mid, o, 64);
+    max_tail_mid = max(max_tail_mid, __shfl_xor(max_tail_mid, o, 64));
     ts_pairs += __shfl_xor(ts_pairs, o, 64);
     n_gather += __shfl_xor(n_gather, o, 64);
     max_tail = max(max_tail, __shfl_xor(max_tail, o, 64));
@@ -758,6 +802,9 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
   if (lane == 0 && act) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_active), (unsigned long long)act);
   if (lane == 0 && n_tiny) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_tiny), (unsigned long long)n_tiny);
   if (lane == 0 && n_small) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_small), (unsigned long long)n_small);
+  if (lane == 0 && n_mid) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_mid), (unsigned long long)n_mid);
+  if (lane == 0 && max_tail_mid)
+    atomicMax(reinterpret_cast<unsigned long long *>(&tot->max_tail_mid), (unsigned long long)max_tail_mid);
   if (lane == 0 && ts_pairs) atomicAdd(reinterpret_cast<unsigned long long *>(&tot->ts_pairs), (unsigned long long)ts_pairs);
   if (lane == 0 && n_gather)
     atomicAdd(reinterpret_cast<unsigned long long *>(&tot->n_gather_rows), (unsigned long long)n_gather);
@@ -821,7 +868,7 @@ __global__ void k_sp_totals(PlanTotals *__restrict__ tot, const int64_t *__restr
   tot->n_chunks = tot->n_split_work + (tot->n_active - tot->n_split);
   tot->work_total = epre[n];
   tot->self_total = spre ? spre[n] : n;
-  qctr[0] = 0;
+  qctr[0] = qctr[1] = 0;
 }
 
 // ---- the accumulate kernel --------------------------------------------------------------------------
@@ -901,7 +948,16 @@ struct WalkOp {
 // of arena0); m = the lanes (bits 0 .. kIds - 1) inside the walked segment, the others are ids of a
 // neighbouring tile range or list (or end-of-list sinks) and are skipped.  Gather mode: an id of tile 0
 // is counted in the dense tile, any other is appended to its tile's bucket (4-B ids, packed).
-template <int kIds>
+// A +1 at dense counter o of the LDS tile: u32 counters, or (mid shape) u16 counters packed two per word.
+template <class Sh>
+__device__ inline void sp_dense_add(uint32_t *R, uint32_t o) {
+  if (Sh::kU16)
+    atomicAdd(&R[o >> 1], 1u << ((o & 1u) << 4));
+  else
+    atomicAdd(&R[o], 1u);
+}
+
+template <class Sh, int kIds>
 __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStatic &S_, const WalkOp &op,
                                       const uint4 &v, uint32_t m) {
   uint32_t x[kIds];
@@ -930,7 +986,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
   if (op.mode == 1) {
 #pragma unroll
     for (int h = 0; h < kIds; h += 4)
-      sp_hash_insert4(L.R, L.R + kHashMax, make_uint4(x[h], x[h + 1], x[h + 2], x[h + 3]), op.hshift, op.hmask, S_);
+      sp_hash_insert4(L.R, L.R + Sh::kHashMax, make_uint4(x[h], x[h + 1], x[h + 2], x[h + 3]), op.hshift, op.hmask, S_);
     return;
   }
   if (op.mode == 2) {
@@ -940,7 +996,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
       if (x[i] == kSink) continue;
       const uint32_t t = x[i] >> kTShift;
       if (t == 0) {
-        atomicAdd(&L.R[x[i]], 1u);
+        sp_dense_add<Sh>(L.R, x[i]);
       } else {
         const uint32_t slot = atomicAdd(&S_.bcur[t], 1u);
         if (slot < S_.bstart[t + 1] - S_.bstart[t]) scr[S_.bstart[t] + slot] = x[i];  // else the bucket overflowed
@@ -950,7 +1006,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
   }
 #pragma unroll
   for (int i = 0; i < kIds; i++)
-    if (x[i] != kSink) atomicAdd(&L.R[x[i] - op.c0], 1u);
+    if (x[i] != kSink) sp_dense_add<Sh>(L.R, x[i] - op.c0);
 }
 
 // One batch of segments: this thread's segment (tid < nb) is the ids at positions [s, e) of ar (16-B
@@ -959,7 +1015,7 @@ __device__ inline void sp_apply_group(const SpArgs &A, const SpShared &L, SpStat
 // contiguous shares of the virtual range and step S groups at a time, kSpU loads in flight per lane,
 // applying op to every id of the segment (lanes outside it masked).  Returns the batch's groups
 // (uniform); ends with a barrier.
-template <int kIds>
+template <class Sh, int kIds>
 __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpStatic &S_, const uint4 *__restrict__ ar,
                                          int64_t nsrc, int nb, uint32_t s, uint32_t e, const WalkOp &op) {
   constexpr uint32_t kSh = kIds == 8 ? 3u : 2u, kLo = kIds - 1;
@@ -967,7 +1023,7 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
   const unsigned long long c_b0 = STAT_CLOCK();
   const uint32_t len = (tid < nb && e > s) ? ((e + kLo) >> kSh) - (s >> kSh) : 0u;
   uint32_t total;
-  const uint32_t ex = block_excl_scan(len, &total, S_.wtot);
+  const uint32_t ex = block_excl_scan<Sh::kWaves>(len, &total, S_.wtot);
   if (total == 0) return 0;  // uniform (scalar branch): no barrier is skipped by part of the block
   const uint32_t mean = total / uint32_t(nb);
 #ifndef COOC_SP_SLONG
@@ -980,7 +1036,7 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
 #define COOC_SP_STIER 32  // segments of >= 32 groups: whole-wave walkers, >= 12: 16 lanes (profiles/r03/walker_ab)
 #endif
   const uint32_t S = mean >= COOC_SP_STIER ? COOC_SP_SLONG : mean >= 12 ? 16u : COOC_SP_SSHORT;
-  const uint32_t nW = kSpThreads / S;
+  const uint32_t nW = uint32_t(Sh::kThreads) / S;
   if (tid < nb) {
     L.vst[tid] = ex;
     L.gb[tid] = int32_t(s >> kSh) - int32_t(ex);
@@ -1053,7 +1109,7 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
         // (stats build, COOC_SP_EXP=2, results invalid: every other group of dense / hash walks is neither
         // loaded nor applied -- how much of a walk is the group delivery)
         const uint32_t mk = (m >> (8 * k)) & 255u;
-        if (mk) sp_apply_group<kIds>(A, L, S_, op, v[k], mk);
+        if (mk) sp_apply_group<Sh, kIds>(A, L, S_, op, v[k], mk);
       }
 #pragma unroll
       for (int k = 0; k < kSpU; k++) v[k] = vn[k];
@@ -1068,6 +1124,7 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
 // Walk the partner ids of contributions [k0, k1) restricted to tiles [t0, t1) (full: whole lists),
 // applying op to every id: the tile-0 part of the lists from arena0 (u16, 8 ids per load), the rest from
 // arena1 (u32), a batch of kSpDb contributions at a time.  Returns the groups walked.
+template <class Sh>
 __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic &S_, int64_t k0, int64_t k1, int t0,
                                    int t1, bool full, const WalkOp &op) {
   uint64_t walked = 0;
@@ -1076,8 +1133,8 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
   const bool has0 = full || t0 == 0;                 // (uniform)
   const int ta = full ? 1 : max(t0, 1), tz = full ? A.T : t1;
   const bool has1 = tz > ta;
-  for (int64_t b0 = k0; b0 < k1; b0 += kSpDb) {
-    const int nb = int(min<int64_t>(kSpDb, k1 - b0));
+  for (int64_t b0 = k0; b0 < k1; b0 += Sh::kDb) {
+    const int nb = int(min<int64_t>(Sh::kDb, k1 - b0));
     uint32_t s0 = 0, e0 = 0, s1 = 0, e1 = 0;
     STAT_ADD(19, op.mode == 1 ? 1 : 0);
     if (tid < nb && okt) {
@@ -1092,8 +1149,8 @@ __device__ inline uint64_t sp_walk(const SpArgs &A, const SpShared &L, SpStatic 
         e1 = uint32_t(tbu[tz]);
       }
     }
-    if (has0) walked += sp_walk_batch<8>(A, L, S_, A.tarena0, A.n_groups0, nb, s0, e0, op);
-    if (has1) walked += sp_walk_batch<4>(A, L, S_, A.tarena, A.n_groups, nb, s1, e1, op);
+    if (has0) walked += sp_walk_batch<Sh, 8>(A, L, S_, A.tarena0, A.n_groups0, nb, s0, e0, op);
+    if (has1) walked += sp_walk_batch<Sh, 4>(A, L, S_, A.tarena, A.n_groups, nb, s1, e1, op);
     if (uni(S_.flag)) break;
   }
   return walked;
@@ -1116,6 +1173,7 @@ __device__ inline void sp_global_sync() {
 // Output space for n more entries of the current row (thread-uniform call).  Moves the row's
 // entries so far to a new slab when the workgroup's slab is exhausted.  Returns the write position
 // (-1 when the output region is exhausted: the host reruns with a larger region).
+template <class Sh>
 __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -1147,7 +1205,7 @@ __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
   if (cn > 0) {  // the row's earlier entries follow it to the new slab (rare)
     sp_global_sync();  // they were just stored by other waves
     const int64_t from = S_.copy_from, to = S_.row_begin;
-    for (int64_t i = tid; i < cn; i += kSpThreads) {
+    for (int64_t i = tid; i < cn; i += Sh::kThreads) {
       if (BCHK(A, to + i < A.cap && from + i < A.cap && from >= 0, 32)) {
         A.col_out[to + i] = A.col_out[from + i];
         A.cnt_out[to + i] = A.cnt_out[from + i];
@@ -1158,67 +1216,88 @@ __device__ inline int64_t sp_reserve(const SpArgs &A, SpStatic &S_, int64_t n) {
 }
 
 // Column-order compaction of w dense counters (16-B aligned), appended to the row's output; the
-// counters are left zero.  Waves own 256-column-aligned ranges, 4 counters per lane.
+// counters are left zero.  Waves own (64 kPer)-column-aligned ranges, kPer counters per lane (one 16-B LDS
+// read: 4 u32 counters, or 8 u16 ones in the mid shape).
+template <class Sh>
 __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t w, int32_t c0,
                                         uint64_t &rsum) {
+  constexpr int kPer = Sh::kPer, kStep = 64 * kPer, kQ = kPer / 4;  // kQ: 16-B id loads per lane and step
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t *row = L.R;
-  const int32_t per = ((w + kSpWaves - 1) / kSpWaves + 255) & ~255;
+  const int32_t per = ((w + Sh::kWaves - 1) / Sh::kWaves + kStep - 1) & ~(kStep - 1);
   const int32_t lo = min(w, wave * per), hi = min(w, lo + per);
   const uint4 *row4 = reinterpret_cast<const uint4 *>(row);
-  auto load = [&](int32_t b, uint32_t v[4]) {
+  auto load = [&](int32_t b, uint32_t v[kPer]) {  // counters b .. b + kPer - 1 (b a multiple of kPer)
     if (b < hi) {
-      const uint4 q = row4[b >> 2];
-      v[0] = q.x;
-      v[1] = b + 1 < hi ? q.y : 0u;
-      v[2] = b + 2 < hi ? q.z : 0u;
-      v[3] = b + 3 < hi ? q.w : 0u;
+      const uint4 q = row4[b / kPer];
+      const uint32_t ww[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < kPer; k++) {
+        const uint32_t x = Sh::kU16 ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : ww[k & 3];
+        v[k] = b + k < hi ? x : 0u;
+      }
     } else {
-      v[0] = v[1] = v[2] = v[3] = 0u;
+#pragma unroll
+      for (int k = 0; k < kPer; k++) v[k] = 0u;
     }
   };
   uint32_t cnt = 0;
-  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
-    uint32_t v[4];
-    load(b0 + 4 * lane, v);
-    cnt += (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+  for (int32_t b0 = lo; b0 < hi; b0 += kStep) {
+    uint32_t v[kPer];
+    load(b0 + kPer * lane, v);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) cnt += v[k] != 0u;
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (lane == 0) S_.wtot[wave] = cnt;
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int wv = 0; wv < kSpWaves; wv++) {
+  for (int wv = 0; wv < Sh::kWaves; wv++) {
     const uint32_t x = S_.wtot[wv];
     off += wv < wave ? x : 0u;
     tot += x;
   }
-  // after a relabel the output ids of tile 0 are hot_col[b]: 16-B loads of the lane's 4 ids, two steps ahead
-  // (their latency overlaps the reservation and the steps before); above tile 0 they are c0 + b - kTW
+  // after a relabel the output ids of tile 0 are hot_col[b]: 16-B loads of the lane's kPer ids, two steps
+  // ahead (their latency overlaps the reservation and the steps before); above tile 0 they are c0 + b - kTW
   const bool map = A.hot_col != nullptr && c0 == 0;
-  auto colq = [&](int32_t b) -> uint4 {
-    return (map && b < hi) ? *reinterpret_cast<const uint4 *>(A.hot_col + b) : make_uint4(0u, 0u, 0u, 0u);
+  auto colq = [&](int32_t b, uint4 q[kQ]) {
+#pragma unroll
+    for (int j = 0; j < kQ; j++)
+      q[j] = (map && b < hi) ? *reinterpret_cast<const uint4 *>(A.hot_col + b + 4 * j) : make_uint4(0u, 0u, 0u, 0u);
   };
-  uint4 q0 = colq(lo + 4 * lane), q1 = colq(lo + 256 + 4 * lane);
-  const int64_t base = sp_reserve(A, S_, tot);  // (barrier: every wave has read wtot)
+  uint4 q0[kQ], q1[kQ];
+  colq(lo + kPer * lane, q0);
+  colq(lo + kStep + kPer * lane, q1);
+  const int64_t base = sp_reserve<Sh>(A, S_, tot);  // (barrier: every wave has read wtot)
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int32_t b0 = lo; b0 < hi; b0 += 256) {
-    const int32_t b = b0 + 4 * lane;
-    const uint4 qc = q0;
-    q0 = q1;
-    q1 = colq(b0 + 512 + 4 * lane);
-    const uint32_t ids[4] = {qc.x, qc.y, qc.z, qc.w};
-    uint32_t v[4];
+  for (int32_t b0 = lo; b0 < hi; b0 += kStep) {
+    const int32_t b = b0 + kPer * lane;
+    uint32_t ids[kPer];
+#pragma unroll
+    for (int j = 0; j < kQ; j++) {
+      ids[4 * j] = q0[j].x;
+      ids[4 * j + 1] = q0[j].y;
+      ids[4 * j + 2] = q0[j].z;
+      ids[4 * j + 3] = q0[j].w;
+      q0[j] = q1[j];
+    }
+    colq(b0 + 2 * kStep + kPer * lane, q1);
+    uint32_t v[kPer];
     load(b, v);
-    const uint32_t c = (v[0] != 0u) + (v[1] != 0u) + (v[2] != 0u) + (v[3] != 0u);
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) c += v[k] != 0u;
     const uint64_t m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u);
+    const uint64_t m3 = kPer > 4 ? __ballot(c & 8u) : 0ull;
     const uint32_t pre = uint32_t(__popcll(m0 & lt_mask)) + 2u * uint32_t(__popcll(m1 & lt_mask)) +
-                         4u * uint32_t(__popcll(m2 & lt_mask));
-    rsum += uint64_t(v[0]) + v[1] + v[2] + v[3];
+                         4u * uint32_t(__popcll(m2 & lt_mask)) + 8u * uint32_t(__popcll(m3 & lt_mask));
+#pragma unroll
+    for (int k = 0; k < kPer; k++) rsum += v[k];
     if (c) {
       int64_t pos = base + off + pre;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < kPer; k++) {
         if (!v[k]) continue;
         if (base >= 0) {
           if (BCHK(A, pos >= 0 && pos < A.cap, 64)) {
@@ -1228,35 +1307,34 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
         }
         pos++;
       }
-      if (b + 3 < hi) {
-        reinterpret_cast<uint4 *>(row)[b >> 2] = make_uint4(0u, 0u, 0u, 0u);
-      } else {
-        for (int k = 0; k < 4 && b + k < hi; k++) row[b + k] = 0u;
-      }
+      // (counters past hi are never incremented -- no id reaches them -- so the whole 16-B word is cleared)
+      reinterpret_cast<uint4 *>(row)[b / kPer] = make_uint4(0u, 0u, 0u, 0u);
     }
-    off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2));
+    off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2)) +
+           8u * uint32_t(__popcll(m3));
   }
   __syncthreads();
 }
 
 // Column-order compaction of the hash table (H slots) of the column range [c0, c1), appended to the
 // row's output; leaves the table, L1 and the scratch it uses zero.  Entries are kept in registers
-// (H / kSpThreads <= 16 per thread); their 32-column blocks are ranked through the L1 bitmap, every
+// (H / kThreads <= 16 per thread); their 32-column blocks are ranked through the L1 bitmap, every
 // block gets a 32-bit column mask (in the keys area) and a base (prefix of mask popcounts, in the
 // counts area); an entry goes to base + popcount(mask below its column).
+template <class Sh>
 __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpStatic &S_, int32_t H, int32_t c0,
                                        int32_t c1, uint64_t &rsum) {
   const int tid = threadIdx.x;
   const unsigned long long c_h0 = STAT_CLOCK();
-  uint32_t *keys = L.R, *cnts = L.R + kHashMax;
-  const int per = H / kSpThreads;
+  uint32_t *keys = L.R, *cnts = L.R + Sh::kHashMax;
+  const int per = H / Sh::kThreads;
   const int32_t nL1 = (c1 - c0 + 1023) >> 10;
-  uint32_t ek[kHashMax / kSpThreads], ec[kHashMax / kSpThreads], er[kHashMax / kSpThreads];
-  // the table swept 4 slots (16 B) per LDS access: thread tid takes slots 4 (tid + q kSpThreads) .. + 3
+  uint32_t ek[Sh::kHashMax / Sh::kThreads], ec[Sh::kHashMax / Sh::kThreads], er[Sh::kHashMax / Sh::kThreads];
+  // the table swept 4 slots (16 B) per LDS access: thread tid takes slots 4 (tid + q kThreads) .. + 3
   (void)per;
 #pragma unroll
-  for (int q = 0; q < kHashMax / (4 * kSpThreads); q++) {
-    const int j = 4 * (tid + q * kSpThreads);
+  for (int q = 0; q < Sh::kHashMax / (4 * Sh::kThreads); q++) {
+    const int j = 4 * (tid + q * Sh::kThreads);
     uint4 k4 = make_uint4(0u, 0u, 0u, 0u), v4 = k4;
     if (j < H) {
       k4 = *reinterpret_cast<const uint4 *>(keys + j);
@@ -1283,15 +1361,15 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   __syncthreads();
   uint32_t nblk;
   {
-    static_assert(kL1Words % kSpThreads == 0, "L1 words per thread");
-    constexpr int kW = kL1Words / kSpThreads;  // consecutive L1 words per thread
+    static_assert(Sh::kL1Words % Sh::kThreads == 0, "L1 words per thread");
+    constexpr int kW = Sh::kL1Words / Sh::kThreads;  // consecutive L1 words per thread
     uint32_t pc[kW], x = 0;
 #pragma unroll
     for (int i = 0; i < kW; i++) {
       pc[i] = kW * tid + i < nL1 ? uint32_t(__popc(L.L1[kW * tid + i])) : 0u;
       x += pc[i];
     }
-    const uint32_t p = block_excl_scan(x, &nblk, S_.wtot);
+    const uint32_t p = block_excl_scan<Sh::kWaves>(x, &nblk, S_.wtot);
     uint32_t run = p;
 #pragma unroll
     for (int i = 0; i < kW; i++) {
@@ -1301,7 +1379,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kHashMax / kSpThreads; i++) {
+  for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) {
     if (ek[i] == ~0u) continue;
     const uint32_t col = ek[i], wd = col >> 10, bit = (col >> 5) & 31u;
     const uint32_t r = L.L1pre[wd] + uint32_t(__popc(L.L1[wd] & ((1u << bit) - 1u)));
@@ -1309,32 +1387,32 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     atomicOr(&keys[r], 1u << (col & 31u));
   }
   __syncthreads();
-  const uint32_t pb = (nblk + kSpThreads - 1) / kSpThreads;
+  const uint32_t pb = (nblk + Sh::kThreads - 1) / Sh::kThreads;
   const uint32_t r0 = min(nblk, uint32_t(tid) * pb), r1 = min(nblk, r0 + pb);
   uint32_t local = 0;
   for (uint32_t r = r0; r < r1; r++) local += uint32_t(__popc(keys[r]));
   uint32_t ne;
-  uint32_t run = block_excl_scan(local, &ne, S_.wtot);
+  uint32_t run = block_excl_scan<Sh::kWaves>(local, &ne, S_.wtot);
   for (uint32_t r = r0; r < r1; r++) {
     cnts[r] = run;
     run += uint32_t(__popc(keys[r]));
   }
   const unsigned long long c_h1 = STAT_CLOCK();
   STAT_ADD(20, c_h1 - c_h0);
-  const int64_t base = sp_reserve(A, S_, ne);  // (barrier: bases visible)
+  const int64_t base = sp_reserve<Sh>(A, S_, ne);  // (barrier: bases visible)
   const unsigned long long c_h2 = STAT_CLOCK();
   STAT_ADD(21, c_h2 - c_h1);
 #ifndef COOC_SP_NO_STAGED_WRITE
-  if (base >= 0 && ne <= uint32_t(kWStage)) {
+  if (base >= 0 && ne <= uint32_t(Sh::kWStage)) {
     // the chunk's entries land in LDS at their sorted positions (the free upper halves of the emptied key
     // and count areas), then leave in order: 16-B stores of whole column / count runs instead of one
     // scattered 4-B store per entry and array
-    uint32_t *sc = keys + kWStage, *sn = cnts + kWStage;
+    uint32_t *sc = keys + Sh::kWStage, *sn = cnts + Sh::kWStage;
     // (after a relabel a column maps back by a lookup in tile 0's 64 KB table, a subtraction above)
     const bool hot0 = A.hot_col && c0 < kTW;
     const uint32_t shift = A.hot_col ? uint32_t(kTW) : 0u;
 #pragma unroll
-    for (int i = 0; i < kHashMax / kSpThreads; i++) {
+    for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) {
       if (ek[i] == ~0u) continue;
       const uint32_t col = ek[i], r = er[i];
       const uint32_t q = cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
@@ -1345,23 +1423,23 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     __syncthreads();
     const uint32_t head = min(ne, uint32_t((4 - (base & 3)) & 3));  // entries before the first 16-B boundary
     const uint32_t body = (ne - head) >> 2;
-    for (uint32_t j = tid; j < head; j += kSpThreads) {
+    for (uint32_t j = tid; j < head; j += Sh::kThreads) {
       A.col_out[base + j] = int32_t(sc[j]);
       A.cnt_out[base + j] = sn[j];
     }
     int4 *co4 = reinterpret_cast<int4 *>(A.col_out + base + head);
     uint4 *cn4 = reinterpret_cast<uint4 *>(A.cnt_out + base + head);
-    for (uint32_t j = tid; j < body; j += kSpThreads) {
+    for (uint32_t j = tid; j < body; j += Sh::kThreads) {
       const uint32_t q = head + 4 * j;
       co4[j] = make_int4(int32_t(sc[q]), int32_t(sc[q + 1]), int32_t(sc[q + 2]), int32_t(sc[q + 3]));
       cn4[j] = make_uint4(sn[q], sn[q + 1], sn[q + 2], sn[q + 3]);
     }
-    for (uint32_t q = head + 4 * body + tid; q < ne; q += kSpThreads) {
+    for (uint32_t q = head + 4 * body + tid; q < ne; q += Sh::kThreads) {
       A.col_out[base + q] = int32_t(sc[q]);
       A.cnt_out[base + q] = sn[q];
     }
     __syncthreads();
-    for (uint32_t q = tid; q < ne; q += kSpThreads) {  // the areas go back to zero for the next chunk
+    for (uint32_t q = tid; q < ne; q += Sh::kThreads) {  // the areas go back to zero for the next chunk
       sc[q] = 0u;
       sn[q] = 0u;
     }
@@ -1369,7 +1447,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
 #endif
   if (base >= 0) {
 #pragma unroll
-    for (int i = 0; i < kHashMax / kSpThreads; i++) {
+    for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) {
       if (ek[i] == ~0u) continue;
       const uint32_t col = ek[i], r = er[i];
       const int64_t pos = base + cnts[r] + uint32_t(__popc(keys[r] & ((1u << (col & 31u)) - 1u)));
@@ -1382,36 +1460,39 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
   __syncthreads();
   STAT_ADD(22, STAT_CLOCK() - c_h2);
   STAT_ADD(23, ne);
-  for (uint32_t r = tid; r < nblk; r += kSpThreads) {
+  for (uint32_t r = tid; r < nblk; r += Sh::kThreads) {
     keys[r] = 0u;
     cnts[r] = 0u;
   }
-  for (int32_t i = tid; i < nL1; i += kSpThreads) L.L1[i] = 0u;
+  for (int32_t i = tid; i < nL1; i += Sh::kThreads) L.L1[i] = 0u;
   __syncthreads();
 }
 
 // The workgroup loop.  A work item is a whole row (its chunks in column order, appended to the row's
 // contiguous output) or a split row's (tile, contribution share), added into the staging row.  One
 // code path for every chunk kind, so that the walk and the two compactions exist once.
-__global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_main(SpArgs A) {  // 2 workgroups per CU: <= 128 VGPRs
+// The shape (SpBig: 512 threads, two workgroups per CU; SpMid: 256 threads, four per CU) fixes the LDS layout;
+// both keep 4 waves per SIMD (<= 128 VGPRs).  A launch takes the queue range [A.q_begin, A.q_end).
+template <class Sh>
+__global__ __launch_bounds__(Sh::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_main(SpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ SpStatic S_;
   SpShared L;
   L.R = lds;
-  L.L1 = L.R + kTW;
-  L.L1pre = L.L1 + kL1Words;
-  L.gb = reinterpret_cast<int32_t *>(L.L1pre + kL1Words);
-  L.info = reinterpret_cast<uint32_t *>(L.gb + kSpDb);
-  L.vst = L.info + kSpDb;
-  L.qstart = reinterpret_cast<int32_t *>(L.vst + kSpDb + 4);
+  L.L1 = L.R + Sh::kRWords;
+  L.L1pre = L.L1 + Sh::kL1Words;
+  L.gb = reinterpret_cast<int32_t *>(L.L1pre + Sh::kL1Words);
+  L.info = reinterpret_cast<uint32_t *>(L.gb + Sh::kDb);
+  L.vst = L.info + Sh::kDb;
+  L.qstart = reinterpret_cast<int32_t *>(L.vst + Sh::kDb + 4);
   const int tid = threadIdx.x;
-  for (int32_t i = tid; i < kTW + kL1Words; i += kSpThreads) L.R[i] = 0u;
+  for (int32_t i = tid; i < Sh::kRWords + Sh::kL1Words; i += Sh::kThreads) L.R[i] = 0u;
   if (tid == 0) {
     S_.slab_cur = S_.slab_end = 0;
     S_.flag = 0u;
   }
-  // (the queue's tail: the small rows (k_sp_small), then the tiny ones (k_sp_tiny))
-  const int64_t n_work = A.tot->n_chunks - A.tot->n_tiny - A.tot->n_small;
+  // (the queue's tail: the mid rows (the mid shape's launch), the small rows (k_sp_small), the tiny ones (k_sp_tiny))
+  const int64_t n_work = A.q_end - A.q_begin;
 #ifdef COOC_SP_STATS
   if (threadIdx.x < 48) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
@@ -1425,7 +1506,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
     // the next item is dequeued now and read at the end of this one (its latency hides behind the work)
     uint32_t next = 0;
     if (tid == 0) next = atomicAdd(A.qctr, 1);
-    const SpWork it = A.queue[w];
+    const SpWork it = A.queue[A.q_begin + w];
     const int32_t a = it.row;
     const int32_t ra = sp_rank(A, a);  // the row's own column (the self term), in column-rank space
     const bool split = it.kind == -2;  // a share of a split row's contributions, every tile, into staging
@@ -1488,7 +1569,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
       if (!dense) {
         const uint64_t rest = t + 1 < 64 ? st >> (t + 1) : 0ull;
         t1 = rest ? min(t_end, t + __ffsll((long long)rest)) : t_end;
-        if (H == 0) H = kHashMin << (((t < 32 ? hz0 : hz1) >> (2 * (t & 31))) & 3u);  // the planner's size
+        if (H == 0) H = min(Sh::kHashMax, kHashMin << (((t < 32 ? hz0 : hz1) >> (2 * (t & 31))) & 3u));  // the planner's size
       }
       const int32_t c0 = t * kTW, c1 = min(A.M, t1 * kTW);
       WalkOp op;
@@ -1506,7 +1587,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
       uint64_t walked;
       if (gather && t == 0) {  // tile 0 (a dense chunk) counted, the other tiles' groups to their buckets
         op.mode = 2;
-        walked = sp_walk(A, L, S_, k0, k1, 0, A.T, true, op);
+        walked = sp_walk<Sh>(A, L, S_, k0, k1, 0, A.T, true, op);
         if (tid < 64) {
           const bool o = tid >= 1 && tid < A.T && S_.bcur[tid] > S_.bstart[tid + 1] - S_.bstart[tid];
           const uint64_t m = __ballot(o);
@@ -1518,9 +1599,9 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const int nb = t1 - t;
         const uint32_t bs = tid < nb ? S_.bstart[t + tid] : 0u;
         const uint32_t be = tid < nb ? bs + S_.bcur[t + tid] : 0u;
-        walked = sp_walk_batch<4>(A, L, S_, A.scratch + op.sbase, A.scr_cap, nb, bs, be, op);
+        walked = sp_walk_batch<Sh, 4>(A, L, S_, A.scratch + op.sbase, A.scr_cap, nb, bs, be, op);
       } else {  // (also a gathered chunk whose bucket overflowed)
-        walked = sp_walk(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
+        walked = sp_walk<Sh>(A, L, S_, k0, k1, t, t1, !split && t == 0 && t1 == A.T, op);
       }
       const unsigned long long c_walked = STAT_CLOCK();
       STAT_ADD(split ? 4 : dense ? 0 : 1, c_walked - c_walk);
@@ -1540,9 +1621,9 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
       if (!dense && uni(S_.flag)) {
         STAT_ADD(7, 1);
         // overflow: clear the table (and the gather walk's state is this item's only); the row is deferred
-        for (int32_t j = tid; j < H; j += kSpThreads) {
+        for (int32_t j = tid; j < H; j += Sh::kThreads) {
           L.R[j] = 0u;
-          L.R[kHashMax + j] = 0u;
+          L.R[Sh::kHashMax + j] = 0u;
         }
         deferred = true;
         __syncthreads();  // every wave has read the flag and cleared its slots
@@ -1552,33 +1633,41 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(4)))
       const uint32_t self = uint32_t(A.spre ? A.spre[k1] - A.spre[k0] : k1 - k0);
       if (split) {
         uint32_t *dst = A.staging + int64_t(A.split_slot[a]) * A.sstride + c0;
-        for (int32_t i = tid; i < c1 - c0; i += kSpThreads) {
-          const uint32_t v = L.R[i];
-          if (v) {
-            atomicAdd(dst + i, v);
-            L.R[i] = 0u;
+        if (!Sh::kU16) {  // (split rows are never mid rows)
+          for (int32_t i = tid; i < c1 - c0; i += Sh::kThreads) {
+            const uint32_t v = L.R[i];
+            if (v) {
+              atomicAdd(dst + i, v);
+              L.R[i] = 0u;
+            }
           }
         }
         __syncthreads();
         STAT_ADD(26, STAT_CLOCK() - c_walked);  // the share's flush of this tile into the staging row
       } else if (dense) {
-        if (tid == 0 && ra >= c0 && ra < c1) L.R[ra - c0] -= self;
+        if (tid == 0 && ra >= c0 && ra < c1) {
+          const uint32_t o = uint32_t(ra - c0);  // (the counter holds >= self: no borrow into the other u16)
+          if (Sh::kU16)
+            L.R[o >> 1] -= self << ((o & 1u) << 4);
+          else
+            L.R[o] -= self;
+        }
         __syncthreads();
-        sp_dense_compact(A, L, S_, c1 - c0, c0, rsum);
+        sp_dense_compact<Sh>(A, L, S_, c1 - c0, c0, rsum);
         STAT_ADD(2, STAT_CLOCK() - c_walked);
       } else {
         if (tid == 0 && ra >= c0 && ra < c1) {
           uint32_t h = (uint32_t(ra) * 0x9E3779B1u) >> op.hshift;
           for (int p = 0; p < H; p++) {
             if (L.R[h] == uint32_t(ra) + 1u) {
-              L.R[kHashMax + h] -= self;
+              L.R[Sh::kHashMax + h] -= self;
               break;
             }
             h = (h + 1u) & op.hmask;
           }
         }
         __syncthreads();
-        sp_hash_compact(A, L, S_, H, c0, c1, rsum);
+        sp_hash_compact<Sh>(A, L, S_, H, c0, c1, rsum);
         STAT_ADD(3, STAT_CLOCK() - c_walked);
 #ifdef COOC_SP_STATS
         STAT_ADD(30 + 6 * hcls, STAT_CLOCK() - c_walked);
@@ -1760,7 +1849,7 @@ __global__ void k_sp_reset_run(PlanTotals *__restrict__ tot, int32_t *__restrict
   tot->n_deferred = 0;
   tot->tiny_ctr = 0;
   tot->small_ctr = 0;
-  qctr[0] = 0;
+  qctr[0] = qctr[1] = 0;
   bump[0] = 0;
 }
 
@@ -2929,7 +3018,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                                             sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(),
                                             order_keys_.as<uint64_t>(),
                                             order_.as<int32_t>(), row_nch_.as<int32_t>(), row_nnz_.as<int32_t>(),
-                                            row_base_.as<int64_t>(), tot, spre, small_off_ ? 1 : 3);
+                                            row_base_.as<int64_t>(), tot, spre, (small_off_ ? 1 : 3) | (mid_off_ ? 0 : 4));
   k_sp_totals<<<1, 1, 0, s>>>(tot, epre, spre, n_c, qctr);  // n_chunks is recomputed below once n_split is final
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
@@ -2986,29 +3075,41 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   }
   // gather scratch: a bucket region per workgroup for the largest expected tail (+25%); a work item
   // whose exact tail is larger walks per chunk instead.  Skipped when memory is short.
-  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kSpLds));
-  int per_cu = 1;
-  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sp_main, kSpThreads, kSpLds));
-  const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_work, 1), int64_t(n_cu_) * std::max(1, per_cu));
-  int64_t scr_cap = 0;
-  if (h_tot_->max_tail > 0 && T < 64) {
-    scr_cap = std::min<int64_t>(kScrGroups, (h_tot_->max_tail + h_tot_->max_tail / 4 + 64 * T + 4096) / 4 + 1);
-    const size_t need = sizeof(uint4) * size_t(grid) * size_t(scr_cap);
+  // the two shapes' launches: the queue's big rows and split shares [0, n_big), then its mid rows
+  const int64_t n_tiny = h_tot_->n_tiny, n_small = h_tot_->n_small, n_mid = h_tot_->n_mid;
+  const int64_t n_big = n_work - n_tiny - n_small - n_mid;
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main<SpBig>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SpBig::kLds));
+  COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_sp_main<SpMid>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SpMid::kLds));
+  int per_cu = 1, per_cu_mid = 1;
+  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sp_main<SpBig>, SpBig::kThreads, SpBig::kLds));
+  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_mid, k_sp_main<SpMid>, SpMid::kThreads, SpMid::kLds));
+  const int64_t grid = std::min<int64_t>(std::max<int64_t>(n_big, 1), int64_t(n_cu_) * std::max(1, per_cu));
+  const int64_t grid_mid = std::min<int64_t>(std::max<int64_t>(n_mid, 1), int64_t(n_cu_) * std::max(1, per_cu_mid));
+  last_mid_grid_ = n_mid > 0 ? grid_mid : 0;
+  // gather scratch (per launch): a bucket region per workgroup for the largest expected tail (+25%); a work item
+  // whose exact tail is larger walks per chunk instead.  Skipped when memory is short.
+  auto scratch = [&](int64_t max_tail, int64_t g, DevBuf &buf) -> int64_t {
+    if (max_tail <= 0 || T >= 64) return 0;
+    const int64_t sc = std::min<int64_t>(kScrGroups, (max_tail + max_tail / 4 + 64 * T + 4096) / 4 + 1);
+    const size_t need = sizeof(uint4) * size_t(g) * size_t(sc);
     size_t f0 = 0, t0 = 0;
-    COOC_HIP_TRY(hipMemGetInfo(&f0, &t0));
-    if (need > sp_scr_.cap && (need > (f0 + sp_scr_.cap) / 4 || !sp_scr_.reserve(need).ok())) scr_cap = 0;
-  }
+    if (hipMemGetInfo(&f0, &t0) != hipSuccess) return 0;
+    if (need > buf.cap && (need > (f0 + buf.cap) / 4 || !buf.reserve(need).ok())) return 0;
+    return sc;
+  };
+  const int64_t scr_cap = scratch(h_tot_->max_tail, grid, sp_scr_);
+  const int64_t scr_cap_mid = n_mid > 0 ? scratch(h_tot_->max_tail_mid, grid_mid, sp_scr_mid_) : 0;
   const int64_t n_gather = T < 64 ? h_tot_->n_gather_rows + h_tot_->n_split_work : 0;  // gather items (bound)
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const int64_t slab = std::max<int64_t>(int64_t(1) << 16, std::min<int64_t>(int64_t(1) << 22, est_nnz / (8 * grid)));
-  const int64_t n_tiny = h_tot_->n_tiny;
   const int64_t grid_tiny = std::min<int64_t>((n_tiny + kTinyWaves - 1) / kTinyWaves, int64_t(n_cu_) * 8);
-  const int64_t n_small = h_tot_->n_small;
   const int64_t grid_small = std::min<int64_t>(n_small, int64_t(n_cu_) * 4);
-  const int64_t slack = 2 * grid * slab + M + (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0) +
+  const int64_t slack = 2 * grid * slab + (n_mid ? 2 * grid_mid * slab : 0) + M +
+                        (n_tiny ? grid_tiny * kTinyWaves * kTinySlab : 0) +
                         (n_small ? grid_small * kSmallSlab : 0) + 2 * int64_t(n_cu_) * kSmallSlab;  // (+ k_srb_row)
   int64_t cap = std::min<int64_t>(bound + slack, est_nnz + est_nnz / 4 + slack);
   const int64_t budget = int64_t((free_b + col_.cap + cnt_.cap) / 10 * 8 / 8);
@@ -3071,14 +3172,16 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
 #ifdef COOC_SP_STATS
     static unsigned long long *d_stats = nullptr;
-    if (!d_stats) hipMalloc(reinterpret_cast<void **>(&d_stats), 48 * 8);
-    hipMemsetAsync(d_stats, 0, 48 * 8, s);
+    if (!d_stats) (void)hipMalloc(reinterpret_cast<void **>(&d_stats), 96 * 8);
+    (void)hipMemsetAsync(d_stats, 0, 96 * 8, s);
     A.stats = d_stats;
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
-    if (n_work > n_tiny + n_small) {
-      k_sp_main<<<unsigned(grid), kSpThreads, kSpLds, s>>>(A);
+    A.q_begin = 0;
+    A.q_end = n_big;
+    if (n_big > 0) {
+      k_sp_main<SpBig><<<unsigned(grid), SpBig::kThreads, SpBig::kLds, s>>>(A);
       COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_TRACE
       for (int it = 0; it < 100 && hipStreamQuery(s) == hipErrorNotReady; it++) usleep(50000);
@@ -3101,6 +3204,19 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       hipStreamSynchronize(s);
       fprintf(stderr, "[sp] bounds flags %llx\n", prog[2047]);
 #endif
+    }
+    if (n_mid > 0) {  // the mid rows (after the big launch: it holds the heaviest rows)
+      SpArgs B = A;
+      B.qctr = qctr + 1;
+      B.q_begin = n_big;
+      B.q_end = n_big + n_mid;
+      B.scratch = scr_cap_mid ? sp_scr_mid_.as<uint4>() : nullptr;
+      B.scr_cap = (scr_cap_mid && n_gather) ? scr_cap_mid : 0;
+#ifdef COOC_SP_STATS
+      B.stats = A.stats + 48;
+#endif
+      k_sp_main<SpMid><<<unsigned(grid_mid), SpMid::kThreads, SpMid::kLds, s>>>(B);
+      COOC_HIP_TRY(hipGetLastError());
     }
     if (n_small > 0) {
       k_sp_small<<<unsigned(grid_small), kSmallThreads, 0, s>>>(A);
@@ -3140,9 +3256,13 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_STATS
     {
-      unsigned long long h[48];
-      hipMemcpy(h, A.stats, sizeof(h), hipMemcpyDeviceToHost);
-      const double g = double(grid);
+      unsigned long long hh[96];
+      (void)hipMemcpy(hh, A.stats, sizeof(hh), hipMemcpyDeviceToHost);
+      for (int shape = 0; shape < 2; shape++) {
+      const unsigned long long *h = hh + 48 * shape;
+      const double g = double(shape ? grid_mid : grid);
+      if (shape && !n_mid) break;
+      fprintf(stderr, "[sp stats] %s shape (%lld WGs):\n", shape ? "mid" : "big", (long long)(shape ? grid_mid : grid));
       fprintf(stderr, "[sp stats] per WG (us): total %.0f walk dense %.0f walk hash %.0f split %.0f compact dense %.0f "
               "compact hash %.0f | chunks dense %llu hash %llu overflows %llu deferred rows %llu | pairs dense %.3g hash %.3g | "
               "rows %llu split items %llu | mean H %.0f | tail sizes %.0f\n",
@@ -3162,6 +3282,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
                 c == 0 ? "light-row" : c == 1 ? "gathered" : "list-walk", q[0], q[1] / 100.0 / g,
                 q[0] ? q[1] / 100.0 / double(q[0]) : 0.0, q[2] / 100.0 / g, q[0] ? q[2] / 100.0 / double(q[0]) : 0.0,
                 q[0] ? double(q[3]) / q[0] : 0.0, q[0] ? double(q[4]) / q[0] : 0.0, q[0] ? double(q[5]) / q[0] : 0.0);
+      }
       }
       fprintf(stderr, "[sp stats] attempt %d: cap %lld slab %lld grid %lld err %lld scr_cap %lld n_gather %lld\n", attempt,
               (long long)cap, (long long)slab, (long long)grid, (long long)err, (long long)A.scr_cap, (long long)n_gather);

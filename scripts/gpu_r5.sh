@@ -8,15 +8,22 @@ ROOT=$(pwd)
 mkdir -p gpurun_out
 fatal() { case "$1" in 0|1) ;; *) echo "fatal rc=$1, stopping"; exit "$1";; esac; }
 if [ "${AB:-0}" = "1" ]; then
+  # same-box A/B of bench_c3 (rank-ordered and permuted ids): the default build against the env settings in
+  # ABENV (";"-separated, e.g. ABENV="COOC_SP_MID=0") and the libraries in ABLIB (space-separated .so paths)
+  IFS=';' read -ra ENVS <<< "${ABENV:-}"
   for pass in 1 2; do
-    for p in "" "--permute"; do
+    for p in "" ${AB_PERM---permute}; do
       n=rank; [ -n "$p" ] && n=perm
-      timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || exit 1
-      if [ "${AB_COLORDER:-0}" = "1" ]; then
-        timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p --column-order > gpurun_out/ab_${n}_co.json 2> gpurun_out/ab_${n}_co.err || exit 1
-        python -c "import json;d=json.load(open('gpurun_out/ab_${n}_co.json'));print('$n column-order', 'ms', round(d['ms'],2), 'k_sp_main', round(d['k_sp_main_ms'],2))"
-      fi
-      python -c "import json;d=json.load(open('gpurun_out/ab_$n.json'));print('$n', 'ms', round(d['ms'],2), 'k_sp_main', round(d['k_sp_main_ms'],2), 'nnz', d['nnz'], d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'])"
+      i=0
+      for e in "" "${ENVS[@]}"; do
+        env $e timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p > gpurun_out/ab_${n}_$i.json 2> gpurun_out/ab_${n}_$i.err || { echo "ab failed: $e"; tail -3 gpurun_out/ab_${n}_$i.err; exit 1; }
+        python -c "import json;d=json.load(open('gpurun_out/ab_${n}_$i.json'));print('$n [$e]', 'ms', round(d['ms'],2), 'span', round(d['k_sp_main_ms'],2), 'nnz', d['nnz'], d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'])"
+        i=$((i+1))
+      done
+      for l in ${ABLIB:-}; do
+        timeout -k 10 300 python -u scripts/bench_c3.py --steps 3 $p --lib $l > gpurun_out/ab_${n}_lib.json 2> gpurun_out/ab_${n}_lib.err || { echo "ab failed: $l"; exit 1; }
+        python -c "import json;d=json.load(open('gpurun_out/ab_${n}_lib.json'));print('$n [$l]', 'ms', round(d['ms'],2), 'span', round(d['k_sp_main_ms'],2), 'nnz', d['nnz'], d['verify']['rows_bad_sum'], d['verify']['rows_bad_entries'])"
+      done
     done
   done
 fi
@@ -62,6 +69,20 @@ if [ "${PROF:-0}" = "1" ]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$ROOT/gpurun_out/prof.log" 2>&1)
   rc=$?; echo "rocprof rc=$rc"; tail -1 "$ROOT/gpurun_out/prof.log" | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "${KPROF:-0}" = "1" ]; then
+  # per-kernel times of one C3 share count (scripts/bench_c3.py) under rocprofv3 --kernel-trace --stats
+  export TMPDIR=/tmp
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/kprof" -o run --output-format csv \
+    -- python3 "$ROOT/scripts/bench_c3.py" --steps 2 ${KPROF_ARGS:-} > "$ROOT/gpurun_out/kprof.log" 2>&1)
+  rc=$?; echo "kprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python3 - "$ROOT/gpurun_out/kprof" <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
+rows = list(csv.DictReader(open(f)))
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:14]:
+    print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>4s} avg {float(r["AverageNs"])/1e6:8.3f} ms')
+PY
 fi
 if [ "${PMC:-0}" = "1" ]; then
   bash scripts/pmc_sparse.sh || exit 1

@@ -153,15 +153,27 @@ def llr_atol(observed: int) -> float:
 
 
 def assert_row_topk(size, vals, scores, want, rtol=1e-6, where="", atol=1e-9):
-    """One row's heap against the oracle's: scores within max(rtol |ref|, atol) (NaN where NaN), and the
-    identical heap layout when every score agrees bit for bit."""
+    """One row's heap against the oracle's: scores within max(rtol |ref|, atol) (NaN where NaN); the identical
+    heap layout when every score agrees bit for bit; otherwise (a score a few ulp off can move an item within
+    the heap, or swap two near-equal items at the boundary) the items whose scores lie clearly above the k-th
+    score -- more than the tolerance above it -- are the same set (SURVEY.md §8(a) parity item 4).
+    Returns True when the heap matched bit for bit (layout and scores)."""
     assert int(size) == len(want), f"{where}: heap size {size} != {len(want)}"
     wv = np.array([v for v, _ in want], np.int32)
     ws = np.array([x for _, x in want], np.float64)
     gs = np.asarray(scores[: int(size)], np.float64)
+    gv = np.asarray(vals[: int(size)])
     assert np.array_equal(np.isnan(gs), np.isnan(ws)), f"{where}: NaN scores differ"
     fin = ~np.isnan(ws)
-    assert np.all(np.abs(gs[fin] - ws[fin]) <= np.maximum(rtol * np.abs(ws[fin]), atol)), (
+    tol = np.maximum(rtol * np.abs(ws[fin]), atol)
+    assert np.all(np.abs(gs[fin] - ws[fin]) <= tol), (
         f"{where}: scores differ by up to {np.max(np.abs(gs[fin] - ws[fin])) if fin.any() else 0} (atol {atol})")
     if np.array_equal(gs[fin], ws[fin]):
-        assert np.array_equal(np.asarray(vals[: int(size)]), wv), f"{where}: heap layout differs"
+        assert np.array_equal(gv, wv), f"{where}: heap layout differs"
+        return True
+    if fin.all() and len(ws):
+        kth = float(np.min(ws))
+        margin = 2 * float(np.max(tol))
+        assert set(gv[gs > kth + margin].tolist()) == set(wv[ws > kth + margin].tolist()), (
+            f"{where}: items above the k-th score differ")
+    return False

@@ -156,11 +156,15 @@ def test_c5_topk_benched_share_vs_oracle(pkg, oracle, torch_cuda):
     assert len(nan_root) > 0, "the benched share has NaN heap roots (int16 wraps): they must be covered"
     atol = llr_atol(observed)
     worst = 0.0
+    exact = 0
     for j, a in enumerate(rows.tolist()):
         want = [(int(w_v[j, i]), float(w_sc[j, i])) for i in range(int(w_sz[j]))]
-        assert_row_topk(sz[a], v[a], sc[a], want, where=f"row {a}", atol=atol)
+        exact += assert_row_topk(sz[a], v[a], sc[a], want, where=f"row {a}", atol=atol)
         fin = ~np.isnan(w_sc[j, :w_sz[j]])
         if fin.any():
             worst = max(worst, float(np.max(np.abs(sc[a, :w_sz[j]][fin] - w_sc[j, :w_sz[j]][fin]))))
     print(f"largest score difference {worst:.3g} (bound {atol:.3g})")
-    print(f"checked {len(rows)} heaps ({len(nan_root)} with a NaN root) over {int(rp[-1])} entries")
+    print(f"checked {len(rows)} heaps ({len(nan_root)} with a NaN root) over {int(rp[-1])} entries; "
+          f"{exact} ({exact / len(rows):.1%}) identical bit for bit (layout and every score)")
+    # the device log and glibc's differ by an ulp now and then; most heaps must still match exactly
+    assert exact >= 0.9 * len(rows), f"only {exact} of {len(rows)} heaps match bit for bit"
