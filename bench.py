@@ -344,12 +344,12 @@ def main():
         # the rescoring pass (cooc_topk_batch_device: k_col_terms + k_rescore) against its own bytes: every
         # entry streamed once (col + cnt, 8 B), the per-row CSR header and row sums (20 B per row), the heaps
         # written (sizes 4 B + k x (value 4 B + score 8 B) per row); the per-column LLR terms it gathers are
-        # counted once (16 B per column) -- their re-reads hit L2 / the Infinity Cache
+        # counted once (32 B per column) -- their re-reads hit L2 / the Infinity Cache
         pmc_rs = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_rescore.json"))
         rs_stale = bool(pmc_rs) and pmc_rs.get("source_digest") != digest
         if rs_stale:
             pmc_rs = {"kernel": "k_rescore", "stale_source_digest": pmc_rs.get("source_digest")}
-        b_rs = 8.0 * D + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 16.0 * M
+        b_rs = 8.0 * D + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
         a_rs = b_rs / (tk * 1e-3) / 1e9
         t_rs = pmc_rs.get("hbm_bytes_per_launch")
         out["roofline_rescore"] = {
@@ -361,8 +361,8 @@ def main():
             "valu_busy": pmc_rs.get("valu_busy"), "limiter": limiter(pmc_rs, t_rs, tk),
             "pmc_source_digest": pmc_rs.get("source_digest") or pmc_rs.get("stale_source_digest"),
             "pmc_stale": rs_stale,
-            "note": "B = 8D + 20M + M(4 + 12k) + 16M per launch (entries streamed, row headers and sums, heaps, "
-                    "16-B column terms), over the HIP-event time of the rescoring call; the PMC (traffic, L2 hit) "
+            "note": "B = 8D + 20M + M(4 + 12k) + 32M per launch (entries streamed, row headers and sums, heaps, "
+                    "32-B column terms), over the HIP-event time of the rescoring call; the PMC (traffic, L2 hit) "
                     "shows how far the column-term gathers (one cache line per missed sparse entry) inflate the "
                     "bytes actually fetched (DESIGN.md §4)",
         }

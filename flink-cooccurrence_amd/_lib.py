@@ -117,6 +117,7 @@ _SIGS = {
     "cooc_copy_column_order": (ctypes.c_int, [vp, i32p]),
     "cooc_count_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocWindowInfo)]),
     "cooc_copy_batch": (ctypes.c_int, [vp, i64p, i32p, u32p, i16p, i64p, i32p]),
+    "cooc_copy_batch_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, i32p, u32p, i16p]),
     "cooc_topk_batch": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
     "cooc_copy_topk_batch": (ctypes.c_int, [vp, i32p, i32p, f64p]),
     "cooc_topk_batch_device": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
@@ -149,6 +150,9 @@ _SIGS = {
     "cooc_topk_owned": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "cooc_count_owned_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocOwnedInfo),
                                              ctypes.POINTER(CoocWindowInfo)]),
+    "cooc_topk_owned_host": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
+    "cooc_copy_topk_batch_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, i32p, i32p, f64p]),
+    "cooc_comm_allgather_i64": (ctypes.c_int, [vp, ctypes.c_int64, i64p]),
     "cooc_snake_owner": (ctypes.c_int, [i64p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p]),
     "cooc_shard_plan": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp,
                                        ctypes.c_int64, vp, i64p, i64p]),

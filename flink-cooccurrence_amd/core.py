@@ -359,6 +359,51 @@ class CooccurrenceCore:
                                       ctypes.byref(winfo)), self._h)
         return self.copy_batch(winfo.nnz, winfo.observed), info
 
+    def count_owned_host_info(self, user_ptr, items):
+        """cooc_count_owned_host without copying the owned rows out: (CoocWindowInfo, CoocOwnedInfo); the rows
+        then stream out with copy_batch_row_ptr / copy_batch_range (what the JVM operators do)."""
+        up = np.ascontiguousarray(user_ptr, np.int64)
+        it = np.ascontiguousarray(items, np.int32)
+        info, winfo = CoocOwnedInfo(), CoocWindowInfo()
+        check(_lib.load().cooc_count_owned_host(self._h, len(up) - 1, _p(up, i64p), _p(it, i32p), ctypes.byref(info),
+                                                ctypes.byref(winfo)), self._h)
+        return winfo, info
+
+    def copy_batch_row_ptr(self):
+        """(row_ptr int64[M + 1], rowsum int64[M], rowsum32 int32[M]) of the last batch (cooc_copy_batch with
+        the entry arrays NULL)."""
+        M = self.n_items
+        rp, rs, rs32 = np.zeros(M + 1, np.int64), np.zeros(M, np.int64), np.zeros(M, np.int32)
+        check(_lib.load().cooc_copy_batch(self._h, _p(rp, i64p), None, None, None, _p(rs, i64p), _p(rs32, i32p)),
+              self._h)
+        return rp, rs, rs32
+
+    def copy_batch_range(self, r0: int, r1: int, cap: int):
+        """cooc_copy_batch_range: (cols int32, cnt uint32, cnt16 int16) of rows [r0, r1), at most cap entries."""
+        cols, cnt, cnt16 = np.zeros(cap, np.int32), np.zeros(cap, np.uint32), np.zeros(cap, np.int16)
+        check(_lib.load().cooc_copy_batch_range(self._h, int(r0), int(r1), int(cap), _p(cols, i32p), _p(cnt, u32p),
+                                                _p(cnt16, i16p)), self._h)
+        return cols, cnt, cnt16
+
+    def topk_owned_host(self, topk: int, exact_scores: bool = False) -> None:
+        """cooc_topk_owned_host: the owned rows' heaps into the context's buffers (copy_topk_range reads them)."""
+        check(_lib.load().cooc_topk_owned_host(self._h, int(topk), _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0),
+              self._h)
+
+    def copy_topk_range(self, r0: int, r1: int, topk: int):
+        """cooc_copy_topk_batch_range: (sizes [n], values [n, k], scores [n, k]) of rows [r0, r1)."""
+        n = int(r1) - int(r0)
+        sizes, vals, scores = np.zeros(n, np.int32), np.zeros((n, topk), np.int32), np.zeros((n, topk), np.float64)
+        check(_lib.load().cooc_copy_topk_batch_range(self._h, int(r0), int(r1), _p(sizes, i32p), _p(vals, i32p),
+                                                     _p(scores, f64p)), self._h)
+        return sizes, vals, scores
+
+    def comm_allgather_i64(self, value: int) -> np.ndarray:
+        """cooc_comm_allgather_i64: every rank's value, in rank order."""
+        out = np.zeros(self.comm_world, np.int64)
+        check(_lib.load().cooc_comm_allgather_i64(self._h, int(value), _p(out, i64p)), self._h)
+        return out
+
     def count_owned(self, user_ptr, items, stream=None):
         """cooc_count_owned: this rank's users -> the rows it owns over the whole job's users (item
         counts all-reduced, owner map, histories all-gathered, owned rows counted, pairs all-reduced),

@@ -170,6 +170,40 @@ int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cn
   });
 }
 
+int cooc_copy_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int64_t cap, int32_t *cols, uint32_t *cnt,
+                          int16_t *cnt16) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    Status s = ctx->copy_batch_range(row_begin, row_end, cap, cols, cnt, cnt16);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *sizes, int32_t *values,
+                               double *scores) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    Status s = ctx->copy_topk_batch_range(row_begin, row_end, sizes, values, scores);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_topk_owned_host(cooc_ctx *ctx, int32_t topk, int32_t flags) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx) return COOC_ERR_ARG;
+    Status s = ctx->topk_owned_host(topk, flags);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_comm_allgather_i64(cooc_ctx *ctx, int64_t value, int64_t *out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx || !out) return COOC_ERR_ARG;
+    Status s = ctx->comm_allgather_i64(value, out);
+    return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
 int cooc_topk_batch(cooc_ctx *ctx, int32_t topk, int32_t flags, void *hip_stream) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;

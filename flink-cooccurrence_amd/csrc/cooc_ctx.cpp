@@ -138,6 +138,7 @@ cooc::Status cooc_ctx::finish_batch(const cooc::CountResult &r, hipStream_t s, c
   out->rowsum = r.rowsum;
   out->dense = r.dense;
   have_batch = true;
+  batch_packed = false;
   batch_result = r;
   batch_result.nnz = nnz;
   batch_observed = r.observed;
@@ -251,6 +252,89 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
     if (rowsum32)  // Java int accumulation (RowSumAggregator.java:25-27, Int2IntOpenHashMap.addTo)
       for (int32_t a = 0; a < M; a++) rowsum32[a] = int32_t(uint32_t(uint64_t(tmp[a])));
   }
+  return Status::Ok();
+}
+
+Status cooc_ctx::copy_batch_range(int32_t r0, int32_t r1, int64_t cap, int32_t *cols, uint32_t *cnt, int16_t *cnt16) {
+  if (!have_batch) return Status{COOC_ERR_STATE, "no batch result on this context"};
+  const int32_t M = cfg.n_items;
+  if (r0 < 0 || r1 > M || r0 > r1) return Status{COOC_ERR_ARG, "bad row range"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  if (!batch_packed) {
+    COOC_TRY(counter.pack(stream, &batch_pk_rp, &batch_pk_col, &batch_pk_cnt));
+    batch_rp_host.resize(size_t(M) + 1);
+    COOC_HIP_TRY(hipMemcpyAsync(batch_rp_host.data(), batch_pk_rp, sizeof(int64_t) * (size_t(M) + 1), hipMemcpyDeviceToHost,
+                                stream));
+    COOC_HIP_TRY(hipStreamSynchronize(stream));
+    batch_packed = true;
+  }
+  const int64_t e0 = batch_rp_host[size_t(r0)], e1 = batch_rp_host[size_t(r1)], n = e1 - e0;
+  if (n > cap) return Status{COOC_ERR_ARG, "rows [" + std::to_string(r0) + ", " + std::to_string(r1) + ") hold " +
+                                               std::to_string(n) + " entries, more than " + std::to_string(cap)};
+  if (n == 0 || (!cols && !cnt && !cnt16)) return Status::Ok();
+  std::vector<int32_t> cc(static_cast<size_t>(n));
+  std::vector<uint32_t> vv(static_cast<size_t>(n));
+  COOC_HIP_TRY(hipMemcpy(cc.data(), batch_pk_col + e0, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
+  COOC_HIP_TRY(hipMemcpy(vv.data(), batch_pk_cnt + e0, sizeof(uint32_t) * size_t(n), hipMemcpyDeviceToHost));
+  if (batch_result.rank_of) {  // ascending column order, as cooc_copy_batch
+    std::vector<uint64_t> kv;
+    for (int32_t a = r0; a < r1; a++) {
+      const int64_t b0 = batch_rp_host[size_t(a)] - e0, b1 = batch_rp_host[size_t(a) + 1] - e0;
+      kv.resize(size_t(b1 - b0));
+      for (int64_t i = b0; i < b1; i++) kv[size_t(i - b0)] = (uint64_t(uint32_t(cc[size_t(i)])) << 32) | vv[size_t(i)];
+      std::sort(kv.begin(), kv.end());
+      for (int64_t i = b0; i < b1; i++) {
+        cc[size_t(i)] = int32_t(kv[size_t(i - b0)] >> 32);
+        vv[size_t(i)] = uint32_t(kv[size_t(i - b0)]);
+      }
+    }
+  }
+  if (cols) std::copy(cc.begin(), cc.end(), cols);
+  if (cnt) std::copy(vv.begin(), vv.end(), cnt);
+  if (cnt16)  // Int2ShortOpenHashMap value: the count modulo 2^16 as a signed short
+    for (int64_t i = 0; i < n; i++) cnt16[i] = int16_t(uint16_t(vv[size_t(i)]));
+  return Status::Ok();
+}
+
+Status cooc_ctx::copy_topk_batch_range(int32_t r0, int32_t r1, int32_t *sizes, int32_t *values, double *scores) {
+  if (batch_topk <= 0) return Status{COOC_ERR_STATE, "cooc_topk_batch has not run"};
+  const int32_t M = cfg.n_items;
+  if (r0 < 0 || r1 > M || r0 > r1) return Status{COOC_ERR_ARG, "bad row range"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  const size_t n = size_t(r1 - r0), k = size_t(batch_topk);
+  if (sizes && n) COOC_HIP_TRY(hipMemcpy(sizes, b_tk_size.as<int32_t>() + r0, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (values && n)
+    COOC_HIP_TRY(hipMemcpy(values, b_tk_val.as<int32_t>() + size_t(r0) * k, sizeof(int32_t) * n * k, hipMemcpyDeviceToHost));
+  if (scores && n)
+    COOC_HIP_TRY(hipMemcpy(scores, b_tk_score.as<double>() + size_t(r0) * k, sizeof(double) * n * k, hipMemcpyDeviceToHost));
+  return Status::Ok();
+}
+
+Status cooc_ctx::topk_owned_host(int32_t topk, int32_t flags) {
+  if (topk <= 0) return Status{COOC_ERR_ARG, std::to_string(topk) + " is <= 0"};  // ItemRowRescorer...java:52-54
+  COOC_HIP_TRY(hipSetDevice(device));
+  const int32_t M = cfg.n_items;
+  COOC_TRY(b_tk_size.reserve(sizeof(int32_t) * M));
+  COOC_TRY(b_tk_val.reserve(sizeof(int32_t) * size_t(M) * topk));
+  COOC_TRY(b_tk_score.reserve(sizeof(double) * size_t(M) * topk));
+  COOC_TRY(topk_owned(topk, flags, b_tk_size.as<int32_t>(), b_tk_val.as<int32_t>(), b_tk_score.as<double>(), nullptr,
+                      stream));
+  COOC_HIP_TRY(hipStreamSynchronize(stream));
+  batch_topk = topk;
+  batch_topk_flags = flags & COOC_FLAG_EXACT_SCORES;
+  return Status::Ok();
+}
+
+Status cooc_ctx::comm_allgather_i64(int64_t value, int64_t *out) {
+  if (!comm) return Status{COOC_ERR_STATE, "cooc_comm_allgather_i64 needs a communicator (cooc_comm_init)"};
+  COOC_HIP_TRY(hipSetDevice(device));
+  const int32_t W = comm->world();
+  COOC_TRY(own_obs.reserve(sizeof(int64_t) * size_t(W + 1)));
+  int64_t *d = own_obs.as<int64_t>();
+  COOC_HIP_TRY(hipMemcpyAsync(d, &value, sizeof(int64_t), hipMemcpyHostToDevice, stream));
+  COOC_TRY(comm->allgather(d, d + 1, sizeof(int64_t), stream));
+  COOC_HIP_TRY(hipMemcpyAsync(out, d + 1, sizeof(int64_t) * size_t(W), hipMemcpyDeviceToHost, stream));
+  COOC_HIP_TRY(hipStreamSynchronize(stream));
   return Status::Ok();
 }
 

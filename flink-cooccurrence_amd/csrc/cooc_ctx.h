@@ -136,6 +136,11 @@ struct cooc_ctx {
   cooc::Status topk_batch_device(int32_t topk, int32_t flags, const int64_t *d_rowsum_global, int32_t *d_sizes,
                                  int32_t *d_values, double *d_scores, hipStream_t s);
   cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
+  // row ranges of the batch result / its top-k (a JVM operator's copy-out: no single Java array holds a C3 share)
+  cooc::Status copy_batch_range(int32_t r0, int32_t r1, int64_t cap, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
+  cooc::Status copy_topk_batch_range(int32_t r0, int32_t r1, int32_t *sizes, int32_t *values, double *scores);
+  cooc::Status topk_owned_host(int32_t topk, int32_t flags);
+  cooc::Status comm_allgather_i64(int64_t value, int64_t *out);
   // cooc_verify_batch: invariant checks + row fingerprints of the last batch result
   cooc::Status verify_batch(int32_t flags, uint64_t *d_row_checksum, int64_t *out8, hipStream_t s);
   cooc::Status llr(int64_t n, const int64_t *k, double *out);
@@ -178,4 +183,10 @@ struct cooc_ctx {
   bool batch_owned = false;  // the last batch counted only the rows of one part (cooc_count_device_owned)
   int64_t batch_observed = 0;
   int64_t batch_nnz = 0;
+  // the batch result packed for range copies (once per batch): its row offsets on the host
+  bool batch_packed = false;
+  std::vector<int64_t> batch_rp_host;
+  int64_t *batch_pk_rp = nullptr;
+  int32_t *batch_pk_col = nullptr;
+  uint32_t *batch_pk_cnt = nullptr;
 };

@@ -114,7 +114,7 @@ constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 
 // compaction), so more independent chunks per CU hide more of them.  The LDS budget (40 KB per workgroup)
 // holds because a count never exceeds its row's pair work W <= 65,535: the dense tile's counters are u16,
 // two per LDS word (a ds_add of 1 << 16 for the odd column never carries), and hash tables have 4K slots
-// (chunks of half the expected keys) over column spans of at most 2^19 (a 512-word block bitmap).
+// (chunks of half the expected keys) over column spans of at most 2^18 (a 256-word block bitmap).
 #ifndef COOC_SP_MID_W
 #define COOC_SP_MID_W 65535
 #endif
@@ -134,7 +134,7 @@ struct SpShape {
   static constexpr int kLds = kRWords * 4 + 2 * L1Words * 4 + Db * 8 + (Db + 4) * 4 + Threads;
 };
 using SpBig = SpShape<kSpThreads, kHashMax, kL1Words, kSpDb, false>;
-using SpMid = SpShape<256, 4096, 512, 256, true>;
+using SpMid = SpShape<256, 4096, 256, 256, true>;  // 38.9 KB of LDS with the static part: four per CU
 static_assert(SpBig::kLds == kSpLds, "the big shape is the original kernel");
 constexpr float kHashFillMid = COOC_SP_FILL * SpMid::kHashMax;
 

@@ -134,15 +134,6 @@ __device__ inline double llr(int64_t k11, int64_t k12, int64_t k21, int64_t k22)
   return 2.0 * (row + column - matrix);
 }
 
-// An entry with k11 == 1 (xlogx(k11) = 0, so all - x_k11 == all exactly): row and column precomputed per row and
-// per column, m1 = all - xLogX(k12) per row; the same operations in the same order as llr_terms.
-__device__ inline double llr_fast(double row, double column, double m1, double x_k21, double x_k22) {
-#pragma clang fp contract(off)
-  const double matrix = m1 - x_k21 - x_k22;
-  if (row + column < matrix) return 0.0;
-  return 2.0 * (row + column - matrix);
-}
-
 // The same function over precomputed x log x terms, in the same operation order (bit-identical when
 // every term is: a term looked up from a table was computed by the same xlogx of the same integer).
 __device__ inline double llr_terms(double all, double x_k11k12, double x_k21k22, double x_k11k21, double x_k12k22,
@@ -156,29 +147,24 @@ __device__ inline double llr_terms(double all, double x_k11k12, double x_k21k22,
 }
 
 // Per column b of the rescored rows (the int32 view of its row sum unless exact): rs = rowSum(b) and the
-// part of an entry's LLR with k11 == 1 that depends on b only (ItemRowRescorer...java:230-240): with
-// k11 == 1, k11 + k12 + k21 + k22 = observed + 2 for EVERY entry, so LogLikelihood.java:52's
-//   column = all - xLogX(k11 + k21) - xLogX(k12 + k22) = (xlogx(observed + 2) - xlogx(rs)) - xlogx(observed + 2 - rs)
-// is a per-column constant, computed here in Java's operation order (bit-identical).  16 B per column: a
-// 128-B line holds 8 columns (the table is 16 MB at 1e6 items, half the former 32-B record's, whose gathers
-// bounded k_rescore); the fast path recomputes xlogx(rs - 1) (one more log per entry) instead of loading it.
+// terms of an entry with k11 == 1 that depend on b only (ItemRowRescorer...java:230-240): k11 + k21 =
+// rs, k21 = rs - 1, k12 + k22 = observed + 2 - rs.  32 B per column, one line per gathered entry.
 constexpr int kRsR = 8;  // 64-entry steps scored before the heap is fed (per wave)
 constexpr int64_t kRsChunk = kRsR * 64;
-struct alignas(16) ColTerms {
+struct alignas(32) ColTerms {
   int64_t rs;
-  double column;  // (xlogx(observed + 2) - xlogx(rs)) - xlogx(observed + 2 - rs)
+  double x_rs;   // xlogx(rs)
+  double x_rs1;  // xlogx(rs - 1)
+  double x_or2;  // xlogx(observed + 2 - rs)
 };
-static_assert(sizeof(ColTerms) == 16, "16-B column terms");
 
 __global__ void k_col_terms(int32_t M, const int64_t *__restrict__ grs, const int64_t *__restrict__ obs, int32_t exact,
                             ColTerms *__restrict__ out) {
-#pragma clang fp contract(off)
   const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= M) return;
   const int64_t observed = exact ? obs[1] : obs[0];
   const int64_t rs = exact ? grs[b] : int64_t(int32_t(uint32_t(uint64_t(grs[b]))));
-  const double all = xlogx(observed + 2);
-  out[b] = ColTerms{rs, all - xlogx(rs) - xlogx(observed + 2 - rs)};
+  out[b] = ColTerms{rs, xlogx(rs), xlogx(rs - 1), xlogx(observed + 2 - rs)};
 }
 
 // xlogx(k11) and xlogx(observed + 2 k11) for every int16 k11 (index k11 + 32768; the second table at
@@ -253,15 +239,11 @@ struct CsrRows {
 struct RowTerms {
   int64_t observed, rs_a;
   double x_a, x_all1, x_r1, x_a1;
-  double row1, m1;  // k11 == 1: row = all - xLogX(k11 + k12) - xLogX(k21 + k22); m1 = (all - xLogX(k11)) - xLogX(k12)
   __device__ RowTerms(int64_t obs, int64_t rs) : observed(obs), rs_a(rs) {
-#pragma clang fp contract(off)
     x_a = xlogx(rs);
     x_all1 = xlogx(obs + 2);
     x_r1 = xlogx(obs + 2 - rs);
     x_a1 = xlogx(rs - 1);
-    row1 = x_all1 - x_a - x_r1;
-    m1 = x_all1 - 0.0 - x_a1;
   }
 };
 
@@ -309,7 +291,7 @@ __device__ inline void rs_score_chunk(const Rows &src, int64_t rb, int64_t i0, i
       if (fast) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
         const ColTerms &t = tg[g];
         const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (t.rs - k11);
-        score = llr_fast(R.row1, t.column, R.m1, xlogx(t.rs - k11), xlogx(k22));
+        score = llr_terms(R.x_all1, R.x_a, R.x_r1, t.x_rs, t.x_or2, 0.0, R.x_a1, t.x_rs1, xlogx(k22));
       }
       const bool slow = v != 0u && !fast;
       const uint64_t sm = __ballot(slow);
@@ -334,7 +316,7 @@ __device__ inline void rs_score_chunk(const Rows &src, int64_t rb, int64_t i0, i
     const bool in = k11 >= -32768 && k11 < 32768;
     const double x_all = in ? k11t[k11 + 32768 + 65536] : xlogx(k11 + k12 + (k21 + k22));
     const double x_11 = in ? k11t[k11 + 32768] : xlogx(k11);
-    rscore[idx] = llr_terms(x_all, R.x_a, xlogx(k21 + k22), xlogx(h.rs), xlogx(k12 + k22), x_11, xlogx(k12), xlogx(k21),
+    rscore[idx] = llr_terms(x_all, R.x_a, xlogx(k21 + k22), h.x_rs, xlogx(k12 + k22), x_11, xlogx(k12), xlogx(k21),
                             xlogx(k22));
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -285,3 +285,49 @@ JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_topKIte
   scratch_put(env, &z, 1, 'I', n);
   scratch_put(env, &i, 0, 'I', 0);
 }
+
+/* ---- owned rows / heaps in row ranges (C-ABI 6): a C3 share never fits one Java array ---- */
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyBatchRange(
+    JNIEnv *env, jclass cls, jlong h, jint rowBegin, jint rowEnd, jint n, jintArray cols, jshortArray cnt16) {
+  scratch c, v;
+  c.p = v.p = NULL;
+  if (!scratch_get(env, &c, cols, sizeof(jint), n, 0, 'I') && !scratch_get(env, &v, cnt16, sizeof(jshort), n, 0, 'S'))
+    check(env, H(h), cooc_copy_batch_range(H(h), rowBegin, rowEnd, n, (int32_t *)c.p, NULL, (int16_t *)v.p));
+  scratch_put(env, &v, 1, 'S', n);
+  scratch_put(env, &c, 1, 'I', n);
+}
+
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_topKOwned(
+    JNIEnv *env, jclass cls, jlong h, jint k, jint flags) {
+  check(env, H(h), cooc_topk_owned_host(H(h), k, flags));
+}
+
+JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyTopKRange(
+    JNIEnv *env, jclass cls, jlong h, jint rowBegin, jint rowEnd, jint k, jintArray sizes, jintArray values,
+    jdoubleArray scores) {
+  const jsize n = rowEnd - rowBegin;
+  scratch z, v, s;
+  z.p = v.p = s.p = NULL;
+  if (!scratch_get(env, &z, sizes, sizeof(jint), n, 0, 'I') && !scratch_get(env, &v, values, sizeof(jint), n * k, 0, 'I') &&
+      !scratch_get(env, &s, scores, sizeof(jdouble), n * k, 0, 'D'))
+    check(env, H(h), cooc_copy_topk_batch_range(H(h), rowBegin, rowEnd, (int32_t *)z.p, (int32_t *)v.p, (double *)s.p));
+  scratch_put(env, &s, 1, 'D', n * k);
+  scratch_put(env, &v, 1, 'I', n * k);
+  scratch_put(env, &z, 1, 'I', n);
+}
+
+JNIEXPORT jlongArray JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_commAllGather(
+    JNIEnv *env, jclass cls, jlong h, jlong value, jint world) {
+  jlong *buf = (jlong *)malloc(sizeof(jlong) * (size_t)(world > 0 ? world : 1));
+  if (!buf) {
+    throw_class(env, "java/lang/OutOfMemoryError", "cooc_jni: native scratch allocation failed");
+    return NULL;
+  }
+  jlongArray out = NULL;
+  if (!check(env, H(h), cooc_comm_allgather_i64(H(h), value, (int64_t *)buf))) {
+    out = (*env)->NewLongArray(env, world);
+    if (out) (*env)->SetLongArrayRegion(env, out, 0, world, buf);
+  }
+  free(buf);
+  return out;
+}

@@ -93,6 +93,25 @@ final class CoocNative {
    */
   static native long[] countOwned(long handle, long[] userPtr, int[] items);
 
+  /**
+   * cooc_copy_batch_range: the entries of batch rows [rowBegin, rowEnd) -- cols int[n], cnt16 short[n] with n =
+   * rowPtr[rowEnd] - rowPtr[rowBegin] from copyBatch(rowPtr, null, null, rowSums32) -- ascending columns per row.
+   */
+  static native void copyBatchRange(long handle, int rowBegin, int rowEnd, int n, int[] cols, short[] cnt16);
+
+  /**
+   * cooc_topk_owned_host: after countOwned, the owned rows' row sums all-reduced (the broadcast row-sum stream,
+   * FlinkCooccurrences.java:163) and every owned row's LLR top-k on the device; read with copyTopKRange.
+   */
+  static native void topKOwned(long handle, int k, int flags);
+
+  /** cooc_copy_topk_batch_range: rows [rowBegin, rowEnd): sizes int[n], values int[n * k], scores double[n * k]. */
+  static native void copyTopKRange(long handle, int rowBegin, int rowEnd, int k, int[] sizes, int[] values,
+      double[] scores);
+
+  /** cooc_comm_allgather_i64: every subtask's value (collective over the handle's communicator), rank order. */
+  static native long[] commAllGather(long handle, long value, int world);
+
   /** cooc_topk_items: topk(handle, items[], k) of the last batch; sizes int[n], values/scores [n * k]. */
   static native void topKItems(long handle, int k, int flags, int[] items, int[] sizes, int[] values,
       double[] scores);

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 5
+#define COOC_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -189,6 +189,13 @@ COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user
 COOC_API int cooc_copy_batch(cooc_ctx *ctx, int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int16_t *cnt16, int64_t *rowsum,
                     int32_t *rowsum32);
 
+/* The entries of batch rows [row_begin, row_end) only, in cooc_copy_batch's packed order (row_ptr from a
+ * cooc_copy_batch call with cols/cnt/cnt16 NULL): cols/cnt/cnt16 hold at least `cap` entries; a range of more
+ * entries than cap is COOC_ERR_ARG and nothing is written.  A JVM operator streams a result larger than one
+ * Java array (a C3 share: ~7e9 entries; an owner's rows: ~4e9) out in row ranges (ItemRowAggregator.java:50-56's
+ * one map per row).  The packed view is built once per batch. */
+COOC_API int cooc_copy_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int64_t cap, int32_t *cols,
+                                   uint32_t *cnt, int16_t *cnt16);
 /* LLR top-k of every row of the last cooc_count_device / cooc_count_host result: what
  * ItemRowRescorer...java:195-241 emits after that one window from an empty state (rows iterated in
  * ascending column order, LogLikelihood.java:41-57 scores, IntDoublePriorityQueue layout).  flags:
@@ -357,6 +364,18 @@ COOC_API int cooc_count_owned_host(cooc_ctx *ctx, int64_t n_users, const int64_t
  * d_rowsum_global (device int64[n_items], may be NULL) receives the all-reduced row sums. */
 COOC_API int cooc_topk_owned(cooc_ctx *ctx, int32_t topk, int32_t flags, int32_t *d_sizes, int32_t *d_values,
                              double *d_scores, int64_t *d_rowsum_global, void *hip_stream);
+/* cooc_topk_owned into the context's own buffers (a JVM subtask: GpuOwnedCooccurrenceTopKOperator), read back
+ * with cooc_copy_topk_batch / cooc_copy_topk_batch_range / cooc_topk_items: every owned row's heap, scored
+ * against the all-reduced row sums and the job's observed total.  Replaces the rescorer of
+ * FlinkCooccurrences.java:162-167 (ItemRowRescorerTwoInputStreamOperator.java:195-226) for a one-window job. */
+COOC_API int cooc_topk_owned_host(cooc_ctx *ctx, int32_t topk, int32_t flags);
+/* Heaps of rows [row_begin, row_end) of the last cooc_topk_batch / cooc_topk_owned_host: sizes int32[n],
+ * values int32[n*topk], scores double[n*topk] (n = row_end - row_begin, layout as cooc_copy_topk_batch). */
+COOC_API int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *sizes,
+                                        int32_t *values, double *scores);
+/* Every rank's `value` (collective over the communicator): out int64[world] in rank order.  The JVM operators
+ * agree on the window they fire with it (a subtask with no records of its own joins the same window). */
+COOC_API int cooc_comm_allgather_i64(cooc_ctx *ctx, int64_t value, int64_t *out);
 /* The owner map of step (2) on the host (no device): counts int64[n_items] -> owner int32[n_items]. */
 COOC_API int cooc_snake_owner(const int64_t *counts, int32_t n_items, int32_t world, int32_t head, int32_t *owner);
 
