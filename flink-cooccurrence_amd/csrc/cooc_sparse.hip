@@ -114,7 +114,7 @@ constexpr int kSpLds = kTW * 4 + 2 * kL1Words * 4 + kSpDb * 8 + (kSpDb + 4) * 4 
 // compaction), so more independent chunks per CU hide more of them.  The LDS budget (40 KB per workgroup)
 // holds because a count never exceeds its row's pair work W <= 65,535: the dense tile's counters are u16,
 // two per LDS word (a ds_add of 1 << 16 for the odd column never carries), and hash tables have 4K slots
-// (chunks of half the expected keys) over column spans of at most 2^18 (a 256-word block bitmap).
+// (chunks of half the expected keys) over column spans of at most 2^19 (a 512-word block bitmap).
 #ifndef COOC_SP_MID_W
 #define COOC_SP_MID_W 65535
 #endif
@@ -134,9 +134,18 @@ struct SpShape {
   static constexpr int kLds = kRWords * 4 + 2 * L1Words * 4 + Db * 8 + (Db + 4) * 4 + Threads;
 };
 using SpBig = SpShape<kSpThreads, kHashMax, kL1Words, kSpDb, false>;
-using SpMid = SpShape<256, 4096, 256, 256, true>;  // 38.9 KB of LDS with the static part: four per CU
+using SpMid = SpShape<256, 4096, 512, 256, true>;  // 40.9 KB of LDS: three per CU (four at 38.9 KB with 2^18-column spans measured slower: more chunks)
 static_assert(SpBig::kLds == kSpLds, "the big shape is the original kernel");
 constexpr float kHashFillMid = COOC_SP_FILL * SpMid::kHashMax;
+// a tile whose expected distinct keys exceed this is a dense chunk (its own tile of counters, compacted by a
+// linear sweep) rather than part of a hash chunk (A/B knobs; default: the hash chunk's own capacity)
+#ifndef COOC_SP_BIG_DENSE
+#define COOC_SP_BIG_DENSE kHashFill
+#endif
+#ifndef COOC_SP_MID_DENSE
+#define COOC_SP_MID_DENSE kHashFillMid
+#endif
+constexpr float kDenseKeys = COOC_SP_BIG_DENSE, kDenseKeysMid = COOC_SP_MID_DENSE;
 
 // One work item of k_sp_main, everything its start needs in one 64-B record (k_sp_queue).
 struct SpWork {
@@ -707,7 +716,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
       // a mid row (k_sp_main's 256-thread shape): its chunks are planned for 4K-slot tables over <= 2^19 columns
       const bool mid = (tiny_on & 4) && !n_tiny && !n_small && W <= kMidW;
       n_mid = mid ? 1 : 0;
-      const float hfill = mid ? kHashFillMid : kHashFill;
+      const float hfill = mid ? kHashFillMid : kHashFill, dkeys = mid ? kDenseKeysMid : kDenseKeys;
       const int hmax = mid ? SpMid::kHashMax : kHashMax;
       const int hmaxtiles = mid ? SpMid::kHashMaxTiles : kHashMaxTiles;
       bound = uint64_t(min<int64_t>(W - self, M));
@@ -736,7 +745,7 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
           const float d = est_distinct(est, t, W);
           const float e = float(W) * gmass[t];
           e_tot += d;
-          if (d > hfill || e > kDensePairs) {
+          if (d > dkeys || e > kDensePairs) {
             close();
             st |= uint64_t(1) << t;
             dn |= uint64_t(1) << t;

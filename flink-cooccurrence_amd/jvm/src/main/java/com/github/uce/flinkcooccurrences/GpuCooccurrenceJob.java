@@ -84,20 +84,31 @@ final class GpuCooccurrenceJob {
 
   /**
    * p > 1 subtasks, one window (the C3 / C5 configs): the keyBy(item) merge of partial rows replaced by the
-   * library's exchange over RCCL (GpuOwnedCooccurrenceRowsOperator): the communicator id is created here, in
-   * the job's client, and every subtask joins it in open(); each subtask emits the complete rows it owns,
-   * which feed the reference's rescorer with no ItemRowMerge / RowSumMerge windows.
+   * library's exchange over RCCL.  gpuRescore: GpuOwnedCooccurrenceTopKOperator rescores the owned rows on the
+   * device too and emits the rescorer's records itself (C5 never rescores on the JVM); otherwise
+   * GpuOwnedCooccurrenceRowsOperator's complete owned rows feed the reference's rescorer with no ItemRowMerge /
+   * RowSumMerge windows.  Each execution attempt's communicator id is created by subtask 0 in open() and handed
+   * over through rendezvousDir (a directory every subtask of the node can read, OwnedExchange).
    */
   static DataStream<Tuple2<Integer, IntDoublePriorityQueue>> topKOwned(
       DataStream<Tuple3<Integer, Integer, Long>> interactionStream, int windowSize, TimeUnit windowUnit, int nItems,
-      int[] devices, short topK, int parallelism) {
-    final byte[] commId = CoocNative.commUniqueId();
+      int[] devices, short topK, int parallelism, String rendezvousDir, boolean gpuRescore) {
+    if (gpuRescore) {
+      return interactionStream
+          .keyBy(0)
+          .transform(
+              "GpuOwnedCooccurrenceTopK (" + windowSize + " " + windowUnit + ", top " + topK + ", " + parallelism
+                  + " GPUs)",
+              GpuNonSampledCooccurrenceTopKOperator.getOutputType(),
+              new GpuOwnedCooccurrenceTopKOperator(windowSize, windowUnit, nItems, devices, topK, rendezvousDir))
+          .setParallelism(parallelism);
+    }
     final SingleOutputStreamOperator<Void> counter = interactionStream
         .keyBy(0)
         .transform(
             "GpuOwnedCooccurrenceRows (" + windowSize + " " + windowUnit + ", " + parallelism + " GPUs)",
             GpuNonSampledCooccurrenceRowsOperator.getOutputType(),
-            new GpuOwnedCooccurrenceRowsOperator(windowSize, windowUnit, nItems, devices, commId))
+            new GpuOwnedCooccurrenceRowsOperator(windowSize, windowUnit, nItems, devices, rendezvousDir))
         .setParallelism(parallelism);
     return counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROWS_TAG)
         .keyBy(0).connect(counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROW_SUM_TAG).broadcast())

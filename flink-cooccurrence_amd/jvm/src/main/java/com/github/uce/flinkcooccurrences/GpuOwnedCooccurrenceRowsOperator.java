@@ -1,7 +1,6 @@
 package com.github.uce.flinkcooccurrences;
 
 import it.unimi.dsi.fastutil.ints.Int2ShortOpenHashMap;
-import java.util.Arrays;
 import java.util.concurrent.TimeUnit;
 import org.apache.flink.api.common.accumulators.LongCounter;
 import org.apache.flink.api.java.tuple.Tuple2;
@@ -21,14 +20,12 @@ import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
  * owns over every user.  Rows are complete on their owner, so the side outputs ({@link
  * GpuNonSampledCooccurrenceRowsOperator#ROWS_TAG}, {@link GpuNonSampledCooccurrenceRowsOperator#ROW_SUM_TAG})
  * carry final rows and row sums and feed ItemRowRescorerTwoInputStreamOperator with no merge
- * ({@link GpuCooccurrenceJob#topKOwned}).
+ * ({@link GpuCooccurrenceJob#topKOwned}); {@link GpuOwnedCooccurrenceTopKOperator} rescores on the device too.
  *
- * <p>The communicator id is created once in the job's main() ({@link CoocNative#commUniqueId}) and handed to
- * every subtask in the constructor; open() joins it as subtask i of p.  A record whose timestamp falls in
- * another window fails the job (IllegalStateException): multi-window streams keep the partial-row path.
- * The owned rows are copied in one call, so a subtask's owned entries must fit a Java array (2^31 - 1);
- * larger results are read through the Panama path (INTEGRATION.md §4).  Uncompiled here (no JDK); the
- * C-ABI sequence it makes is tests/test_multiproc_gpu.py's "library_host" case.
+ * <p>The communicator rendezvous (an id per execution attempt, created by subtask 0 in open()) and the window
+ * every subtask fires together are {@link OwnedExchange}'s.  The owned rows stream out in row ranges
+ * ({@link CoocBatchReader}: an owner's ~4e9 entries at C3 never need one Java array).  Uncompiled here (no
+ * JDK); tests/test_owned_operator_replay.py replays its C-ABI call sequence on two subtasks against the oracle.
  */
 public class GpuOwnedCooccurrenceRowsOperator
     extends AbstractStreamOperator<Void>
@@ -39,114 +36,69 @@ public class GpuOwnedCooccurrenceRowsOperator
   private final long windowSizeMs;
   private final int nItems;
   private final int[] devices;
-  private final byte[] commId;
+  private final String rendezvousDir;
 
   private transient long handle;
-  private transient int buffered;
-  private transient int[] users;
-  private transient int[] items;
-  private transient long windowStart;
-  private transient boolean fired;
+  private transient OwnedExchange exchange;
+  private transient CoocBatchReader reader;
   private transient LongCounter observedCooccurrences;
   private transient LongCounter rowSumCounter;
 
-  GpuOwnedCooccurrenceRowsOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices, byte[] commId) {
+  GpuOwnedCooccurrenceRowsOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices,
+      String rendezvousDir) {
     this.windowSizeMs = windowUnit.toMillis(windowSize);
     this.nItems = nItems;
     this.devices = devices.clone();
-    this.commId = commId.clone();
+    this.rendezvousDir = rendezvousDir;
   }
 
   @Override
   public void open() throws Exception {
     super.open();
     final int subtask = getRuntimeContext().getIndexOfThisSubtask();
+    final int world = getRuntimeContext().getNumberOfParallelSubtasks();
+    final byte[] commId = OwnedExchange.rendezvous(rendezvousDir,
+        getContainingTask().getEnvironment().getJobID().toString(), getRuntimeContext().getAttemptNumber(), subtask);
     this.handle = CoocNative.create(devices, subtask, nItems, 0, 0, windowSizeMs, (short) 0);
-    CoocNative.commInit(handle, commId, subtask, getRuntimeContext().getNumberOfParallelSubtasks());
-    this.users = new int[1 << 16];
-    this.items = new int[1 << 16];
-    this.windowStart = Long.MIN_VALUE;
+    CoocNative.commInit(handle, commId, subtask, world);
+    this.exchange = new OwnedExchange(handle, windowSizeMs, world);
+    this.reader = new CoocBatchReader();
     this.observedCooccurrences = getRuntimeContext().getLongCounter("UserInteractionCounterObservedCooccurrences");
     this.rowSumCounter = getRuntimeContext().getLongCounter("RowSumProcessWindowRowSum");
   }
 
   @Override
   public void processElement(StreamRecord<Tuple3<Integer, Integer, Long>> element) throws Exception {
-    // TumblingEventTimeWindows' start (offset 0): the one window this operator serves
-    final long ts = element.getTimestamp();
-    final long start = ts - Math.floorMod(ts, windowSizeMs);
-    if (windowStart == Long.MIN_VALUE) {
-      windowStart = start;
-    } else if (start != windowStart || fired) {
-      throw new IllegalStateException("GpuOwnedCooccurrenceRowsOperator serves one window; record at " + ts);
-    }
-    if (buffered == users.length) {
-      users = Arrays.copyOf(users, 2 * buffered);
-      items = Arrays.copyOf(items, 2 * buffered);
-    }
-    users[buffered] = element.getValue().f0;
-    items[buffered] = element.getValue().f1;
-    buffered++;
+    exchange.add(element.getValue().f0, element.getValue().f1, element.getTimestamp());
   }
 
   @Override
   public void processWatermark(Watermark mark) throws Exception {
-    // every subtask reaches the window's end (the final watermark of a bounded source at the latest) and
-    // takes part in the exchange, also one that holds no users
-    final long maxTimestamp = windowStart == Long.MIN_VALUE ? Long.MAX_VALUE - 1 : windowStart + windowSizeMs - 1;
-    if (!fired && mark.getTimestamp() >= maxTimestamp) {
-      fired = true;
-      emitOwnedRows(maxTimestamp);
+    final long ts = exchange.fireAt(mark.getTimestamp());  // (collective over the subtasks)
+    if (ts != Long.MIN_VALUE) {
+      emitOwnedRows(ts);
     }
     super.processWatermark(mark);
   }
 
-  /** CSR of the shard's users (a user's items in arrival order), the exchange, the owned rows out. */
+  /** The exchange, then one Int2ShortOpenHashMap per owned row and its int row sum, ascending items. */
   private void emitOwnedRows(long timestamp) {
-    final int[] order = new int[buffered];
-    final int[] userIds = Arrays.copyOf(users, buffered);
-    final Integer[] idx = new Integer[buffered];
-    for (int i = 0; i < buffered; i++) {
-      idx[i] = i;
-    }
-    Arrays.sort(idx, (x, y) -> userIds[x] != userIds[y] ? Integer.compare(userIds[x], userIds[y]) : Integer.compare(x, y));
-    int nUsers = 0;
-    for (int i = 0; i < buffered; i++) {
-      order[i] = items[idx[i]];
-      if (i == 0 || userIds[idx[i]] != userIds[idx[i - 1]]) {
-        nUsers++;
-      }
-    }
-    final long[] userPtr = new long[nUsers + 1];
-    for (int i = 0, u = 0; i < buffered; i++) {
-      if (i > 0 && userIds[idx[i]] != userIds[idx[i - 1]]) {
-        userPtr[++u] = i;
-      }
-    }
-    userPtr[nUsers] = buffered;
-    final long[] res = CoocNative.countOwned(handle, userPtr, order);  // {nnz, observed, rows, job observed}
-    final long[] rowPtr = new long[nItems + 1];
-    final int[] cols = new int[Math.toIntExact(res[0])];
-    final short[] cnt16 = new short[cols.length];
-    final int[] rowSums32 = new int[nItems];
-    CoocNative.copyBatch(handle, rowPtr, cols, cnt16, rowSums32);
-    for (int a = 0; a < nItems; a++) {
-      final int from = (int) rowPtr[a], to = (int) rowPtr[a + 1];
+    final long[] res = exchange.countOwned();  // {nnz, observed, rows, job observed}
+    reader.forEachRow(handle, nItems, (item, cols, cnt16, from, to, rowSum32) -> {
       if (to > from) {  // ItemRowAggregator.java:50-56: one map per item with a row
         final Int2ShortOpenHashMap row = new Int2ShortOpenHashMap(to - from);
         for (int j = from; j < to; j++) {
           row.put(cols[j], cnt16[j]);
         }
-        output.collect(GpuNonSampledCooccurrenceRowsOperator.ROWS_TAG, new StreamRecord<>(Tuple2.of(a, row), timestamp));
+        output.collect(GpuNonSampledCooccurrenceRowsOperator.ROWS_TAG, new StreamRecord<>(Tuple2.of(item, row), timestamp));
       }
-      if (rowSums32[a] != 0) {  // RowSumAggregator.java:66 (non-owned rows are 0 here)
-        rowSumCounter.add(rowSums32[a]);
+      if (rowSum32 != 0) {  // RowSumAggregator.java:66 (non-owned rows are 0 here)
+        rowSumCounter.add(rowSum32);
         output.collect(GpuNonSampledCooccurrenceRowsOperator.ROW_SUM_TAG,
-            new StreamRecord<>(Tuple2.of(a, rowSums32[a]), timestamp));
+            new StreamRecord<>(Tuple2.of(item, rowSum32), timestamp));
       }
-    }
+    });
     observedCooccurrences.add(res[1]);  // this subtask's owned pairs: the p accumulators sum to the job's
-    buffered = 0;
   }
 
   @Override

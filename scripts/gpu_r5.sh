@@ -84,6 +84,9 @@ for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:14]:
     print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>4s} avg {float(r["AverageNs"])/1e6:8.3f} ms')
 PY
 fi
+if [ "${PMCIC:-0}" = "1" ]; then
+  bash scripts/pmc_icache.sh || exit 1
+fi
 if [ "${PMC:-0}" = "1" ]; then
   bash scripts/pmc_sparse.sh || exit 1
   python3 scripts/pmc_summary.py gpurun_out/pmc_sp gpurun_out/pmc_k_sp_main.json
