@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--permute-items", action="store_true",
                     help="C3/C5: item ids through the fixed bijection datagen.c3_item_perm (ids not in popularity order)")
+    ap.add_argument("--no-permuted", action="store_true",
+                    help="C3 at N=1: skip the line's `permuted` sub-record (the same log with permuted item ids)")
     args = ap.parse_args()
 
     import torch
@@ -265,6 +267,28 @@ def main():
         D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.local_observed), res.n_interactions_all, res.n_users_all
     else:
         D, P_counted, N_seen, U_seen = int(res.owned.nnz), int(res.owned.observed), N, U
+    # the same workload with its item ids permuted (datagen.c3_item_perm: ids carry no popularity order, as real
+    # ids -- MovieLens, hashed -- do not), timed the same way: the id-order independence of the counting path
+    permuted = None
+    if large and world == 1 and args.config == "c3" and not args.permute_items and not args.no_permuted:
+        del up, it
+        up_p, it_p = datagen.c3_users(u0, u1, device=dev, permute=True)
+        core.count_device(up_p, it_p)  # warm-up (allocations)
+        torch.cuda.synchronize()
+        n_p, kms_p = max(3, min(args.steps, 5)), []
+        tp = time.perf_counter()
+        for _ in range(n_p):
+            r_p = core.count_device(up_p, it_p)
+            kms_p.append(core.last_kernel_ms())
+        torch.cuda.synchronize()
+        el_p = time.perf_counter() - tp
+        assert r_p.observed == P_local and int(r_p.nnz) == D, "permuted ids: a different result size"
+        k_p = float(np.median(kms_p))
+        permuted = {"workload": "the same users with item ids through datagen.c3_item_perm (PCG64 seed "
+                                f"{datagen.C3_PERM_SEED:#x})", "steps": n_p, "ms_per_step": el_p / n_p * 1e3,
+                    "value": P_local * n_p / el_p, "kernel_ms": k_p,
+                    "frac": algorithmic_bytes(P_local, N, U, D) / (k_p * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        del up_p, it_p
     stats = torch.tensor([elapsed, float(P_local), float(D)], dtype=torch.float64, device=dev)
     if world > 1:
         t = stats[:1].clone()
@@ -314,6 +338,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            "traffic_kernels": (pmc.get("kernels") or pmc.get("kernel")) if traffic else None,
             "traffic_gbps": (traffic / (k_ms * 1e-3) / 1e9) if traffic else None,
             "hbm_frac_measured": (traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
             "lds_util": pmc.get("lds_util"),
@@ -335,8 +360,12 @@ def main():
                     "profiles/pmc_<kernel>.json) when collected; see DESIGN.md §4",
         },
         "cpu_baseline": None,
+        "permuted": None,
         "checks": {"device_verify": chk, "in_kernel_row_sum_check": "every step (err bit -> exception)"},
     }
+    if permuted is not None:
+        permuted["vs_rank_ordered"] = permuted["ms_per_step"] / ms_per_step
+        out["permuted"] = permuted
     if args.config == "c5":
         out["config"]["topk"] = args.topk
         out["config"]["output"] += f"; top-{args.topk} heaps (sizes, values, scores) per row in HBM"

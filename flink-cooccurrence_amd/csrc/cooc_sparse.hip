@@ -84,7 +84,7 @@ constexpr int kMaxProbe = 64;                          // linear probes before a
 constexpr int kSpU = 4;                                // partner loads in flight per lane
 constexpr int kEstK = 84;                              // estimate table: W_k = 2^(k/2), k < kEstK
 constexpr int kTinyW = 256;                            // rows of at most this many pairs: one wave each (k_sp_tiny)
-constexpr int kSmallW = 4096;                          // ... of at most this many: one 256-thread workgroup each (k_sp_small)
+constexpr int kSmallW = 4096;                          // ... of at most this many: one 512-thread workgroup each (k_sp_small)
 #ifndef COOC_SP_SPLIT_LG
 #define COOC_SP_SPLIT_LG 23
 #endif
@@ -904,7 +904,7 @@ struct SpStatic {
   uint64_t ovf;                     // tiles whose bucket overflowed (their chunks walk the lists)
   unsigned long long rsum;          // the current whole row's compacted counts, summed (row-sum check)
 #ifdef COOC_SP_STATS
-  unsigned long long st[48];
+  unsigned long long st[64];
 #endif
 };
 
@@ -1096,6 +1096,10 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
     };
     uint4 v[kSpU] = {};
     uint32_t m = 0;  // 8 lane bits per group in flight
+#ifdef COOC_SP_STATS
+    const unsigned long long c_issue = STAT_CLOCK();
+    bool first_seen = false;
+#endif
 #pragma unroll
     for (int k = 0; k < kSpU; k++) {
       const uint32_t gk = g + S * k;
@@ -1119,6 +1123,15 @@ __device__ inline uint32_t sp_walk_batch(const SpArgs &A, const SpShared &L, SpS
         // loaded nor applied -- how much of a walk is the group delivery)
         const uint32_t mk = (m >> (8 * k)) & 255u;
         if (mk) sp_apply_group<Sh, kIds>(A, L, S_, op, v[k], mk);
+#ifdef COOC_SP_STATS
+        if (op.mode == 1 && k == 0 && !first_seen) {  // thread 0: the first group's data arrived and was applied
+          first_seen = true;
+          if (threadIdx.x == 0) {
+            S_.st[54] += STAT_CLOCK() - c_issue;
+            S_.st[55] += 1;
+          }
+        }
+#endif
       }
 #pragma unroll
       for (int k = 0; k < kSpU; k++) v[k] = vn[k];
@@ -1232,6 +1245,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
                                         uint64_t &rsum) {
   constexpr int kPer = Sh::kPer, kStep = 64 * kPer, kQ = kPer / 4;  // kQ: 16-B id loads per lane and step
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long c_d0 = STAT_CLOCK();
   uint32_t *row = L.R;
   const int32_t per = ((w + Sh::kWaves - 1) / Sh::kWaves + kStep - 1) & ~(kStep - 1);
   const int32_t lo = min(w, wave * per), hi = min(w, lo + per);
@@ -1260,6 +1274,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (lane == 0) S_.wtot[wave] = cnt;
   __syncthreads();
+  STAT_ADD(48, STAT_CLOCK() - c_d0);
   uint32_t off = 0, tot = 0;
 #pragma unroll
   for (int wv = 0; wv < Sh::kWaves; wv++) {
@@ -1279,6 +1294,7 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
   colq(lo + kPer * lane, q0);
   colq(lo + kStep + kPer * lane, q1);
   const int64_t base = sp_reserve<Sh>(A, S_, tot);  // (barrier: every wave has read wtot)
+  STAT_ADD(49, STAT_CLOCK() - c_d0);
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int32_t b0 = lo; b0 < hi; b0 += kStep) {
     const int32_t b = b0 + kPer * lane;
@@ -1322,7 +1338,9 @@ __device__ inline void sp_dense_compact(const SpArgs &A, const SpShared &L, SpSt
     off += uint32_t(__popcll(m0)) + 2u * uint32_t(__popcll(m1)) + 4u * uint32_t(__popcll(m2)) +
            8u * uint32_t(__popcll(m3));
   }
+  STAT_ADD(50, STAT_CLOCK() - c_d0);
   __syncthreads();
+  STAT_ADD(51, STAT_CLOCK() - c_d0);
 }
 
 // Column-order compaction of the hash table (H slots) of the column range [c0, c1), appended to the
@@ -1368,6 +1386,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     }
   }
   __syncthreads();
+  STAT_ADD(46, STAT_CLOCK() - c_h0);
   uint32_t nblk;
   {
     static_assert(Sh::kL1Words % Sh::kThreads == 0, "L1 words per thread");
@@ -1396,6 +1415,7 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
     atomicOr(&keys[r], 1u << (col & 31u));
   }
   __syncthreads();
+  STAT_ADD(47, STAT_CLOCK() - c_h0);
   const uint32_t pb = (nblk + Sh::kThreads - 1) / Sh::kThreads;
   const uint32_t r0 = min(nblk, uint32_t(tid) * pb), r1 = min(nblk, r0 + pb);
   uint32_t local = 0;
@@ -1503,7 +1523,7 @@ __global__ __launch_bounds__(Sh::kThreads) __attribute__((amdgpu_waves_per_eu(4)
   // (the queue's tail: the mid rows (the mid shape's launch), the small rows (k_sp_small), the tiny ones (k_sp_tiny))
   const int64_t n_work = A.q_end - A.q_begin;
 #ifdef COOC_SP_STATS
-  if (threadIdx.x < 48) S_.st[threadIdx.x] = 0ull;
+  if (threadIdx.x < 64) S_.st[threadIdx.x] = 0ull;
   const unsigned long long t_start = STAT_CLOCK();
 #endif
   if (tid == 0) S_.work = atomicAdd(A.qctr, 1);
@@ -1726,7 +1746,7 @@ __global__ __launch_bounds__(Sh::kThreads) __attribute__((amdgpu_waves_per_eu(4)
 #ifdef COOC_SP_STATS
   if (tid == 0) {
     S_.st[13] = STAT_CLOCK() - t_start;
-    for (int k = 0; k < 48; k++) atomicAdd(A.stats + k, S_.st[k]);
+    for (int k = 0; k < 64; k++) atomicAdd(A.stats + k, S_.st[k]);
   }
 #endif
 }
@@ -3181,8 +3201,8 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #endif
 #ifdef COOC_SP_STATS
     static unsigned long long *d_stats = nullptr;
-    if (!d_stats) (void)hipMalloc(reinterpret_cast<void **>(&d_stats), 96 * 8);
-    (void)hipMemsetAsync(d_stats, 0, 96 * 8, s);
+    if (!d_stats) (void)hipMalloc(reinterpret_cast<void **>(&d_stats), 128 * 8);
+    (void)hipMemsetAsync(d_stats, 0, 128 * 8, s);
     A.stats = d_stats;
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
@@ -3222,7 +3242,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       B.scratch = scr_cap_mid ? sp_scr_mid_.as<uint4>() : nullptr;
       B.scr_cap = (scr_cap_mid && n_gather) ? scr_cap_mid : 0;
 #ifdef COOC_SP_STATS
-      B.stats = A.stats + 48;
+      B.stats = A.stats + 64;
 #endif
       k_sp_main<SpMid><<<unsigned(grid_mid), SpMid::kThreads, SpMid::kLds, s>>>(B);
       COOC_HIP_TRY(hipGetLastError());
@@ -3265,10 +3285,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipGetLastError());
 #ifdef COOC_SP_STATS
     {
-      unsigned long long hh[96];
+      unsigned long long hh[128];
       (void)hipMemcpy(hh, A.stats, sizeof(hh), hipMemcpyDeviceToHost);
       for (int shape = 0; shape < 2; shape++) {
-      const unsigned long long *h = hh + 48 * shape;
+      const unsigned long long *h = hh + 64 * shape;
       const double g = double(shape ? grid_mid : grid);
       if (shape && !n_mid) break;
       fprintf(stderr, "[sp stats] %s shape (%lld WGs):\n", shape ? "mid" : "big", (long long)(shape ? grid_mid : grid));
@@ -3282,6 +3302,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
               "compact rank %.0f reserve %.0f write %.0f | entries %.3g\n", h[16] / 100.0 / g, h[17] / 100.0 / g,
               double(h[18]), h[19], h[20] / 100.0 / g, h[21] / 100.0 / g, h[22] / 100.0 / g, double(h[23]));
       fprintf(stderr, "[sp stats] split flush (staging atomics) per WG (us): %.0f\n", h[26] / 100.0 / g);
+      fprintf(stderr, "[sp stats] hash compaction cumulative (us/WG): table+L1 %.0f, +masks %.0f | dense compaction "
+              "cumulative (us/WG): count %.0f, +reserve %.0f, +writes %.0f, +barrier %.0f | hash walk: first group "
+              "applied after %.2f us (thread 0, %llu walks)\n", h[46] / 100.0 / g, h[47] / 100.0 / g, h[48] / 100.0 / g,
+              h[49] / 100.0 / g, h[50] / 100.0 / g, h[51] / 100.0 / g, h[55] ? h[54] / 100.0 / double(h[55]) : 0.0, h[55]);
       fprintf(stderr, "[sp stats] thread-0 sample: ids inserted %llu, probe rounds %llu (%.2f per group call)\n", h[24], h[25],
               h[24] ? double(h[25]) / double(h[24]) * 4.0 : 0.0);
       for (int c = 0; c < 3; c++) {
