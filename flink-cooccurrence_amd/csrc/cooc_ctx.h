@@ -48,6 +48,11 @@ class StreamState {
   Status pack_delta(cooc_ctx &ctx);
   Status copy_entries(int64_t e0, int64_t e1, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
   Status grow_arena(cooc_ctx &ctx, int64_t need);
+  // p > 1 subtasks (a communicator on the context): the window's partial delta rows routed to their owners
+  // (a mod world) and merged there, the row-sum deltas and the observed pairs all-reduced
+  Status exchange_window(cooc_ctx &ctx, hipStream_t s, const CountResult *r, int64_t obs_local, int64_t *obs_total);
+  Status finish_owned(cooc_ctx &ctx, hipStream_t s, int64_t ts, int64_t obs_local, int64_t obs_total,
+                      cooc_window_info *info);
   // n_items >= 40,320: one window through the large-universe planner, old / new positions in one pass
   Status count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int64_t> &act_off,
                             const std::vector<int32_t> &act_len, const std::vector<int32_t> &act_old,
@@ -90,6 +95,13 @@ class StreamState {
   uint32_t *pk_cnt_ = nullptr;
   std::vector<int32_t> delta_rows_;
   std::vector<int64_t> delta_start_;
+  // p > 1: the last window's owned delta rows (an M-row view over the merge's rows), the all-reduced window row
+  // sums, the exchange buffers, and the packed copy-out of the owned rows
+  bool owned_window_ = false;
+  const int32_t *own_col_ = nullptr;
+  const uint32_t *own_cnt_ = nullptr;
+  DevBuf d_own_base_, d_own_nnz_, d_rs_win_, d_x_nnz_, d_x_ent_, d_r_nnz_, d_r_ent_, d_x_h_, d_zero_;
+  DevBuf d_own_rp_, d_own_pcol_, d_own_pcnt_;
 };
 
 // NonSampledUserInteractionCounterOneInputStreamOperator mirror: late-element drop, tumbling

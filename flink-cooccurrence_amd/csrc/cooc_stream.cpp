@@ -61,7 +61,10 @@ void StreamState::release() {
                    &d_new_items_, &d_new_dst_ptr_, &d_new_dst_,     &d_reloc_,     &d_global_,
                    &d_grs_,       &d_touched_,     &d_scan_tmp_,    &d_scal_,      &d_topk_val_,
                    &d_topk_score_, &d_topk_size_, &d_llr_terms_, &d_lw_items_, &d_lw_up2_,
-                   &d_lw_dsta_,   &d_lw_dstb_,     &d_lw_srcb_,     &d_lw_lenb_};
+                   &d_lw_dsta_,   &d_lw_dstb_,     &d_lw_srcb_,     &d_lw_lenb_,   &d_own_base_,
+                   &d_own_nnz_,   &d_rs_win_,      &d_x_nnz_,       &d_x_ent_,     &d_r_nnz_,
+                   &d_r_ent_,     &d_x_h_,         &d_zero_,        &d_own_rp_,    &d_own_pcol_,
+                   &d_own_pcnt_};
   for (DevBuf *b : all) b->release();
   gs_.release();
   global_ready_ = false;
@@ -198,6 +201,18 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   PhaseTrace tr;
   delta_packed_ = false;  // the packed copy-out view belongs to the previous window
   empty_window_ = n_act == 0;
+  // p > 1 subtasks: every subtask takes part in every window's exchange, also with no user of its own
+  const bool multi = ctx.comm && ctx.comm->world() > 1;
+  owned_window_ = multi;
+  if (multi && ctx.counter.sparse())
+    return Status{COOC_ERR_STATE, "multi-GPU streaming windows need n_items < 40,320 (owners merge dense rows)"};
+  if (multi && empty_window_) {
+    int64_t obs_total = 0;
+    COOC_TRY(exchange_window(ctx, s, nullptr, 0, &obs_total));
+    empty_window_ = false;
+    COOC_TRY(ensure_global(ctx));
+    return finish_owned(ctx, s, ts, 0, obs_total, info);
+  }
   if (empty_window_) {
     // every interaction of the window was cut (user_cut): onEventTime emits nothing, no row is
     // touched and the global state is unchanged
@@ -276,6 +291,12 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
     COOC_TRY(count_large_window(ctx, s, n_act, act_off, act_len, act_old, cbase[n_act], &r));
   tr.mark("count", s);
 
+  if (multi) {  // ---- the owners' rows, then the same merge and rescoring over them
+    int64_t obs_total = 0;
+    COOC_TRY(exchange_window(ctx, s, &r, observed_window, &obs_total));
+    COOC_TRY(ensure_global(ctx));
+    return finish_owned(ctx, s, ts, observed_window, obs_total, info);
+  }
   // ---- global merge + rescoring (ItemRowRescorer...java:144-228)
   COOC_TRY(ensure_global(ctx));
   int64_t *scal = d_scal_.as<int64_t>();
@@ -341,6 +362,135 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   return Status::Ok();
 }
 
+// p > 1: route the window's partial delta rows (r; nullptr: this subtask has no user in the window) to their
+// owners over the communicator -- row a to subtask a mod world, the keyBy(ItemCooccurrences::getItem) of
+// FlinkCooccurrences.java:152 -- and merge them there (Sharder: each owned row summed in a dense LDS row, checked
+// against the all-reduced row sum); the window row sums (the rowSumStream.broadcast() of :163) and the window's
+// ordered pairs all-reduced.  Leaves the owned rows as an M-row view (d_own_base_, d_own_nnz_, own_col_/cnt_)
+// and every item's window row sum in d_rs_win_.
+Status StreamState::exchange_window(cooc_ctx &ctx, hipStream_t s, const CountResult *r, int64_t obs_local,
+                                    int64_t *obs_total) {
+  Comm &c = *ctx.comm;
+  const int32_t M = ctx.cfg.n_items, W = c.world(), part = c.rank();
+  auto rows_owned = [&](int32_t q) { return int64_t(M > q ? (M - q + W - 1) / W : 0); };
+  CountResult zero;
+  if (!r) {  // no user here: zero partial rows
+    COOC_TRY(d_zero_.reserve(sizeof(int64_t) * size_t(M) * 2 + 64));
+    COOC_HIP_TRY(hipMemsetAsync(d_zero_.p, 0, sizeof(int64_t) * size_t(M) * 2 + 64, s));
+    zero.row_base = d_zero_.as<int64_t>();
+    zero.rowsum = d_zero_.as<int64_t>() + M;
+    zero.row_nnz = reinterpret_cast<int32_t *>(d_zero_.as<int64_t>());
+    zero.col = reinterpret_cast<int32_t *>(d_zero_.as<int64_t>());
+    zero.cnt = reinterpret_cast<uint32_t *>(d_zero_.as<int64_t>());
+    r = &zero;
+  }
+  // 1. entries per owner, the owner-major row counts and entries; every subtask's counts all-gathered
+  std::vector<int64_t> h_ent(W), H(size_t(W) * W);
+  COOC_TRY(ctx.sharder.plan(*r, M, W, s, h_ent.data()));
+  int64_t n_send = 0;
+  for (int64_t v : h_ent) n_send += v;
+  COOC_TRY(d_x_nnz_.reserve(sizeof(int32_t) * size_t(M) + 4));
+  COOC_TRY(d_x_ent_.reserve(sizeof(uint64_t) * size_t(n_send + 1)));
+  COOC_TRY(ctx.sharder.pack(*r, M, W, s, d_x_nnz_.as<int32_t>(), n_send ? d_x_ent_.as<uint64_t>() : nullptr));
+  COOC_TRY(d_x_h_.reserve(sizeof(int64_t) * size_t(W) * (W + 1)));
+  int64_t *dh = d_x_h_.as<int64_t>();
+  COOC_HIP_TRY(hipMemcpyAsync(dh, h_ent.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, s));
+  COOC_TRY(c.allgather(dh, dh + W, sizeof(int64_t) * W, s));
+  COOC_HIP_TRY(hipMemcpyAsync(H.data(), dh + W, sizeof(int64_t) * W * W, hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  // 2. row counts and entries to their owners (every peer pair in one exchange)
+  const int64_t R = rows_owned(part);
+  std::vector<int64_t> so(W), sb(W), ro(W), rb(W);
+  int64_t off = 0;
+  for (int32_t q = 0; q < W; q++) {
+    so[q] = off;
+    sb[q] = sizeof(int32_t) * rows_owned(q);
+    off += sb[q];
+    ro[q] = int64_t(sizeof(int32_t)) * q * R;
+    rb[q] = int64_t(sizeof(int32_t)) * R;
+  }
+  COOC_TRY(d_r_nnz_.reserve(sizeof(int32_t) * size_t(W * R) + 4));
+  COOC_TRY(c.alltoallv(d_x_nnz_.p, so.data(), sb.data(), d_r_nnz_.p, ro.data(), rb.data(), s));
+  int64_t n_recv = 0;
+  off = 0;
+  for (int32_t q = 0; q < W; q++) {
+    so[q] = off;
+    sb[q] = int64_t(sizeof(uint64_t)) * h_ent[q];
+    off += sb[q];
+    ro[q] = int64_t(sizeof(uint64_t)) * n_recv;
+    rb[q] = int64_t(sizeof(uint64_t)) * H[size_t(q) * W + part];
+    n_recv += H[size_t(q) * W + part];
+  }
+  COOC_TRY(d_r_ent_.reserve(sizeof(uint64_t) * size_t(n_recv + 1)));
+  COOC_TRY(c.alltoallv(d_x_ent_.p, so.data(), sb.data(), d_r_ent_.p, ro.data(), rb.data(), s));
+  // 3. the window row sums of every item and the window's pairs, all-reduced
+  COOC_TRY(d_rs_win_.reserve(sizeof(int64_t) * (size_t(M) + 1)));
+  int64_t *rs = d_rs_win_.as<int64_t>();
+  COOC_HIP_TRY(hipMemcpyAsync(rs, r->rowsum, sizeof(int64_t) * size_t(M), hipMemcpyDeviceToDevice, s));
+  COOC_HIP_TRY(hipMemcpyAsync(rs + M, &obs_local, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  COOC_TRY(c.allreduce_sum_i64(rs, M + 1, s));
+  COOC_HIP_TRY(hipMemcpyAsync(obs_total, rs + M, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  // 4. the owned rows merged (checked against the all-reduced row sums), as an M-row view
+  MergeResult m;
+  COOC_TRY(ctx.sharder.merge(M, W, part, d_r_nnz_.as<int32_t>(), d_r_ent_.as<uint64_t>(), rs, s, &m));
+  COOC_TRY(d_own_base_.reserve(sizeof(int64_t) * size_t(M)));
+  COOC_TRY(d_own_nnz_.reserve(sizeof(int32_t) * size_t(M)));
+  COOC_TRY(launch_owned_view(s, M, W, part, m.n_rows, m.row_base, m.row_nnz, d_own_base_.as<int64_t>(),
+                             d_own_nnz_.as<int32_t>()));
+  own_col_ = m.col;
+  own_cnt_ = m.cnt;
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  return Status::Ok();
+}
+
+// p > 1: the owned delta rows merged into the resident rows, every item's row sum into the global row sums, the
+// owned touched rows rescored; the window's outputs are this subtask's owned rows (each item on one subtask).
+Status StreamState::finish_owned(cooc_ctx &ctx, hipStream_t s, int64_t ts, int64_t obs_local, int64_t obs_total,
+                                 cooc_window_info *info) {
+  const int32_t M = ctx.cfg.n_items;
+  int64_t *scal = d_scal_.as<int64_t>();
+  COOC_TRY(launch_merge_owned(s, M, d_own_base_.as<int64_t>(), d_own_nnz_.as<int32_t>(), own_col_, own_cnt_,
+                              d_rs_win_.as<int64_t>(), d_global_.as<uint32_t>(), d_grs_.as<int64_t>(), scal, obs_total));
+  COOC_TRY(d_touched_.reserve(sizeof(int32_t) * M));
+  COOC_TRY(launch_touched(s, M, d_own_nnz_.as<int32_t>(), d_touched_.as<int32_t>(), scal, d_scan_tmp_));
+  const int32_t topk = ctx.cfg.topk;
+  if (topk > 0) {
+    COOC_TRY(d_topk_size_.reserve(sizeof(int32_t) * M));
+    COOC_TRY(d_topk_val_.reserve(sizeof(int32_t) * size_t(M) * topk));
+    COOC_TRY(d_topk_score_.reserve(sizeof(double) * size_t(M) * topk));
+    COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
+                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
+                            d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+  }
+  int64_t h_scal[8];
+  COOC_HIP_TRY(hipMemcpyAsync(h_scal, scal, sizeof(h_scal), hipMemcpyDeviceToHost, s));
+  int64_t nnz = 0;
+  COOC_TRY(launch_pack_rows(s, M, d_own_base_.as<int64_t>(), d_own_nnz_.as<int32_t>(), own_col_, own_cnt_, d_own_rp_,
+                            d_own_pcol_, d_own_pcnt_, d_scan_tmp_, &nnz));  // (synchronises s)
+  PlanTotals t;
+  COOC_TRY(ctx.counter.read_totals(&t));
+  if (t.err & 8) return Status{COOC_ERR_STATE, "internal bounds check failed"};
+  if (t.err & 2) return Status{COOC_ERR_OVERFLOW, "a co-occurrence count exceeded uint32"};
+  n_touched_ = int32_t(h_scal[0]);
+  observed_exact += obs_local;  // this subtask's users' pairs (the rescorer's total, observed_ref, is the job's)
+  observed_ref = h_scal[2];
+  rowsum_acc += h_scal[4];      // this subtask's owned row sums: the p accumulators sum to the job's
+  rescored_items += n_touched_;
+  std::memset(&last_, 0, sizeof(last_));
+  last_.ts = ts;
+  last_.nnz = nnz;
+  last_.observed = obs_local;   // this subtask's users' pairs: the p accumulators sum to the job's
+  last_.n_rows = n_touched_;
+  last_.topk = topk;
+  last_.n_topk = topk > 0 ? n_touched_ : 0;
+  *info = last_;
+  have_window_ = true;
+  staged_ = false;
+  n_staged_ = 0;
+  window_seq_++;
+  return Status::Ok();
+}
+
 Status StreamState::count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_act, const std::vector<int64_t> &act_off,
                                       const std::vector<int32_t> &act_len, const std::vector<int32_t> &act_old,
                                       int64_t n_full, CountResult *r) {
@@ -399,7 +549,13 @@ Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, i
 Status StreamState::pack_delta(cooc_ctx &ctx) {
   if (delta_packed_) return Status::Ok();
   const int32_t M = ctx.cfg.n_items;
-  COOC_TRY(ctx.counter.pack(ctx.stream, &pk_rp_, &pk_col_, &pk_cnt_));
+  if (owned_window_) {  // (packed by finish_owned)
+    pk_rp_ = d_own_rp_.as<int64_t>();
+    pk_col_ = d_own_pcol_.as<int32_t>();
+    pk_cnt_ = d_own_pcnt_.as<uint32_t>();
+  } else {
+    COOC_TRY(ctx.counter.pack(ctx.stream, &pk_rp_, &pk_col_, &pk_cnt_));
+  }
   COOC_HIP_TRY(hipStreamSynchronize(ctx.stream));
   std::vector<int64_t> rp(M + 1);
   COOC_HIP_TRY(hipMemcpy(rp.data(), pk_rp_, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
@@ -457,8 +613,11 @@ Status StreamState::copy_rowsums(cooc_ctx &ctx, int32_t *items, int64_t *delta, 
   const int32_t M = ctx.cfg.n_items;
   std::vector<int32_t> nnz(M);
   std::vector<int64_t> rs(M);
-  COOC_HIP_TRY(hipMemcpy(nnz.data(), ctx.counter.last_row_nnz(), sizeof(int32_t) * M, hipMemcpyDeviceToHost));
-  COOC_HIP_TRY(hipMemcpy(rs.data(), ctx.counter.last_rowsum(), sizeof(int64_t) * M, hipMemcpyDeviceToHost));
+  // (p > 1: the owned rows with a delta and their all-reduced row sums: each item on its owner only)
+  COOC_HIP_TRY(hipMemcpy(nnz.data(), owned_window_ ? d_own_nnz_.as<int32_t>() : ctx.counter.last_row_nnz(),
+                         sizeof(int32_t) * M, hipMemcpyDeviceToHost));
+  COOC_HIP_TRY(hipMemcpy(rs.data(), owned_window_ ? d_rs_win_.as<int64_t>() : ctx.counter.last_rowsum(),
+                         sizeof(int64_t) * M, hipMemcpyDeviceToHost));
   int32_t k = 0;
   for (int32_t a = 0; a < M; a++) {
     if (nnz[a] == 0) continue;
@@ -573,6 +732,20 @@ Status Operator::process_watermark(cooc_ctx &ctx, int64_t wm, int32_t *fired, co
   if (wm > watermark) watermark = wm;
   *fired = 0;
   auto it = pending_.begin();
+  if (ctx.comm && ctx.comm->world() > 1) {
+    // p > 1 subtasks see the same watermarks; they fire the earliest window due on ANY of them, together (a
+    // subtask with no record in it joins the window's exchange with no user)
+    const int64_t mine = (it != pending_.end() && it->first <= watermark) ? it->first : INT64_MAX;
+    std::vector<int64_t> all(size_t(ctx.comm->world()));
+    COOC_TRY(ctx.comm_allgather_i64(mine, all.data()));
+    const int64_t due = *std::min_element(all.begin(), all.end());
+    if (due == INT64_MAX) return Status::Ok();
+    if (mine != due) {
+      COOC_TRY(ctx.stream_state.finish(ctx, due, info));
+      *fired = 1;
+      return Status::Ok();
+    }
+  }
   if (it == pending_.end() || it->first > watermark) return Status::Ok();
   // onEventTime for every user of the window: group the buffered interactions by user, keeping
   // each user's arrival order (windowState list order, :118).

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *
       uint32_t *g = G + a * int64_t(M);
       for (int32_t i = lane; i < n; i += 64) g[col[b + i]] += cnt[b + i];  // unique (a, col) per window
     }
-    if (lane == 0) {
+    if (lane == 0 && rowsum_delta) {
       const int64_t d = rowsum_delta[a];
       grs[a] += d;
       d32 += int64_t(int32_t(uint32_t(uint64_t(d))));  // RowSumAggregator's int value, ItemRowRescorer...java:154
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *
   }
   if (lane == 0) s_d32[threadIdx.x >> 6] = d32;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && scal) {
     const int64_t t = s_d32[0] + s_d32[1] + s_d32[2] + s_d32[3];
     if (t) atomicAdd(reinterpret_cast<unsigned long long *>(scal + 1), (unsigned long long)t);
   }
@@ -109,6 +109,66 @@ __global__ __launch_bounds__(256) void k_merge_global(int32_t M, const int64_t *
 __global__ void k_finish_scalars(int64_t *__restrict__ scal, int64_t observed_window) {
   scal[2] += scal[1];
   scal[3] += observed_window;
+}
+
+// ---- multi-GPU windows (p > 1 subtasks, the keyBy(item) of FlinkCooccurrences.java:152): after the owner
+// merged its rows' partial deltas (Sharder::merge: rows a = part + r W), the M-row view of them, their merge
+// into the resident rows, every item's all-reduced row-sum delta, and the packed copy-out.
+__global__ void k_own_scatter(int32_t R, int32_t W, int32_t part, const int64_t *__restrict__ mbase,
+                              const int32_t *__restrict__ mnnz, int64_t *__restrict__ base, int32_t *__restrict__ nnz) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int64_t a = int64_t(part) + int64_t(r) * W;
+  base[a] = mbase[r];
+  nnz[a] = mnnz[r];
+}
+
+// every item's window row sum (all-reduced: the broadcast row-sum stream, :163) into the global row sums; scal[1]
+// = the sum of their int views over ALL items (the rescorer's observed, :154), scal[4] = over the OWNED rows with
+// a delta only (this subtask's RowSumProcessWindowRowSum accumulator, RowSumAggregator.java:50,67)
+__global__ __launch_bounds__(256) void k_add_rowsums(int32_t M, const int64_t *__restrict__ rs, const int32_t *__restrict__ nnz,
+                                                     int64_t *__restrict__ grs, int64_t *__restrict__ scal) {
+  __shared__ int64_t s_all[4], s_own[4];
+  int64_t all = 0, own = 0;
+  for (int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; a < M; a += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t d = rs[a];
+    if (d == 0) continue;
+    grs[a] += d;
+    const int64_t d32 = int64_t(int32_t(uint32_t(uint64_t(d))));
+    all += d32;
+    if (nnz[a] > 0) own += d32;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    all += __shfl_xor(all, o, 64);
+    own += __shfl_xor(own, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_all[threadIdx.x >> 6] = all;
+    s_own[threadIdx.x >> 6] = own;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t t = s_all[0] + s_all[1] + s_all[2] + s_all[3], u = s_own[0] + s_own[1] + s_own[2] + s_own[3];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long *>(scal + 1), (unsigned long long)t);
+    if (u) atomicAdd(reinterpret_cast<unsigned long long *>(scal + 4), (unsigned long long)u);
+  }
+}
+
+// one wave per row: the row's entries copied to its packed offset rp[a]
+__global__ __launch_bounds__(256) void k_pack_rows(int32_t M, const int64_t *__restrict__ base, const int32_t *__restrict__ nnz,
+                                                   const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+                                                   const uint32_t *__restrict__ cnt, int32_t *__restrict__ out_col,
+                                                   uint32_t *__restrict__ out_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t a = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; a < M; a += n_waves) {
+    const int32_t n = nnz[a];
+    const int64_t b = base[a], o = rp[a];
+    for (int32_t i = lane; i < n; i += 64) {
+      out_col[o + i] = col[b + i];
+      out_cnt[o + i] = cnt[b + i];
+    }
+  }
 }
 
 struct IsTouched {
@@ -598,6 +658,50 @@ Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, co
   k_merge_global<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
       M, row_base, row_nnz, col, cnt, rowsum_delta, G, grs, scal);
   k_finish_scalars<<<1, 1, 0, s>>>(scal, observed_window);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_owned_view(hipStream_t s, int32_t M, int32_t W, int32_t part, int32_t R, const int64_t *mbase,
+                         const int32_t *mnnz, int64_t *base, int32_t *nnz) {
+  COOC_HIP_TRY(hipMemsetAsync(base, 0, sizeof(int64_t) * size_t(M), s));
+  COOC_HIP_TRY(hipMemsetAsync(nnz, 0, sizeof(int32_t) * size_t(M), s));
+  if (R > 0) k_own_scatter<<<blocks_for(R, 256), 256, 0, s>>>(R, W, part, mbase, mnnz, base, nnz);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_merge_owned(hipStream_t s, int32_t M, const int64_t *base, const int32_t *nnz, const int32_t *col,
+                          const uint32_t *cnt, const int64_t *rs_all, uint32_t *G, int64_t *grs, int64_t *scal,
+                          int64_t observed_window) {
+  COOC_HIP_TRY(hipMemsetAsync(scal + 1, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipMemsetAsync(scal + 4, 0, sizeof(int64_t), s));
+  // the owned rows' entries into the dense global rows (k_merge_global with no row sums: zero deltas)
+  k_merge_global<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
+      M, base, nnz, col, cnt, nullptr, G, nullptr, nullptr);
+  k_add_rowsums<<<std::min<unsigned>(blocks_for(M, 256), 1024), 256, 0, s>>>(M, rs_all, nnz, grs, scal);
+  k_finish_scalars<<<1, 1, 0, s>>>(scal, observed_window);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
+Status launch_pack_rows(hipStream_t s, int32_t M, const int64_t *base, const int32_t *nnz, const int32_t *col,
+                        const uint32_t *cnt, DevBuf &rp, DevBuf &out_col, DevBuf &out_cnt, DevBuf &tmp, int64_t *total) {
+  COOC_TRY(rp.reserve(sizeof(int64_t) * (size_t(M) + 1)));
+  int64_t *d_rp = rp.as<int64_t>();
+  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> n64(nnz, WidenI64{});
+  size_t b = 0;
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, n64, d_rp + 1, M, s));
+  COOC_TRY(tmp.reserve(b));
+  b = tmp.cap;
+  COOC_HIP_TRY(hipMemsetAsync(d_rp, 0, sizeof(int64_t), s));
+  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, n64, d_rp + 1, M, s));
+  COOC_HIP_TRY(hipMemcpyAsync(total, d_rp + M, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  COOC_HIP_TRY(hipStreamSynchronize(s));
+  COOC_TRY(out_col.reserve(sizeof(int32_t) * size_t(*total + 1)));
+  COOC_TRY(out_cnt.reserve(sizeof(uint32_t) * size_t(*total + 1)));
+  k_pack_rows<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
+      M, base, nnz, d_rp, col, cnt, out_col.as<int32_t>(), out_cnt.as<uint32_t>());
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }

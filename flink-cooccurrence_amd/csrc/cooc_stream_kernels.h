@@ -18,6 +18,17 @@ Status launch_append(hipStream_t s, int64_t n, const int64_t *new_ptr, const int
 Status launch_merge_global(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                            const int32_t *col, const uint32_t *cnt, const int64_t *rowsum_delta, uint32_t *G,
                            int64_t *grs, int64_t *scal, int64_t observed_window);
+// p > 1 windows: the owner's merged rows (R rows a = part + r W) as an M-row view (base, nnz: zero elsewhere);
+// their entries merged into the dense global rows G and every item's all-reduced row-sum delta rs_all into grs
+// (scal[1]: sum of the int views over all items, scal[4]: over the owned rows with a delta); the view packed for
+// copy-out (rp int64[M+1], *total entries; synchronises s).
+Status launch_owned_view(hipStream_t s, int32_t M, int32_t W, int32_t part, int32_t R, const int64_t *mbase,
+                         const int32_t *mnnz, int64_t *base, int32_t *nnz);
+Status launch_merge_owned(hipStream_t s, int32_t M, const int64_t *base, const int32_t *nnz, const int32_t *col,
+                          const uint32_t *cnt, const int64_t *rs_all, uint32_t *G, int64_t *grs, int64_t *scal,
+                          int64_t observed_window);
+Status launch_pack_rows(hipStream_t s, int32_t M, const int64_t *base, const int32_t *nnz, const int32_t *col,
+                        const uint32_t *cnt, DevBuf &rp, DevBuf &out_col, DevBuf &out_cnt, DevBuf &tmp, int64_t *total);
 // kMax cap of a device CSR: cut_ptr int64[n_users+1], cut_items int32[<= n]; *n_cut = cut_ptr[n_users]
 // (read back: the caller sizes the next pass with it).
 Status launch_user_cut(hipStream_t s, int64_t n_users, const int64_t *up, const int32_t *items, int32_t cut,
