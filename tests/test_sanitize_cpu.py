@@ -21,8 +21,9 @@ def test_host_parsers_under_asan_ubsan(tmp_path):
            "-fno-sanitize-recover=all", "-Wall", "-o", exe, os.path.join(ROOT, "tests", "sanitize", "host_fuzz.cpp"),
            os.path.join(CSRC, "cooc_codec.cpp"), os.path.join(CSRC, "cooc_ingest.cpp")]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
-    env.pop("LD_PRELOAD", None)  # (the sanitizer runtime must come first)
+    # (verify_asan_link_order=0: the environment may preload a library ahead of the sanitizer runtime)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "host_fuzz ok" in r.stdout
