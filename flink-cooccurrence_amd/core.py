@@ -98,8 +98,9 @@ class CooccurrenceCore:
         whole row through the sort + segmented-reduce path: packed 64-bit pair keys, radix sort, runs).
         user_cut: kMax, 0 = off; else only the first user_cut interactions of every user are expanded
         (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped).
-        column_order: COOC_FLAG_COLUMN_ORDER (device rows of the large-universe path in column-id order instead
-        of descending batch frequency)."""
+        column_order: COOC_FLAG_COLUMN_ORDER (device rows of the large-universe path in id order instead of the
+        renumbered order: the batch's 16,384 most frequent items first, in id order, then the rest in id order;
+        the renumbering is skipped when 15/16 of those hot items already have ids below 16,384)."""
         L = _lib.load()
         flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
         if output not in ("auto", "csr", "dense"):

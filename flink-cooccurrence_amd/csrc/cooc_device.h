@@ -247,8 +247,9 @@ class Counter {
   int64_t last_deferred_ = 0, last_deferred_pairs_ = 0;
   int32_t last_hot_overlap_ = -1;  // hot items with an id below kTW at the last relabel decision (-1: none)
   bool sort_rows_ = false;  // COOC_FLAG_SORT_ROWS
-  // batch windows of the large-universe path: columns relabelled by descending frequency (off: column ids,
-  // COOC_FLAG_COLUMN_ORDER); the last run's maps (NULL without a relabel)
+  // batch windows of the large-universe path: the kTW most frequent items renumbered into tile 0 (ascending
+  // ids), the others at id + kTW; skipped when 15/16 of them have ids < kTW (off: COOC_FLAG_COLUMN_ORDER); the
+  // last run's maps (NULL without a relabel)
   bool relabel_ = true;
   DevBuf sp_rank_, sp_rkeys_, sp_bits_;  // (sp_bits_: the hot-column and owned-row bitmaps of the user passes)
   const int32_t *last_hot_col_ = nullptr, *last_pos_of_ = nullptr;

@@ -84,12 +84,15 @@ enum cooc_status {
  * takes the rows whose LDS hash table overflows; the flag sends all of them (A/B and tests). */
 #define COOC_FLAG_SORT_ROWS 16
 /* Large universes, batch windows: keep the columns of a row in ascending id order.  By default the
- * large-universe path numbers the columns of a batch by descending frequency (that batch's item counts, or
- * the global counts of cooc_count_device_owned; ties: the smaller id first) so that its tiling works
- * whatever order the ids come in, and a device result's rows are in THAT order -- which is also the order
- * the rescorer scores them in (the top-k tie order).  The host copies (cooc_copy_batch) are always in
- * ascending column order.  This flag restores id order on the device at the price of the relabel's gain
- * (ids not numbered by popularity run up to ~1.8x slower). */
+ * large-universe path renumbers the columns of a batch so that its first 16,384-column tile holds the
+ * batch's 16,384 most frequent items (that batch's item counts, or the global counts of
+ * cooc_count_device_owned): column c < 16,384 is the c-th of those hot items in ASCENDING id order, and
+ * every other item b is column b + 16,384 (the hot items leave holes there).  The renumbering is skipped
+ * -- identity order -- when at least 15/16 of the hot items already have ids below 16,384 (ids numbered by
+ * popularity), and for universes of one tile.  A device result's rows are in this column order, which is
+ * also the order the rescorer scores them in (the top-k tie order); cooc_copy_column_order reports it.
+ * The host copies (cooc_copy_batch) are always in ascending id order.  This flag keeps id order on the
+ * device at the price of the renumbering's gain (ids not numbered by popularity run up to ~1.8x slower). */
 #define COOC_FLAG_COLUMN_ORDER 32
 
 typedef struct cooc_ctx cooc_ctx;
@@ -132,9 +135,10 @@ typedef struct cooc_device_result {
   int64_t observed;       /* exact ordered pairs sum_u n_u (n_u - 1) */
   const int64_t *row_base;  /* [n_items]: first entry of row a in col/cnt (rows padded, not packed) */
   const int32_t *row_nnz;   /* [n_items]: entries of row a (both layouts) */
-  const int32_t *col;       /* ascending within a row in the result's column order: column id, or, for a
-                               large-universe batch (n_items >= 40,320 without COOC_FLAG_COLUMN_ORDER),
-                               descending batch frequency of the column (ties: smaller id first) */
+  const int32_t *col;       /* item ids, ascending within a row in the result's column order: the id itself,
+                               or, for a renumbered large-universe batch (n_items >= 40,320 without
+                               COOC_FLAG_COLUMN_ORDER), the hot items first in id order, then the others in
+                               id order (see COOC_FLAG_COLUMN_ORDER, cooc_copy_column_order) */
   const uint32_t *cnt;      /* exact counts */
   const int64_t *rowsum;    /* [n_items]: exact row sums sum_b C[a,b] */
   const uint32_t *dense;    /* [n_items * n_items] row-major exact counts, 0 = key absent */
@@ -178,8 +182,9 @@ COOC_API int cooc_count_device_owned(cooc_ctx *ctx, int64_t n_users, const int64
 COOC_API int cooc_item_counts(cooc_ctx *ctx, const int32_t *d_items, int64_t n_interactions, int64_t *d_counts,
                               void *hip_stream);
 /* The column order of the last batch result's device rows (and of its top-k iteration, the tie order):
- * rank_of int32[n_items] gets the position of every column in that order -- its rank by descending batch
- * frequency after the large-universe relabel, else the column id itself (see COOC_FLAG_COLUMN_ORDER). */
+ * rank_of int32[n_items] gets the position of every item in that order -- after a large-universe
+ * renumbering, c for the c-th hot item (ascending ids) and id + 16,384 for every other item; else the id
+ * itself (see COOC_FLAG_COLUMN_ORDER for when the renumbering happens).  Only the relative order counts. */
 COOC_API int cooc_copy_column_order(cooc_ctx *ctx, int32_t *rank_of);
 /* Same from host buffers; afterwards cooc_copy_batch copies the packed CSR out. */
 COOC_API int cooc_count_host(cooc_ctx *ctx, int64_t n_users, const int64_t *user_ptr, const int32_t *items,
@@ -233,7 +238,17 @@ COOC_API int cooc_topk_items(cooc_ctx *ctx, int32_t k, int32_t flags, int32_t n,
  * new items in arrival order (user_ptr int64[n_users+1] into items).  Several submits to the same
  * window append.  cooc_finish_window expands every staged user against its resident history,
  * reduces the window's delta rows and row sums, merges them into the global state and, if
- * topk > 0, rescores every touched row (ItemRowRescorer...java:144-228). */
+ * topk > 0, rescores every touched row (ItemRowRescorer...java:144-228).
+ * Across GPUs (a communicator of world > 1 on ctx, cooc_comm_init / cooc_comm_init_ops; item universes below
+ * 40,320): each context holds the resident histories of ITS users (a keyBy(user) shard,
+ * FlinkCooccurrences.java:70) and cooc_finish_window is collective: every rank expands its own users, the
+ * partial delta rows go to their owners (row a on rank a mod world: the keyBy(item) of :152), the row-sum
+ * deltas and the window's pairs are all-reduced (the broadcast of :163), and each owner merges its rows into
+ * its resident global rows and rescores them against the job's row sums.  The window's outputs on a rank
+ * are its owned rows (every row of the job on exactly one rank); info->observed is this rank's users' pairs
+ * (the ObservedCooccurrences accumulator; the ranks' values add up to the job's).  Every rank finishes the
+ * same windows in the same order: cooc_op_process_watermark fires the earliest window due on ANY rank
+ * (agreed by an all-gather), so a rank without records in it still joins. */
 COOC_API int cooc_submit_batch(cooc_ctx *ctx, int64_t window_ts, int32_t n_users, const int32_t *user_ids,
                       const int64_t *user_ptr, const int32_t *items);
 COOC_API int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_info *info);

@@ -43,8 +43,8 @@ class _Rows:
         self.rowsum = _d2h(res.rowsum, M, np.int64)
 
     def row(self, a):
-        """Row a in ascending column order (the device row's own order -- descending batch frequency after
-        the large-universe relabel -- is checked by cooc_verify_batch)."""
+        """Row a in ascending id order (the device row's own order -- hot items first after the
+        large-universe renumbering, cooc.h COOC_FLAG_COLUMN_ORDER -- is checked by cooc_verify_batch)."""
         n, b = int(self.nnz[a]), int(self.base[a])
         c, v = _d2h(self.res.col, n, np.int32, b), _d2h(self.res.cnt, n, np.uint32, b).astype(np.int64)
         o = np.argsort(c, kind="stable")
@@ -264,7 +264,7 @@ def test_c5_topk_c3_shape_vs_oracle(pkg, oracle, torch_cuda):
         sizes, vals, scores = core.topk_items(sample, k)
         empty = np.setdiff1d(np.arange(0, M, 9973), rows)[:5]
         esz, _, _ = core.topk_items(empty, k)
-        order = core.column_order()  # the device rows' column order (descending frequency): the tie order
+        order = core.column_order()  # the device rows' column order (hot items first): the tie order
     assert np.all(esz == 0)
     for i, a in enumerate(sample.tolist()):
         s, e = got.row_ptr[a], got.row_ptr[a + 1]
