@@ -1119,6 +1119,14 @@ void Counter::release() {
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
+  for (int i = 0; i < 2; i++) {
+    if (aux_[i]) (void)hipStreamDestroy(aux_[i]);
+    if (ev_join_[i]) (void)hipEventDestroy(ev_join_[i]);
+    aux_[i] = nullptr;
+    ev_join_[i] = nullptr;
+  }
+  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+  ev_fork_ = nullptr;
 }
 
 Status Counter::read_totals(PlanTotals *t) {

@@ -258,6 +258,12 @@ class Counter {
   bool srb_hipcub_ = getenv("COOC_SR_HIPCUB") && getenv("COOC_SR_HIPCUB")[0] == '1';
   bool small_off_ = getenv("COOC_SP_SMALL") && getenv("COOC_SP_SMALL")[0] == '0';  // (A/B: small rows in k_sp_main)
   bool mid_off_ = getenv("COOC_SP_MID") && getenv("COOC_SP_MID")[0] == '0';  // (A/B: mid rows in the big shape)
+  // the mid-row and small-row launches on streams of their own, forked from and joined back to the caller's
+  // stream, so that their workgroups fill the CUs the big launch's last workgroups leave idle (COOC_SP_FORK=0:
+  // one after the other on the caller's stream)
+  int fork_mode_ = getenv("COOC_SP_FORK") ? atoi(getenv("COOC_SP_FORK")) : 0;  // (A/B: 1 fork at the start, 2 small rows beside the mid launch)
+  hipStream_t aux_[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork_ = nullptr, ev_join_[2] = {nullptr, nullptr};
   DevBuf sp_scr_mid_;      // the mid launch's gather scratch
   int64_t last_mid_grid_ = 0;
   Status run_deferred(int64_t n_def, int32_t T, const int64_t *row_ptr, const int64_t *epre, const uint32_t *vals,

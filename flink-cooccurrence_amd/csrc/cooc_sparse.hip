@@ -3207,6 +3207,22 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     A.exp = getenv("COOC_SP_EXP") ? atoi(getenv("COOC_SP_EXP")) : 0;
 #endif
     if (timer && timer->enabled) COOC_HIP_TRY(hipEventRecord(timer->acc_begin, s));
+    // the mid and small/tiny launches fork onto streams of their own (after everything before on s) and join
+    // s again before the span ends; the big launch is issued first, so its workgroups take the CUs first
+    const bool fork = fork_mode_ != 0 && (n_mid > 0 || n_small > 0 || n_tiny > 0);
+    hipStream_t s_mid = s, s_small = s;
+    if (fork) {
+      if (!ev_fork_) {
+        COOC_HIP_TRY(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+        for (int i = 0; i < 2; i++) {
+          COOC_HIP_TRY(hipStreamCreateWithFlags(&aux_[i], hipStreamNonBlocking));
+          COOC_HIP_TRY(hipEventCreateWithFlags(&ev_join_[i], hipEventDisableTiming));
+        }
+      }
+      COOC_HIP_TRY(hipEventRecord(ev_fork_, s));
+      s_mid = fork_mode_ == 2 ? s : aux_[0];
+      s_small = aux_[1];
+    }
     A.q_begin = 0;
     A.q_end = n_big;
     if (n_big > 0) {
@@ -3244,15 +3260,18 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
 #ifdef COOC_SP_STATS
       B.stats = A.stats + 64;
 #endif
-      k_sp_main<SpMid><<<unsigned(grid_mid), SpMid::kThreads, SpMid::kLds, s>>>(B);
+      if (fork && fork_mode_ == 2) COOC_HIP_TRY(hipEventRecord(ev_fork_, s));  // (after the big launch)
+      if (fork && s_mid != s) COOC_HIP_TRY(hipStreamWaitEvent(s_mid, ev_fork_, 0));
+      k_sp_main<SpMid><<<unsigned(grid_mid), SpMid::kThreads, SpMid::kLds, s_mid>>>(B);
       COOC_HIP_TRY(hipGetLastError());
     }
+    if (fork && (n_small > 0 || n_tiny > 0)) COOC_HIP_TRY(hipStreamWaitEvent(s_small, ev_fork_, 0));
     if (n_small > 0) {
-      k_sp_small<<<unsigned(grid_small), kSmallThreads, 0, s>>>(A);
+      k_sp_small<<<unsigned(grid_small), kSmallThreads, 0, s_small>>>(A);
       COOC_HIP_TRY(hipGetLastError());
     }
     if (n_tiny > 0) {
-      k_sp_tiny<<<unsigned(grid_tiny), kTinyThreads, 0, s>>>(A);
+      k_sp_tiny<<<unsigned(grid_tiny), kTinyThreads, 0, s_small>>>(A);
       COOC_HIP_TRY(hipGetLastError());
     }
   SPT("main");
@@ -3262,6 +3281,12 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
           cnt_.as<uint32_t>(), bump_.as<unsigned long long>(), cap, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(),
           tot, spre, hot_col, pos_of);
       COOC_HIP_TRY(hipGetLastError());
+    }
+    if (fork) {  // s waits for the forked launches
+      COOC_HIP_TRY(hipEventRecord(ev_join_[0], s_mid));
+      COOC_HIP_TRY(hipEventRecord(ev_join_[1], s_small));
+      COOC_HIP_TRY(hipStreamWaitEvent(s, ev_join_[0], 0));
+      COOC_HIP_TRY(hipStreamWaitEvent(s, ev_join_[1], 0));
     }
     // (the timed span: every counting kernel of the run -- k_sp_main, k_sp_small, k_sp_tiny, the split rows'
     // finalize -- so that moving rows between them cannot flatter the kernel time)

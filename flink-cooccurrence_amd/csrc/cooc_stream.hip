@@ -314,10 +314,15 @@ struct RowTerms {
 // others (hot pairs, wrapped or zero int16 views) are queued in LDS and scored 64 at a time with the
 // full formula (5 logs; the two terms that depend on k11 alone come from k_k11_terms' tables).  Both
 // are LogLikelihood.java:41-57 in Java's operation order, bit for bit.
+// The full formula's xlogx(k12) = xlogx(rs_a - k11) and xlogx(k21 + k22) = xlogx(observed + 2 k11 - rs_a) depend
+// on the row and k11 only: the row's LDS tables over k11 < kRsK (tr12, tr2122) hold them, and xlogx(k21) of a
+// column with |rs_b - k11| < 32768 is a k11t entry -- the same function of the same integer, so the same bits.
+constexpr int kRsK = 64;
 template <class Rows>
 __device__ inline void rs_score_chunk(const Rows &src, int64_t rb, int64_t i0, int64_t n, const RowTerms &R,
                                       int32_t exact, const ColTerms *__restrict__ cterm,
-                                      const double *__restrict__ k11t, double *rscore, int32_t *rcol, int32_t *rq) {
+                                      const double *__restrict__ k11t, const double *tr12, const double *tr2122,
+                                      double *rscore, int32_t *rcol, int32_t *rq) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint32_t npend = 0;
@@ -373,11 +378,13 @@ __device__ inline void rs_score_chunk(const Rows &src, int64_t rb, int64_t i0, i
     const int64_t k22 = R.observed + k11 - k12 - k21;
     // xlogx(k11) and xlogx(k11 + k12 + k21 + k22) = xlogx(observed + 2 k11) depend on k11 only: tables
     // over the int16 range (the same function, so the same bits)
-    const bool in = k11 >= -32768 && k11 < 32768;
+    const bool in = k11 >= -32768 && k11 < 32768, inK = k11 >= 0 && k11 < kRsK;
     const double x_all = in ? k11t[k11 + 32768 + 65536] : xlogx(k11 + k12 + (k21 + k22));
     const double x_11 = in ? k11t[k11 + 32768] : xlogx(k11);
-    rscore[idx] = llr_terms(x_all, R.x_a, xlogx(k21 + k22), h.x_rs, xlogx(k12 + k22), x_11, xlogx(k12), xlogx(k21),
-                            xlogx(k22));
+    const double x_12 = inK ? tr12[k11] : xlogx(k12);
+    const double x_2122 = inK ? tr2122[k11] : xlogx(k21 + k22);
+    const double x_21 = (k21 >= -32768 && k21 < 32768) ? k11t[k21 + 32768] : xlogx(k21);
+    rscore[idx] = llr_terms(x_all, R.x_a, x_2122, h.x_rs, xlogx(k12 + k22), x_11, x_12, x_21, xlogx(k22));
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -408,6 +415,8 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
   double *rscore = ring + int64_t(wave) * kRsChunk * 2;
   int32_t *rcol = reinterpret_cast<int32_t *>(rscore + kRsChunk);
   int32_t *rq = rcol + kRsChunk;
+  double *tr12 = ring + int64_t(waves) * kRsChunk * 2 + int64_t(wave) * 2 * kRsK;
+  double *tr2122 = tr12 + kRsK;
   const int64_t n_rows = n_rows_p[0];
   const int64_t observed = exact ? obs[1] : obs[0];
   for (int64_t t = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 1ull)) : 0ll, 0, 64); t < n_rows;
@@ -418,8 +427,14 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
     int32_t size = 0;
     double least = 0.0;
     const int64_t rb = n > 0 ? src.base(a) : 0;
+    if (lane < kRsK) {  // (the previous row's reads of them are behind the wave barrier at its last chunk)
+      tr12[lane] = xlogx(R.rs_a - lane);
+      tr2122[lane] = xlogx(observed + 2 * int64_t(lane) - R.rs_a);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int64_t i0 = 0; i0 < n; i0 += kRsChunk) {
-      rs_score_chunk(src, rb, i0, n, R, exact, cterm, k11t, rscore, rcol, rq);
+      rs_score_chunk(src, rb, i0, n, R, exact, cterm, k11t, tr12, tr2122, rscore, rcol, rq);
       for (int j = 0; j < kRsR && i0 + j * 64 < n; j++) {
         const int32_t c = rcol[j * 64 + lane];
         const double score = rscore[j * 64 + lane];
@@ -749,7 +764,8 @@ int rescore_waves_per_block(int32_t topk) { return topk <= 1024 ? 4 : 1; }
 size_t rescore_lds_bytes(int32_t topk) {
   const size_t w = size_t(rescore_waves_per_block(topk));
   const size_t heaps = sizeof(double) * (w * size_t(topk + 1) + (w * size_t(topk + 1) + 1) / 2);
-  return heaps + w * kRsR * 64 * (sizeof(double) * 2);  // + per-wave score / column / queue rings
+  return heaps + w * kRsR * 64 * (sizeof(double) * 2)  // + per-wave score / column / queue rings
+         + w * 2 * kRsK * sizeof(double);                 // + the per-wave row tables
 }
 
 template <class Rows>
