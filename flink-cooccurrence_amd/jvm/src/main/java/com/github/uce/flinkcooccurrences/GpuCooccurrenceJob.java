@@ -83,6 +83,41 @@ final class GpuCooccurrenceJob {
   }
 
   /**
+   * p > 1 subtasks, a multi-window stream (n_items < 40,320): the keyBy(item) merge of partial rows replaced by
+   * the library's exchange per window (cooc.h, cooc_finish_window across GPUs).  Each subtask keeps its users'
+   * histories and the global rows it owns resident; gpuRescore: GpuNonSampledCooccurrenceTopKOperator rescores
+   * the owned rows on the device at parallelism p; otherwise the rows operator's complete owned rows and their
+   * job-wide row sums feed the reference's rescorer with no ItemRowMerge / RowSumMerge windows.
+   */
+  static DataStream<Tuple2<Integer, IntDoublePriorityQueue>> topKStreamOwned(
+      DataStream<Tuple3<Integer, Integer, Long>> interactionStream, int windowSize, TimeUnit windowUnit, int nItems,
+      int[] devices, short topK, int parallelism, String rendezvousDir, boolean gpuRescore) {
+    if (gpuRescore) {
+      return interactionStream
+          .keyBy(0)
+          .transform(
+              "GpuNonSampledCooccurrenceTopK (" + windowSize + " " + windowUnit + ", top " + topK + ", "
+                  + parallelism + " GPUs)",
+              GpuNonSampledCooccurrenceTopKOperator.getOutputType(),
+              new GpuNonSampledCooccurrenceTopKOperator(windowSize, windowUnit, nItems, devices, topK, rendezvousDir))
+          .setParallelism(parallelism);
+    }
+    final SingleOutputStreamOperator<Void> counter = interactionStream
+        .keyBy(0)
+        .transform(
+            "GpuNonSampledCooccurrenceRows (" + windowSize + " " + windowUnit + ", " + parallelism + " GPUs)",
+            GpuNonSampledCooccurrenceRowsOperator.getOutputType(),
+            new GpuNonSampledCooccurrenceRowsOperator(windowSize, windowUnit, nItems, devices, rendezvousDir))
+        .setParallelism(parallelism);
+    return counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROWS_TAG)
+        .keyBy(0).connect(counter.getSideOutput(GpuNonSampledCooccurrenceRowsOperator.ROW_SUM_TAG).broadcast())
+        .transform(
+            "ItemRowRescorer",
+            ItemRowRescorerTwoInputStreamOperator.getOutputType(),
+            new ItemRowRescorerTwoInputStreamOperator(topK));
+  }
+
+  /**
    * p > 1 subtasks, one window (the C3 / C5 configs): the keyBy(item) merge of partial rows replaced by the
    * library's exchange over RCCL.  gpuRescore: GpuOwnedCooccurrenceTopKOperator rescores the owned rows on the
    * device too and emits the rescorer's records itself (C5 never rescores on the JVM); otherwise

@@ -30,10 +30,17 @@ import org.apache.flink.util.OutputTag;
  *   RowSumProcessWindowRowSum accumulator (:50,67).</li>
  * </ul>
  * Every record carries the window's maxTimestamp, as a window operator's output does.  With one subtask
- * the rows and row sums are final and feed ItemRowRescorerTwoInputStreamOperator directly; with p > 1
- * each subtask holds a user shard (keyBy(0)), so its rows are partial and one keyed reduce per stream
- * ({@link GpuCooccurrenceJob}) sums the p partial rows per item and window -- p records per row
- * instead of one record per ordered pair.  Emitted objects are fresh (the rescorer buffers them by
+ * the rows and row sums are final and feed ItemRowRescorerTwoInputStreamOperator directly.  With p > 1
+ * each subtask holds a user shard (keyBy(0)); then either
+ * <ul>
+ *   <li>a rendezvousDir is given: the p handles join one communicator (the attempt's id from subtask 0,
+ *   {@link OwnedExchange#rendezvous}) and every window's exchange runs inside the library
+ *   (cooc_op_process_watermark is collective: partial delta rows to their owners a mod p over RCCL, row
+ *   sums all-reduced, the window agreed by an all-gather); each subtask emits the complete rows it owns and
+ *   the job's row sums of those rows, which feed the rescorer with no merge windows; or</li>
+ *   <li>its rows are partial and one keyed reduce per stream ({@link GpuCooccurrenceJob}) sums the p
+ *   partial rows per item and window -- p records per row instead of one record per ordered pair.</li>
+ * </ul>  Emitted objects are fresh (the rescorer buffers them by
  * timestamp, ItemRowRescorer...java:83-113, and object reuse is on, FlinkCooccurrences.java:44).
  * Uncompiled in the build container (no JDK, Flink 1.3.2 / fastutil jars absent); the C-ABI call
  * sequence it makes is replayed by tests/test_boundary_sequence.py.
@@ -55,6 +62,7 @@ public class GpuNonSampledCooccurrenceRowsOperator
   private final long windowSizeMs;
   private final int nItems;
   private final int[] devices;
+  private final String rendezvousDir;  // null: partial rows at p > 1 (merged downstream)
 
   private transient long handle;
   private transient int buffered;
@@ -68,16 +76,29 @@ public class GpuNonSampledCooccurrenceRowsOperator
   private transient LongCounter rowSumCounter;
 
   GpuNonSampledCooccurrenceRowsOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices) {
+    this(windowSize, windowUnit, nItems, devices, null);
+  }
+
+  /** rendezvousDir: a directory every subtask of the node reads (the communicator id per attempt). */
+  GpuNonSampledCooccurrenceRowsOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices,
+      String rendezvousDir) {
     this.windowSizeMs = windowUnit.toMillis(windowSize);
     this.nItems = nItems;
     this.devices = devices.clone();
+    this.rendezvousDir = rendezvousDir;
   }
 
   @Override
   public void open() throws Exception {
     super.open();
-    this.handle = CoocNative.create(devices, getRuntimeContext().getIndexOfThisSubtask(), nItems, 0, 0,
-        windowSizeMs, (short) 0);
+    final int subtask = getRuntimeContext().getIndexOfThisSubtask();
+    final int world = getRuntimeContext().getNumberOfParallelSubtasks();
+    this.handle = CoocNative.create(devices, subtask, nItems, 0, 0, windowSizeMs, (short) 0);
+    if (rendezvousDir != null && world > 1) {  // owned rows: the windows' exchange inside the library
+      CoocNative.commInit(handle, OwnedExchange.rendezvous(rendezvousDir,
+          getContainingTask().getEnvironment().getJobID().toString(), getRuntimeContext().getAttemptNumber(),
+          subtask), subtask, world);
+    }
     this.users = new int[1 << 16];
     this.items = new int[1 << 16];
     this.timestamps = new long[1 << 16];

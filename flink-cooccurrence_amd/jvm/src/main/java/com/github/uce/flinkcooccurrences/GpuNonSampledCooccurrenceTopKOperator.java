@@ -27,9 +27,15 @@ import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
  * Like the reference, one queue and one record are reused for every output (ItemRowRescorer...java:42-68);
  * rows are scored in the device's column order (cooc_copy_column_order), where the reference iterates
  * its hash map's slot order: ties at the k-th score may pick other items, as between two fastutil builds.
- * One subtask holds every user (the graph sets parallelism 1 on it): the resident global state is the
- * rescorer's, which the reference also keeps whole per item.  Uncompiled in the build container (no JDK,
- * Flink 1.3.2 / fastutil jars absent); tests/test_boundary_sequence.py replays its C-ABI call sequence.
+ * Without a rendezvousDir one subtask holds every user (the graph sets parallelism 1 on it): the resident
+ * global state is the rescorer's, which the reference also keeps whole per item.  With one, p subtasks each
+ * hold a keyBy(user) shard and the rows they own (a mod p): the p handles join one communicator and every
+ * window's exchange runs in the library (cooc_op_process_watermark is collective: partial delta rows to their
+ * owners, row sums and the window's pairs all-reduced -- the broadcast row-sum stream of
+ * FlinkCooccurrences.java:163 -- and the window agreed by an all-gather); each subtask rescores and emits its
+ * owned touched rows, so every item's queue appears on exactly one subtask.  Uncompiled in the build container
+ * (no JDK, Flink 1.3.2 / fastutil jars absent); tests/test_boundary_sequence.py replays its C-ABI call
+ * sequence at p = 1, tests/test_streaming_multiproc.py the same sequence on two subtasks.
  */
 public class GpuNonSampledCooccurrenceTopKOperator
     extends AbstractStreamOperator<Tuple2<Integer, IntDoublePriorityQueue>>
@@ -41,6 +47,7 @@ public class GpuNonSampledCooccurrenceTopKOperator
   private final int nItems;
   private final int[] devices;
   private final short topK;
+  private final String rendezvousDir;  // null: one subtask
 
   private transient long handle;
   private transient int buffered;
@@ -58,6 +65,12 @@ public class GpuNonSampledCooccurrenceTopKOperator
   private transient LongCounter rescoredItems;
 
   GpuNonSampledCooccurrenceTopKOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices, short topK) {
+    this(windowSize, windowUnit, nItems, devices, topK, null);
+  }
+
+  /** rendezvousDir: a directory every subtask of the node reads (the communicator id per attempt). */
+  GpuNonSampledCooccurrenceTopKOperator(int windowSize, TimeUnit windowUnit, int nItems, int[] devices, short topK,
+      String rendezvousDir) {
     if (topK <= 0) {  // ItemRowRescorerTwoInputStreamOperator.java:52-54
       throw new IllegalArgumentException(topK + " is <= 0");
     }
@@ -65,13 +78,20 @@ public class GpuNonSampledCooccurrenceTopKOperator
     this.nItems = nItems;
     this.devices = devices.clone();
     this.topK = topK;
+    this.rendezvousDir = rendezvousDir;
   }
 
   @Override
   public void open() throws Exception {
     super.open();
-    this.handle = CoocNative.create(devices, getRuntimeContext().getIndexOfThisSubtask(), nItems, topK, 0,
-        windowSizeMs, (short) 0);
+    final int subtask = getRuntimeContext().getIndexOfThisSubtask();
+    final int world = getRuntimeContext().getNumberOfParallelSubtasks();
+    this.handle = CoocNative.create(devices, subtask, nItems, topK, 0, windowSizeMs, (short) 0);
+    if (rendezvousDir != null && world > 1) {  // owned rows: the windows' exchange inside the library
+      CoocNative.commInit(handle, OwnedExchange.rendezvous(rendezvousDir,
+          getContainingTask().getEnvironment().getJobID().toString(), getRuntimeContext().getAttemptNumber(),
+          subtask), subtask, world);
+    }
     this.users = new int[1 << 16];
     this.items = new int[1 << 16];
     this.timestamps = new long[1 << 16];

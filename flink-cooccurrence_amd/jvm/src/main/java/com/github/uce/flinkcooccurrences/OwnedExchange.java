@@ -26,7 +26,8 @@ import java.util.Arrays;
  * holds no record) through the library's communicator (cooc_comm_allgather_i64); the window fires on EVERY
  * subtask once its end has passed -- a subtask without records joins the same collectives with an empty shard
  * -- and records of two different windows fail every subtask alike (IllegalStateException).  Multi-window
- * streams keep the partial-row path (GpuCooccurrenceJob.topK).
+ * streams use the library's per-window exchange instead (GpuCooccurrenceJob.topKStreamOwned), which shares
+ * {@link #rendezvous}.
  */
 final class OwnedExchange {
 

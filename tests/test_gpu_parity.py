@@ -355,6 +355,37 @@ def test_c2_scale_properties(pkg, oracle, torch_cuda):
         assert np.array_equal(cnt[s:e], row[row != 0])
 
 
+def test_c2_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda):
+    """BASELINE configs[1] (C2) at full size, EVERY row: the dense batch path's result (k_acc_batch) checked on
+    the device against per-row fingerprints of the closed-form CPU restatement (oracle.row_checksums:
+    checksum = sum of splitmix64(col << 32 ^ count) over the row's keys, key count, count sum; it agrees with
+    the record-by-record restatement in tests/test_oracle_semantics.py)."""
+    torch = torch_cuda
+    from bench import cpu_threads
+    from flink_cooccurrence_amd import datagen
+
+    d = datagen.config_c2()
+    up, it, M = d["user_ptr"], d["items"], d["n_items"]
+    dev = torch.device("cuda", 0)
+    with pkg.CooccurrenceCore(n_items=M, device=0) as core:
+        res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+        cs = torch.zeros(M, dtype=torch.int64, device=dev)
+        chk = core.verify_batch(symmetry=False, row_checksum=cs)
+        torch.cuda.synchronize()
+        nnz = _d2h(res.row_nnz, M, np.int32)
+        cs = cs.cpu().numpy().view(np.uint64)
+        observed, entries = res.observed, res.nnz
+    want = oracle.row_checksums(up, it, M, cpu_threads()[0])
+    P = datagen.ordered_pairs(up)
+    assert observed == P == want.pairs
+    assert chk["rows_bad_sum"] == 0 and chk["rows_bad_entries"] == 0
+    assert chk["sum_counts"] == chk["sum_rowsums"] == P
+    assert chk["entries"] == entries == want.distinct
+    assert np.array_equal(nnz.astype(np.int64), want.nnz), "per-row key counts differ"
+    bad = np.flatnonzero(cs != want.checksum)
+    assert len(bad) == 0, f"{len(bad)} of {M} rows differ from the oracle, e.g. {bad[:10].tolist()}"
+
+
 def _d2h(ptr, n, dtype):
     import ctypes
 
