@@ -141,6 +141,9 @@ def main():
                     help="C3/C5: item ids through the fixed bijection datagen.c3_item_perm (ids not in popularity order)")
     ap.add_argument("--no-permuted", action="store_true",
                     help="C3 at N=1: skip the line's `permuted` sub-record (the same log with permuted item ids)")
+    ap.add_argument("--ordered-rows", action="store_true",
+                    help="C3: rows in column order (without it the counting line runs with COOC_FLAG_ANY_ORDER, the "
+                         "rows operator's setting: hash chunks in slot order, as the reference's Int2ShortOpenHashMap)")
     args = ap.parse_args()
 
     import torch
@@ -199,7 +202,10 @@ def main():
     if pmc_stale:  # counters of other code: not reported as this kernel's
         pmc = {"kernel": pmc.get("kernel"), "stale_source_digest": pmc.get("source_digest")}
 
-    core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
+    # C3 counts for the rows operators, which build hash maps from the rows: no column order needed
+    # (COOC_FLAG_ANY_ORDER); C5 feeds the heaps in column order (the tie contract of its parity tests)
+    any_order = args.config == "c3" and not args.ordered_rows
+    core = pkg.CooccurrenceCore(n_items=M, device=local_rank, any_order=any_order)
     core.set_kernel_timing(True)
     # N > 1, C3/C5: the exchange runs inside the library (cooc_count_owned / cooc_topk_owned) over its own RCCL
     # communicator; COOC_BENCH_EXCHANGE=torch keeps the torch.distributed orchestration of sharding.py
@@ -324,7 +330,9 @@ def main():
             "workload": workload,
             "users_per_gpu": U, "items": M, "interactions_per_gpu": N, "ordered_pairs_total": int(p_total),
             "distinct_keys_total": int(d_total),
-            "output": "padded CSR (row_base, row_nnz, col int32, cnt uint32) in HBM, exact counts",
+            "output": "padded CSR (row_base, row_nnz, col int32, cnt uint32) in HBM, exact counts" + (
+                "; a row's entries in no particular order (COOC_FLAG_ANY_ORDER: hash chunks in slot order, as the "
+                "reference's Int2ShortOpenHashMap rows)" if any_order else "; rows in column order"),
             "parallelism": f"users sharded over {world} GPU(s)" + (
                 "; rows owned by frequency-snake order, histories all-gathered over RCCL" + (
                     " inside the library (cooc_count_owned)" if lib_exchange else " (torch.distributed)")

@@ -27,6 +27,7 @@ COOC_FLAG_OUTPUT_DENSE = 4
 COOC_FLAG_GENERAL_PLANNER = 8
 COOC_FLAG_SORT_ROWS = 16
 COOC_FLAG_COLUMN_ORDER = 32
+COOC_FLAG_ANY_ORDER = 64
 COOC_VERIFY_SYMMETRY = 1
 
 i16p = ctypes.POINTER(ctypes.c_int16)

@@ -91,7 +91,7 @@ class CooccurrenceCore:
 
     def __init__(self, n_items: int, topk: int = 0, window_size_ms: int = 1000, device: int = -1,
                  exact_scores: bool = False, output: str = "auto", planner: str = "auto", user_cut: int = 0,
-                 devices=None, subtask: int = 0, column_order: bool = False):
+                 devices=None, subtask: int = 0, column_order: bool = False, any_order: bool = False):
         """output: layout of count_device results: "auto", "csr" (padded CSR) or "dense" (n_items^2).
         planner: "auto" (the batch planner below 40,320 items, the large-universe planner above), "large"
         (the large-universe planner at any n_items; "general" is an alias) or "sort" (large, with every
@@ -100,7 +100,9 @@ class CooccurrenceCore:
         (UserInteractionCounter...java:168-205, the deterministic branch; later ones are dropped).
         column_order: COOC_FLAG_COLUMN_ORDER (device rows of the large-universe path in id order instead of the
         renumbered order: the batch's 16,384 most frequent items first, in id order, then the rest in id order;
-        the renumbering is skipped when 15/16 of those hot items already have ids below 16,384)."""
+        the renumbering is skipped when 15/16 of those hot items already have ids below 16,384).
+        any_order: COOC_FLAG_ANY_ORDER (large-universe batch rows in no particular order: the LDS hash chunks skip
+        their column ranking; host copies still come out sorted)."""
         L = _lib.load()
         flags = _lib.COOC_FLAG_EXACT_SCORES if exact_scores else 0
         if output not in ("auto", "csr", "dense"):
@@ -111,6 +113,7 @@ class CooccurrenceCore:
         flags |= _lib.COOC_FLAG_GENERAL_PLANNER if planner != "auto" else 0
         flags |= _lib.COOC_FLAG_SORT_ROWS if planner == "sort" else 0
         flags |= _lib.COOC_FLAG_COLUMN_ORDER if column_order else 0
+        flags |= _lib.COOC_FLAG_ANY_ORDER if any_order else 0
         cfg = CoocConfig(device, n_items, topk, flags, window_size_ms, user_cut, 0)
         h = ctypes.c_void_p()
         if devices is None:

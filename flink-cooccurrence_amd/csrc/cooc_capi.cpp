@@ -375,6 +375,8 @@ int cooc_partition_plan(cooc_ctx *ctx, int32_t n_parts, int64_t *h_entries) {
   return guarded(ctx, [&]() -> int {
     if (!ctx || !h_entries) return COOC_ERR_ARG;
     if (!ctx->have_batch) return fail(ctx, COOC_ERR_STATE, "no cooc_count_device result to partition");
+    if (ctx->batch_result.unordered)
+      return fail(ctx, COOC_ERR_STATE, "a COOC_FLAG_ANY_ORDER result cannot be partitioned (the merge needs ordered rows)");
     Status s = hipSetDevice(ctx->device) == hipSuccess
                    ? ctx->sharder.plan(ctx->batch_result, ctx->cfg.n_items, n_parts, ctx->stream, h_entries)
                    : Status{COOC_ERR_HIP, "hipSetDevice"};

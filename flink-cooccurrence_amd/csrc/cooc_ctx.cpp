@@ -39,6 +39,7 @@ Status cooc_ctx::init(const cooc_config &c) {
   counter.set_general_only((c.flags & COOC_FLAG_GENERAL_PLANNER) != 0);
   counter.set_sort_rows((c.flags & COOC_FLAG_SORT_ROWS) != 0);
   counter.set_relabel((c.flags & COOC_FLAG_COLUMN_ORDER) == 0);
+  counter.set_any_order((c.flags & COOC_FLAG_ANY_ORDER) != 0);
   return Status::Ok();
 }
 
@@ -207,11 +208,14 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
   uint32_t *d_cnt;
   COOC_TRY(counter.pack(stream, &d_rp, &d_col, &d_cnt));
   COOC_HIP_TRY(hipStreamSynchronize(stream));
-  if (!batch_result.rank_of) {
+  // the device rows need sorting on the way out when they are not in id order: a relabel's column order, or
+  // no order at all (COOC_FLAG_ANY_ORDER)
+  const bool resort = batch_result.rank_of || batch_result.unordered;
+  if (!resort) {
     if (row_ptr) COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
     if (cols && batch_nnz) COOC_HIP_TRY(hipMemcpy(cols, d_col, sizeof(int32_t) * batch_nnz, hipMemcpyDeviceToHost));
   }
-  if ((cnt || cnt16 || batch_result.rank_of) && batch_nnz) {
+  if ((cnt || cnt16 || resort) && batch_nnz) {
     std::vector<uint32_t> tmp;
     uint32_t *dst = cnt;
     if (!dst) {
@@ -219,9 +223,8 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
       dst = tmp.data();
     }
     COOC_HIP_TRY(hipMemcpy(dst, d_cnt, sizeof(uint32_t) * batch_nnz, hipMemcpyDeviceToHost));
-    if (batch_result.rank_of) {
-      // the device rows are in descending-frequency column order (the large-universe relabel): the packed
-      // host copy is in ascending column order, each row sorted as (column, count) pairs
+    if (resort) {
+      // the packed host copy is in ascending column order, each row sorted as (column, count) pairs
       std::vector<int64_t> rp(static_cast<size_t>(M) + 1);
       std::vector<int32_t> cc(static_cast<size_t>(batch_nnz));
       COOC_HIP_TRY(hipMemcpy(rp.data(), d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
@@ -242,7 +245,7 @@ Status cooc_ctx::copy_batch(int64_t *row_ptr, int32_t *cols, uint32_t *cnt, int1
     }
     if (cnt16)  // Int2ShortOpenHashMap value: the count modulo 2^16 as a signed short
       for (int64_t i = 0; i < batch_nnz; i++) cnt16[i] = int16_t(uint16_t(dst[i]));
-  } else if (batch_result.rank_of && row_ptr) {
+  } else if (resort && row_ptr) {
     COOC_HIP_TRY(hipMemcpy(row_ptr, d_rp, sizeof(int64_t) * (M + 1), hipMemcpyDeviceToHost));
   }
   if (rowsum || rowsum32) {
@@ -276,7 +279,7 @@ Status cooc_ctx::copy_batch_range(int32_t r0, int32_t r1, int64_t cap, int32_t *
   std::vector<uint32_t> vv(static_cast<size_t>(n));
   COOC_HIP_TRY(hipMemcpy(cc.data(), batch_pk_col + e0, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
   COOC_HIP_TRY(hipMemcpy(vv.data(), batch_pk_cnt + e0, sizeof(uint32_t) * size_t(n), hipMemcpyDeviceToHost));
-  if (batch_result.rank_of) {  // ascending column order, as cooc_copy_batch
+  if (batch_result.rank_of || batch_result.unordered) {  // ascending column order, as cooc_copy_batch
     std::vector<uint64_t> kv;
     for (int32_t a = r0; a < r1; a++) {
       const int64_t b0 = batch_rp_host[size_t(a)] - e0, b1 = batch_rp_host[size_t(a) + 1] - e0;
@@ -428,7 +431,7 @@ Status cooc_ctx::verify_batch(int32_t flags, uint64_t *d_row_checksum, int64_t *
   COOC_HIP_TRY(hipMemcpyAsync(h, b_verify.p, sizeof(h), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   for (int i = 0; i < 8; i++) out8[i] = int64_t(h[i]);
-  if (!sym || batch_result.dense) out8[5] = -1;
+  if (!sym || batch_result.dense || batch_result.unordered) out8[5] = -1;
   out8[6] = out8[7] = 0;
   return Status::Ok();
 }

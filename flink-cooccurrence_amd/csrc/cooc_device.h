@@ -134,6 +134,7 @@ struct CountResult {
   // the column order of the rows: ascending rank_of[col] (the large-universe batch path puts the batch's
   // 16,384 most frequent items first, then the rest, each group by id); NULL = ascending column id
   const int32_t *rank_of = nullptr;
+  bool unordered = false;  // COOC_FLAG_ANY_ORDER: the rows' entries in no particular order
   int64_t nnz = 0;
   int64_t observed = 0;  // ordered pairs of the run
   int64_t work = 0;
@@ -193,6 +194,7 @@ class Counter {
   // path (otherwise only rows whose LDS hash table overflowed); rows and pairs it took in the last run
   void set_sort_rows(bool on) { sort_rows_ = on; }
   void set_relabel(bool on) { relabel_ = on; }
+  void set_any_order(bool on) { any_order_ = on; }
   const int32_t *last_rank_of() const { return last_pos_of_; }
   int64_t last_deferred_rows() const { return last_deferred_; }
   int64_t last_deferred_pairs() const { return last_deferred_pairs_; }
@@ -251,6 +253,7 @@ class Counter {
   // ids), the others at id + kTW; skipped when 15/16 of them have ids < kTW (off: COOC_FLAG_COLUMN_ORDER); the
   // last run's maps (NULL without a relabel)
   bool relabel_ = true;
+  bool any_order_ = false;  // COOC_FLAG_ANY_ORDER: hash chunks emitted in slot order (batch results)
   DevBuf sp_rank_, sp_rkeys_, sp_bits_;  // (sp_bits_: the hot-column and owned-row bitmaps of the user passes)
   const int32_t *last_hot_col_ = nullptr, *last_pos_of_ = nullptr;
   int32_t last_mc_ = 0;       // columns of the last run's (relabelled) space

@@ -190,6 +190,7 @@ struct SpArgs {
   const int64_t *spre;      // streaming window: [n_contrib + 1] prefix of the kSelfBit flags; NULL: all set
   int32_t *deferred;        // [M] whole rows left to the sort + segmented-reduce path (k_sr_*), in tot->n_deferred
   int32_t sort_all;         // COOC_FLAG_SORT_ROWS: every whole row goes to that path (A/B and tests)
+  int32_t any_order;        // COOC_FLAG_ANY_ORDER: hash chunks emitted in slot order (no column ranking)
   // column relabel (batch windows, k_relabel_*): the kernels work in relabelled column space -- tile 0 holds
   // the batch's kTW most frequent items (hot_col[c], ascending ids), column c >= kTW the item c - kTW (its
   // own id shifted one tile up; the hot items leave holes there) -- and write the item ids to the output.
@@ -1381,12 +1382,71 @@ __device__ inline void sp_hash_compact(const SpArgs &A, const SpShared &L, SpSta
         ek[i] = col;
         ec[i] = vv[u];
         rsum += vv[u];
-        atomicOr(&L.L1[col >> 10], 1u << ((col >> 5) & 31u));
+        if (!A.any_order) atomicOr(&L.L1[col >> 10], 1u << ((col >> 5) & 31u));
       }
     }
   }
   __syncthreads();
   STAT_ADD(46, STAT_CLOCK() - c_h0);
+  if (A.any_order) {  // COOC_FLAG_ANY_ORDER: the keys in slot order, a thread's after the threads before it
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) cnt += ek[i] != ~0u;
+    uint32_t ne;
+    uint32_t q = block_excl_scan<Sh::kWaves>(cnt, &ne, S_.wtot);
+    const unsigned long long c_a1 = STAT_CLOCK();
+    STAT_ADD(20, c_a1 - c_h0);
+    const int64_t base = sp_reserve<Sh>(A, S_, ne);  // (barrier)
+    const unsigned long long c_a2 = STAT_CLOCK();
+    STAT_ADD(21, c_a2 - c_a1);
+    if (base >= 0 && ne <= uint32_t(Sh::kWStage)) {  // staged in LDS, then 16-B stores (as below)
+      uint32_t *sc = keys + Sh::kWStage, *sn = cnts + Sh::kWStage;
+#pragma unroll
+      for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) {
+        if (ek[i] == ~0u) continue;
+        sc[q] = uint32_t(sp_col(A, uint32_t(c0) + ek[i]));
+        sn[q] = ec[i];
+        q++;
+      }
+      __syncthreads();
+      const uint32_t head = min(ne, uint32_t((4 - (base & 3)) & 3));
+      const uint32_t body = (ne - head) >> 2;
+      for (uint32_t j = tid; j < head; j += Sh::kThreads) {
+        A.col_out[base + j] = int32_t(sc[j]);
+        A.cnt_out[base + j] = sn[j];
+      }
+      int4 *co4 = reinterpret_cast<int4 *>(A.col_out + base + head);
+      uint4 *cn4 = reinterpret_cast<uint4 *>(A.cnt_out + base + head);
+      for (uint32_t j = tid; j < body; j += Sh::kThreads) {
+        const uint32_t r = head + 4 * j;
+        co4[j] = make_int4(int32_t(sc[r]), int32_t(sc[r + 1]), int32_t(sc[r + 2]), int32_t(sc[r + 3]));
+        cn4[j] = make_uint4(sn[r], sn[r + 1], sn[r + 2], sn[r + 3]);
+      }
+      for (uint32_t r = head + 4 * body + tid; r < ne; r += Sh::kThreads) {
+        A.col_out[base + r] = int32_t(sc[r]);
+        A.cnt_out[base + r] = sn[r];
+      }
+      __syncthreads();
+      for (uint32_t r = tid; r < ne; r += Sh::kThreads) {
+        sc[r] = 0u;
+        sn[r] = 0u;
+      }
+    } else if (base >= 0) {
+#pragma unroll
+      for (int i = 0; i < Sh::kHashMax / Sh::kThreads; i++) {
+        if (ek[i] == ~0u) continue;
+        if (BCHK(A, base + q < A.cap, 128)) {
+          A.col_out[base + q] = sp_col(A, uint32_t(c0) + ek[i]);
+          A.cnt_out[base + q] = ec[i];
+        }
+        q++;
+      }
+    }
+    __syncthreads();
+    STAT_ADD(22, STAT_CLOCK() - c_a2);
+    STAT_ADD(23, ne);
+    return;
+  }
   uint32_t nblk;
   {
     static_assert(Sh::kL1Words % Sh::kThreads == 0, "L1 words per thread");
@@ -3174,6 +3234,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sp_defer_.reserve(sizeof(int32_t) * size_t(M)));
   proto.deferred = sp_defer_.as<int32_t>();
   proto.sort_all = sort_rows_ ? 1 : 0;
+  proto.any_order = (any_order_ && !win) ? 1 : 0;
   proto.hot_col = hot_col;
   proto.pos_of = pos_of;
   int64_t last_err = 0;
@@ -3370,6 +3431,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   out->dense = nullptr;
   out->rowsum = rowsum_.as<int64_t>();
   out->rank_of = pos_of;
+  out->unordered = proto.any_order != 0;
   out->work = work_total;
   out->observed = work_total - self_total;  // ordered pairs of the counted rows
   out->nnz = -1;  // known after the stream drains: read_totals().nnz_total

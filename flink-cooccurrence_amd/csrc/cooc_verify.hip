@@ -5,7 +5,8 @@
 // that check, and the ones the CSR contract adds, over a whole cooc_count_device result in HBM:
 //   * sum over the row's counts == rowsum[a] (the closed form W_a - c_a the planner wrote),
 //   * columns strictly ascending within a row (in the result's column order: ascending rank_of[col] after the
-//     large-universe path's frequency relabel, else ascending id) and inside [0, n_items), every stored
+//     large-universe path's frequency relabel, else ascending id; not checked for a COOC_FLAG_ANY_ORDER
+//     result) and inside [0, n_items), every stored
 //     count > 0
 //     (a key exists iff it was touched: every increment is +1, ItemRowAggregator.java:29),
 //   * optionally C[a, b] == C[b, a] for every entry (the ordered pairs of a user are symmetric),
@@ -39,7 +40,7 @@ __device__ inline uint64_t wave_sum(uint64_t v) {
 __global__ __launch_bounds__(256) void k_verify_csr(int32_t M, const int64_t *__restrict__ row_base,
                                                     const int32_t *__restrict__ row_nnz, const int32_t *__restrict__ col,
                                                     const uint32_t *__restrict__ cnt, const int64_t *__restrict__ rowsum,
-                                                    const int32_t *__restrict__ rank_of,
+                                                    const int32_t *__restrict__ rank_of, int32_t ordered,
                                                     uint64_t *__restrict__ cs_out, unsigned long long *__restrict__ tot) {
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void k_verify_csr(int32_t M, const int64_t *__
       h += row_key_hash(c, v);
       s += v;
       bool ok = c >= 0 && c < M && v > 0u;
-      if (ok && i + 1 < n) {
+      if (ok && ordered && i + 1 < n) {
         const int32_t c1 = col[b + i + 1];
         ok = rank_of ? (c1 >= 0 && c1 < M && rank_of[c1] > rank_of[c]) : c1 > c;
       }
@@ -171,8 +172,9 @@ Status launch_verify(hipStream_t s, int32_t M, const CountResult &r, bool symmet
   if (r.dense) {
     k_verify_dense<<<grid, 256, 0, s>>>(M, r.dense, r.row_nnz, r.rowsum, d_cs, d_tot);
   } else {
-    k_verify_csr<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, r.rank_of, d_cs, d_tot);
-    if (symmetry) k_verify_symmetry<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rank_of, d_tot);
+    k_verify_csr<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rowsum, r.rank_of, r.unordered ? 0 : 1,
+                                      d_cs, d_tot);
+    if (symmetry && !r.unordered) k_verify_symmetry<<<grid, 256, 0, s>>>(M, r.row_base, r.row_nnz, r.col, r.cnt, r.rank_of, d_tot);
   }
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();

@@ -94,6 +94,16 @@ enum cooc_status {
  * The host copies (cooc_copy_batch) are always in ascending id order.  This flag keeps id order on the
  * device at the price of the renumbering's gain (ids not numbered by popularity run up to ~1.8x slower). */
 #define COOC_FLAG_COLUMN_ORDER 32
+/* Large universes, batch results: a row's entries may come out in any order (the row holds the same keys and
+ * counts).  Without it every row is in the result's column order, which costs the LDS hash chunks a column
+ * ranking of their keys; the reference's own row is an Int2ShortOpenHashMap, iterated in slot order
+ * (ItemRowAggregator.java:50-56, ItemRowRescorer...java:195), so a consumer that builds maps from the rows
+ * (the Flink rows operators) or only sums them needs no order.  The host copies (cooc_copy_batch,
+ * cooc_copy_batch_range) still sort every row; the top-k of an unordered result feeds each heap in the row's
+ * order (ties may resolve differently, as between two fastutil builds); cooc_verify_batch checks keys,
+ * counts and sums but not the order (and not the symmetry: [5] = -1); cooc_partition_plan refuses such a
+ * result (the partial-row merge needs ordered rows).  Streaming windows always keep column order. */
+#define COOC_FLAG_ANY_ORDER 64
 
 typedef struct cooc_ctx cooc_ctx;
 

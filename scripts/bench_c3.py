@@ -47,7 +47,10 @@ def main():
     t_gen = time.perf_counter() - t0
     P = datagen.c3_ordered_pairs(0, U)
     M = datagen.C3_ITEMS
-    core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner, column_order=args.column_order)
+    # COOC_BENCH_ANY_ORDER=1: COOC_FLAG_ANY_ORDER (rows in no particular order; A/B through the environment)
+    any_order = os.environ.get("COOC_BENCH_ANY_ORDER", "0") == "1"
+    core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner, column_order=args.column_order,
+                                any_order=any_order)
     core.set_kernel_timing(True)
     res = core.count_device(up, it)  # warm-up (allocations)
     torch.cuda.synchronize()

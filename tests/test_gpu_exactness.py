@@ -37,9 +37,9 @@ def _threads():
     return cpu_threads()[0]
 
 
-def _device_checks(pkg, torch, up_d, it_d, M, symmetry):
+def _device_checks(pkg, torch, up_d, it_d, M, symmetry, any_order=False):
     dev = up_d.device
-    with pkg.CooccurrenceCore(n_items=M, device=dev.index or 0) as core:
+    with pkg.CooccurrenceCore(n_items=M, device=dev.index or 0, any_order=any_order) as core:
         res = core.count_device(up_d, it_d)
         cs = torch.zeros(M, dtype=torch.int64, device=dev)
         chk = core.verify_batch(symmetry=symmetry, row_checksum=cs)
@@ -78,17 +78,19 @@ def test_c3_256th_every_row_vs_record_by_record_oracle(pkg, oracle, torch_cuda, 
     _compare(res, chk, cs, nnz, want, datagen.ordered_pairs(up))
 
 
-@pytest.mark.parametrize("share,permute", [(64, False), (8, False), (8, True)])
-def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share, permute):
-    """share = 8 is the benchmark's workload (bench.py, N = 1): users [0, 1.25e6) of the 1B log."""
+@pytest.mark.parametrize("share,permute,any_order", [(64, False, False), (8, False, False), (8, True, False),
+                                                     (8, False, True), (64, True, True)])
+def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share, permute, any_order):
+    """share = 8 is the benchmark's workload (bench.py, N = 1): users [0, 1.25e6) of the 1B log.  any_order:
+    COOC_FLAG_ANY_ORDER (rows in no particular order; the fingerprints are order-independent sums)."""
     torch = torch_cuda
     from flink_cooccurrence_amd import datagen
 
     U, M = datagen.C3_USERS // share, datagen.C3_ITEMS
     dev = torch.device("cuda", 0)
     up_d, it_d = datagen.c3_users(0, U, device=dev, permute=permute)
-    res, chk, cs, nnz = _device_checks(pkg, torch, up_d, it_d, M, symmetry=share >= 64)
-    if share >= 64:
+    res, chk, cs, nnz = _device_checks(pkg, torch, up_d, it_d, M, symmetry=share >= 64, any_order=any_order)
+    if share >= 64 and not any_order:
         assert chk["asymmetric_entries"] == 0
     up, it = up_d.cpu().numpy(), it_d.cpu().numpy()
     del up_d, it_d

@@ -172,6 +172,57 @@ def test_c3_shape_vs_closed_form(pkg, oracle, torch_cuda, planner, permute):
     assert np.array_equal(got.rowsum, rowsums)
 
 
+@pytest.mark.parametrize("permute", [False, True])
+def test_any_order_rows_vs_closed_form(pkg, oracle, torch_cuda, permute):
+    """COOC_FLAG_ANY_ORDER (hash chunks emitted in slot order, no column ranking) on 3,000 users of the C3 log:
+    every device row holds the closed form's keys and counts (as a set), the host copy comes out sorted and
+    equal to the closed form, the in-range row copies too, cooc_verify_batch passes without an order check,
+    the top-k heaps score the same entries (the sorted score lists equal the ordered run's), and the
+    partial-row partition refuses the result."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    up, it = datagen.c3_users(0, 3000, permute=permute)
+    M = datagen.C3_ITEMS
+    rp, cols, data, rowsums, observed = oracle.closed_form(up, it, M)
+    dev = torch.device("cuda")
+    k = 10
+    tops = []
+    for any_order in (False, True):
+        with pkg.CooccurrenceCore(n_items=M, device=0, any_order=any_order) as core:
+            res = core.count_device(torch.from_numpy(up).to(dev), torch.from_numpy(it).to(dev))
+            torch.cuda.current_stream().synchronize()
+            chk = core.verify_batch()
+            assert chk["rows_bad_sum"] == 0 and chk["rows_bad_entries"] == 0
+            assert chk["sum_counts"] == chk["sum_rowsums"] == observed
+            rows = _Rows(res, M)
+            for a in np.flatnonzero(np.diff(rp))[::37]:
+                c, n = rows.row(int(a))  # (sorted here: the device order is free)
+                assert np.array_equal(c, cols[rp[a]:rp[a + 1]]) and np.array_equal(n, data[rp[a]:rp[a + 1]])
+            got = core.copy_batch(res.nnz, res.observed)
+            assert np.array_equal(got.row_ptr, rp) and np.array_equal(got.cols, cols)
+            assert np.array_equal(got.cnt.astype(np.int64), data) and np.array_equal(got.rowsum, rowsums)
+            r0, r1 = 0, 50_000
+            e0, e1 = rp[r0], rp[r1]
+            cc, vv, _ = core.copy_batch_range(r0, r1, e1 - e0)
+            assert np.array_equal(cc, cols[e0:e1]) and np.array_equal(vv.astype(np.int64), data[e0:e1])
+            sample = np.flatnonzero(np.diff(rp))[:200].astype(np.int32)
+            sizes, vals, scores = core.topk_items(sample, k)
+            tops.append((sizes, [np.sort(scores[i, :s]) for i, s in enumerate(sizes)]))
+            if any_order:
+                with pytest.raises(pkg.CoocError):
+                    core.partition_plan(2)
+    assert np.array_equal(tops[0][0], tops[1][0])
+    # the same top scores whatever order fed the heaps -- in rows without a NaN score (an int16-wrapped count:
+    # NaN compares false in the heap, so which entries stay depends on the feeding order, as in the reference)
+    compared = 0
+    for x, y in zip(tops[0][1], tops[1][1]):
+        if not (np.isnan(x).any() or np.isnan(y).any()):
+            assert np.array_equal(x, y)
+            compared += 1
+    assert compared > 100
+
+
 def test_c3_sixty_fourth_properties(pkg, torch_cuda):
     """1/64 of C3 (156,250 users, ~1.6e7 interactions, ~4e9 ordered pairs) generated on the GPU:
     observed == P and sum(rowsum) == P from the generator's lengths, sum(row_nnz) == nnz, sampled rows
