@@ -142,8 +142,8 @@ def main():
     ap.add_argument("--no-permuted", action="store_true",
                     help="C3 at N=1: skip the line's `permuted` sub-record (the same log with permuted item ids)")
     ap.add_argument("--ordered-rows", action="store_true",
-                    help="C3: rows in column order (without it the counting line runs with COOC_FLAG_ANY_ORDER, the "
-                         "rows operator's setting: hash chunks in slot order, as the reference's Int2ShortOpenHashMap)")
+                    help="C3: rows in column order (without it the counting line runs with COOC_FLAG_ANY_ORDER: a "
+                         "row's entries in no particular order, as the reference's Int2ShortOpenHashMap rows)")
     args = ap.parse_args()
 
     import torch
@@ -202,8 +202,9 @@ def main():
     if pmc_stale:  # counters of other code: not reported as this kernel's
         pmc = {"kernel": pmc.get("kernel"), "stale_source_digest": pmc.get("source_digest")}
 
-    # C3 counts for the rows operators, which build hash maps from the rows: no column order needed
-    # (COOC_FLAG_ANY_ORDER); C5 feeds the heaps in column order (the tie contract of its parity tests)
+    # C3 counts: the reference's rows are hash maps, so the count itself owes no column order (COOC_FLAG_ANY_ORDER;
+    # consumers that want one pay for it: the host copies sort); C5 feeds the heaps in column order (the tie
+    # contract of its parity tests)
     any_order = args.config == "c3" and not args.ordered_rows
     core = pkg.CooccurrenceCore(n_items=M, device=local_rank, any_order=any_order)
     core.set_kernel_timing(True)
