@@ -365,8 +365,9 @@ def main():
             "note": "B_alg = 4P + 4N + 8(U+1) + 12D per launch of the dominant kernel (SURVEY.md §8(d); for C3 the "
                     "counting kernels together, which share the rows between them), divided by its time from HIP "
                     "events on its stream; frac > 1 would flag cache reuse. "
-                    "traffic = HBM-side bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, "
-                    "profiles/pmc_<kernel>.json) when collected; see DESIGN.md §4",
+                    "traffic = HBM-side bytes per launch (C3: per step, summed over traffic_kernels, the same span) "
+                    "from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, profiles/pmc_<kernel>.json) when collected; see "
+                    "DESIGN.md §4",
         },
         "cpu_baseline": None,
         "permuted": None,

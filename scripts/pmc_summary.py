@@ -14,14 +14,24 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_k_acc_batch.json"
+# argv[3] = steps per pass: the counters of every matched launch of a pass summed and divided by the steps
+# (several kernels per step, e.g. the counting span's k_sp_main launches + k_sp_small); else one kernel,
+# averaged over its launches
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 vals = collections.defaultdict(list)
-kernel = None
+names = set()
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        kernel = (__import__("re").search(r"(k_\w+)", r["Kernel_Name"]) or [None, r["Kernel_Name"]])[1]
+        names.add((__import__("re").search(r"(k_\w+)", r["Kernel_Name"]) or [None, r["Kernel_Name"]])[1])
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-avg = {k: sum(v) / len(v) for k, v in vals.items()}
-res = {"kernel": kernel, "launches_averaged": max(len(v) for v in vals.values()), "counters_avg": avg}
+if steps:
+    avg = {k: sum(v) / steps for k, v in vals.items()}  # (every counter's pass ran `steps` steps)
+    res = {"kernel": "+".join(sorted(names)), "kernels": sorted(names), "per": f"step (sum of the kernels' launches, {steps} steps per pass)",
+           "counters_avg": avg}
+else:
+    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    res = {"kernel": sorted(names)[0] if names else None, "launches_averaged": max(len(v) for v in vals.values()),
+           "counters_avg": avg}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     fetch = avg["FETCH_SIZE"] * 1024
     write = avg["WRITE_SIZE"] * 1024
