@@ -49,7 +49,8 @@ def main():
     del ups, its
     M = datagen.C3_ITEMS
     N = int(it.numel())
-    core = pkg.CooccurrenceCore(n_items=M, device=0)
+    # (COOC_BENCH_ANY_ORDER=1: the bench line's COOC_FLAG_ANY_ORDER)
+    core = pkg.CooccurrenceCore(n_items=M, device=0, any_order=os.environ.get("COOC_BENCH_ANY_ORDER", "0") == "1")
     core.set_kernel_timing(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # the rank's own share of the frequencies (cooc_item_counts on 1/world of the log), timed
