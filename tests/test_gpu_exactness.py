@@ -168,5 +168,15 @@ def test_c5_topk_benched_share_vs_oracle(pkg, oracle, torch_cuda):
     print(f"largest score difference {worst:.3g} (bound {atol:.3g})")
     print(f"checked {len(rows)} heaps ({len(nan_root)} with a NaN root) over {int(rp[-1])} entries; "
           f"{exact} ({exact / len(rows):.1%}) identical bit for bit (layout and every score)")
+    # (kept where a GPU run collects its outputs, gpurun_out/, so the match rate survives a -q log)
+    import json
+    import os
+
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "c5_heap_match.json"), "w") as f:
+            json.dump({"heaps_checked": len(rows), "nan_root_heaps": len(nan_root), "entries": int(rp[-1]),
+                       "bit_identical": exact, "bit_identical_frac": exact / len(rows),
+                       "largest_score_difference": worst, "bound": atol}, f, indent=1)
     # the device log and glibc's differ by an ulp now and then; most heaps must still match exactly
     assert exact >= 0.9 * len(rows), f"only {exact} of {len(rows)} heaps match bit for bit"
