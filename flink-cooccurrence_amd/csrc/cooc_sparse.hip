@@ -74,6 +74,7 @@ constexpr int kSpWaves = kSpThreads / 64;
 constexpr int kTShift = COOC_SP_TSHIFT;
 constexpr int kTW = 1 << kTShift;  // dense tile width (16384: 64 KB of uint32 LDS counters)
 constexpr int kSpMaxTiles = 64;                        // per-row plans are 64-bit tile masks
+constexpr uint64_t kGatherFlag = 1;                    // in a row plan's hz[0] (tile 0's code slot, tile 0 dense)
 constexpr int kHashMax = 8192;                        // slots: keys + counts = the dense tile's 128 KB
 constexpr int kWStage = kHashMax / 2;                  // hash compaction: entries staged in LDS for 16-B stores
 constexpr int kHashMin = 1024;                         // one slot per thread at least
@@ -763,8 +764,10 @@ __global__ __launch_bounds__(256) void k_sp_plan(int32_t M, int32_t T, const int
           }
         }
         close();
-        if (T < 64 && (dn & 1ull) && __popcll(st) >= kGatherMinChunks) {  // gather mode (k_sp_main)
-          dn |= uint64_t(1) << 63;
+        if ((dn & 1ull) && __popcll(st) >= kGatherMinChunks) {  // gather mode (k_sp_main)
+          // the flag: bit 0 of tile 0's hash-size code, unused when tile 0 is dense (every bit of dn is a
+          // tile: a 64-tile universe, 1,032,193 to 1,048,576 columns, has one in bit 63)
+          h0 |= kGatherFlag;
           max_tail = uint64_t(float(W) * fmaxf(0.f, 1.f - gmass[0]));
           if (mid) {
             max_tail_mid = max_tail;
@@ -854,7 +857,7 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
       x.k1 = r0 + (r1 - r0) * (s + 1) / ns;
       x.row = a;
       x.kind = -2;
-      x.gslot = T < 64 ? int32_t(atomicAdd(ng, 1ull)) : -1;
+      x.gslot = int32_t(atomicAdd(ng, 1ull));
       queue[q + s] = x;
     }
   } else {
@@ -867,7 +870,7 @@ __global__ void k_sp_queue(const int32_t *__restrict__ order, const uint64_t *__
     x.hz[1] = hz[2 * a + 1];
     x.row = a;
     x.kind = -1;
-    x.gslot = (x.dn >> 63) & 1ull ? int32_t(atomicAdd(ng, 1ull)) : -1;
+    x.gslot = ((x.dn & 1ull) && (x.hz[0] & kGatherFlag)) ? int32_t(atomicAdd(ng, 1ull)) : -1;
     x.est = row_nnz[a];
     queue[n_split_work + (r - n_split)] = x;
   }
@@ -3180,7 +3183,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   // gather scratch (per launch): a bucket region per workgroup for the largest expected tail (+25%); a work item
   // whose exact tail is larger walks per chunk instead.  Skipped when memory is short.
   auto scratch = [&](int64_t max_tail, int64_t g, DevBuf &buf) -> int64_t {
-    if (max_tail <= 0 || T >= 64) return 0;
+    if (max_tail <= 0) return 0;
     const int64_t sc = std::min<int64_t>(kScrGroups, (max_tail + max_tail / 4 + 64 * T + 4096) / 4 + 1);
     const size_t need = sizeof(uint4) * size_t(g) * size_t(sc);
     size_t f0 = 0, t0 = 0;
@@ -3190,7 +3193,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   };
   const int64_t scr_cap = scratch(h_tot_->max_tail, grid, sp_scr_);
   const int64_t scr_cap_mid = n_mid > 0 ? scratch(h_tot_->max_tail_mid, grid_mid, sp_scr_mid_) : 0;
-  const int64_t n_gather = T < 64 ? h_tot_->n_gather_rows + h_tot_->n_split_work : 0;  // gather items (bound)
+  const int64_t n_gather = h_tot_->n_gather_rows + h_tot_->n_split_work;  // gather items (bound)
   // 8. output region: the expected entries plus slab slack, at most the exact bound
   size_t free_b = 0, total_b = 0;
   COOC_HIP_TRY(hipMemGetInfo(&free_b, &total_b));

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--planner", default="auto", help='CooccurrenceCore planner ("sort": every whole row through '
                     'the sort + segmented-reduce path)')
     ap.add_argument("--permute", action="store_true", help="item ids through datagen.c3_item_perm (not rank-ordered)")
+    ap.add_argument("--n-items", type=int, default=None, help="the universe passed to the core (default 1e6; "
+                    "larger: unused items at the top, more tiles)")
     ap.add_argument("--column-order", action="store_true", help="COOC_FLAG_COLUMN_ORDER (no frequency relabel)")
     args = ap.parse_args()
     import torch
@@ -46,7 +48,7 @@ def main():
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     P = datagen.c3_ordered_pairs(0, U)
-    M = datagen.C3_ITEMS
+    M = args.n_items or datagen.C3_ITEMS
     # COOC_BENCH_ANY_ORDER=1: COOC_FLAG_ANY_ORDER (rows in no particular order; A/B through the environment)
     any_order = os.environ.get("COOC_BENCH_ANY_ORDER", "0") == "1"
     core = pkg.CooccurrenceCore(n_items=M, device=0, planner=args.planner, column_order=args.column_order,

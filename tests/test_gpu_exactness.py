@@ -98,6 +98,24 @@ def test_c3_share_every_row_vs_closed_form_oracle(pkg, oracle, torch_cuda, share
     _compare(res, chk, cs, nnz, want, datagen.c3_ordered_pairs(0, U))
 
 
+def test_c3_64th_in_a_64_tile_universe(pkg, oracle, torch_cuda):
+    """n_items = 1,040,000 (the top 40,000 ids unused): 64 column tiles, every bit of a row plan's 64-bit
+    tile masks a tile -- the gather mode's flag lives outside them (it was bit 63 of the dense mask, which
+    turned gather mode off for 64-tile universes: 1.6x slower).  1/64 of C3, bit-exact against the closed form."""
+    torch = torch_cuda
+    from flink_cooccurrence_amd import datagen
+
+    U, M = datagen.C3_USERS // 64, 1_040_000
+    dev = torch.device("cuda", 0)
+    up_d, it_d = datagen.c3_users(0, U, device=dev)
+    res, chk, cs, nnz = _device_checks(pkg, torch, up_d, it_d, M, symmetry=True)
+    assert chk["asymmetric_entries"] == 0
+    up, it = up_d.cpu().numpy(), it_d.cpu().numpy()
+    del up_d, it_d
+    want = oracle.row_checksums(up, it, M, _threads())
+    _compare(res, chk, cs, nnz, want, datagen.c3_ordered_pairs(0, U))
+
+
 def _d2h(ptr, n, dtype, offset=0):
     import ctypes
 
