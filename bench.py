@@ -99,6 +99,24 @@ def source_digest() -> str:
     return h.hexdigest()[:16]
 
 
+def entries_read(res, M: int, k: int, sizes, scores):
+    """Entries k_rescore reads (cooc_stream.hip): every entry of a row, except that a row whose heap is full
+    with a NaN root stops after its first ceil(k / 64) * 64 entries (min 512)."""
+    import ctypes
+
+    import torch
+
+    nnz = np.zeros(M, np.int32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    if hip.hipMemcpy(nnz.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(res.row_nnz), ctypes.c_size_t(nnz.nbytes),
+                     ctypes.c_int(2)) != 0:
+        return None
+    first = min(512, (k + 63) // 64 * 64)
+    cut = ((sizes == k) & torch.isnan(scores[:, 0])).cpu().numpy()
+    n = nnz.astype(np.int64)
+    return int(np.where(cut, np.minimum(n, first), n).sum())
+
+
 def limiter(pmc: dict, traffic, k_ms: float):
     """What the PMC counters (profiles/pmc_<kernel>.json, collected by scripts/pmc_sparse.sh) say
     bounds the kernel: HBM when the measured HBM-side bytes run near the peak, LDS when the LDS is
@@ -388,20 +406,26 @@ def main():
         rs_stale = bool(pmc_rs) and pmc_rs.get("source_digest") != digest
         if rs_stale:
             pmc_rs = {"kernel": "k_rescore", "stale_source_digest": pmc_rs.get("source_digest")}
-        b_rs = 8.0 * D + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
+        # entries the kernel reads: a full heap whose root is NaN takes nothing more (score > NaN is false,
+        # ItemRowRescorer...java:218-222), so k_rescore stops such a row after its first ceil(k / 64) * 64
+        # entries; D_read counts what it does read (1 GPU: from the heaps and row lengths), not D
+        d_read = entries_read(res, M, args.topk, tk_sizes, tk_scores) if world == 1 else None
+        D_rs = d_read if d_read is not None else D
+        b_rs = 8.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
         a_rs = b_rs / (tk * 1e-3) / 1e9
         t_rs = pmc_rs.get("hbm_bytes_per_launch")
         out["roofline_rescore"] = {
             "bound": "hbm", "kernel": "k_col_terms+k_rescore", "achieved": a_rs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": a_rs / HBM_PEAK_GBPS, "traffic": t_rs, "kernel_ms": tk, "algorithmic_bytes_per_launch": b_rs,
-            "units_per_launch": {"entries": D, "rows": M, "topk": args.topk},
+            "units_per_launch": {"entries": D, "entries_read": d_read, "rows": M, "topk": args.topk},
             "traffic_gbps": (t_rs / (tk * 1e-3) / 1e9) if t_rs else None,
             "l2_hit_rate": pmc_rs.get("l2_hit_rate"), "wave_wait_frac": pmc_rs.get("wave_wait_frac"),
             "valu_busy": pmc_rs.get("valu_busy"), "limiter": limiter(pmc_rs, t_rs, tk),
             "pmc_source_digest": pmc_rs.get("source_digest") or pmc_rs.get("stale_source_digest"),
             "pmc_stale": rs_stale,
-            "note": "B = 8D + 20M + M(4 + 12k) + 32M per launch (entries streamed, row headers and sums, heaps, "
-                    "32-B column terms), over the HIP-event time of the rescoring call; the PMC (traffic, L2 hit) "
+            "note": "B = 8D_read + 20M + M(4 + 12k) + 32M per launch (entries read: rows behind a NaN heap root "
+                    "end early; row headers and sums, heaps, 32-B column terms), over the HIP-event time of the "
+                    "rescoring call; the PMC (traffic, L2 hit) "
                     "shows how far the column-term gathers (one cache line per missed sparse entry) inflate the "
                     "bytes actually fetched (DESIGN.md §4)",
         }

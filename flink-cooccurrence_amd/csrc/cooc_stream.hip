@@ -406,7 +406,7 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
                           const double *__restrict__ k11t,
                           const int64_t *__restrict__ obs, int32_t exact, unsigned long long *__restrict__ row_ctr,
                           int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
-                          double *__restrict__ out_score) {
+                          double *__restrict__ out_score, int32_t no_nan_exit, int32_t rbatch) {
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
   double *hs = smem + int64_t(wave) * (topk + 1);
@@ -419,8 +419,16 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
   double *tr2122 = tr12 + kRsK;
   const int64_t n_rows = n_rows_p[0];
   const int64_t observed = exact ? obs[1] : obs[0];
-  for (int64_t t = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 1ull)) : 0ll, 0, 64); t < n_rows;
-       t = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 1ull)) : 0ll, 0, 64)) {
+  // rows taken rbatch at a time from the counter (one atomic on one address per row costs more than a
+  // short row's scoring once NaN roots end rows early)
+  int64_t t_next = 0, t_end = 0;
+  for (;;) {
+    if (t_next == t_end) {
+      t_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, (unsigned long long)rbatch)) : 0ll, 0, 64);
+      t_end = t_next + rbatch;
+    }
+    const int64_t t = t_next++;
+    if (t >= n_rows) break;
     const int32_t a = rows ? rows[t] : int32_t(t);
     const RowTerms R(observed, rs_row_sum(grs, a, exact));
     const int64_t n = src.size(a);
@@ -433,9 +441,12 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (int64_t i0 = 0; i0 < n; i0 += kRsChunk) {
-      rs_score_chunk(src, rb, i0, n, R, exact, cterm, k11t, tr12, tr2122, rscore, rcol, rq);
-      for (int j = 0; j < kRsR && i0 + j * 64 < n; j++) {
+    // the first chunk only as many 64-entry steps as fill the heap: a NaN root can end the row there
+    const int64_t first = no_nan_exit ? kRsChunk : std::min<int64_t>(kRsChunk, (int64_t(topk) + 63) & ~int64_t(63));
+    for (int64_t i0 = 0, span = first; i0 < n; i0 += span, span = kRsChunk) {
+      const int64_t lim = std::min<int64_t>(n, i0 + span);
+      rs_score_chunk(src, rb, i0, lim, R, exact, cterm, k11t, tr12, tr2122, rscore, rcol, rq);
+      for (int j = 0; j < kRsR && i0 + j * 64 < lim; j++) {
         const int32_t c = rcol[j * 64 + lane];
         const double score = rscore[j * 64 + lane];
         uint64_t m = __ballot(c >= 0 && (size < topk || score > least));
@@ -454,6 +465,11 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      // a full heap whose root (the least score) is NaN takes nothing more: the offer is score > least
+      // (heap_update's test, IntDoublePriorityQueue.java:132-205), false against NaN, and nothing else
+      // moves the root -- the rest of the row cannot change the heap, so it is not read (the wrapped int
+      // views of a large window make nearly every root NaN)
+      if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
     }
     out_size[t] = size;
     for (int32_t i = lane; i < size; i += 64) {
@@ -782,6 +798,11 @@ Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_
   k_k11_terms<<<256, 256, 0, s>>>(obs, exact ? 1 : 0, k11t);
   const int waves = rescore_waves_per_block(topk);
   const size_t lds = rescore_lds_bytes(topk);
+  // COOC_RS_NO_NAN_EXIT=1: every entry scored even behind a NaN heap root (timing the full work; same output)
+  const char *nx = getenv("COOC_RS_NO_NAN_EXIT");
+  const int32_t no_nan_exit = (nx && nx[0] == '1') ? 1 : 0;
+  const char *rbs = getenv("COOC_RS_BATCH");  // rows per counter grab (A/B knob)
+  const int32_t rbatch = rbs ? std::max(1, atoi(rbs)) : 4;
   if (lds > 160 * 1024 - 256) return Status{1, "topk too large for the LDS heaps"};
   if (lds > 64 * 1024)
     COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore<Rows>),
@@ -792,7 +813,7 @@ Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_
   const int64_t want = (max_rows + waves - 1) / waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
   k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), k11t, obs, exact ? 1 : 0,
-                                                 row_ctr, topk, out_size, out_val, out_score);
+                                                 row_ctr, topk, out_size, out_val, out_score, no_nan_exit, rbatch);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }
