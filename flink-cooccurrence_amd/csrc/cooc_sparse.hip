@@ -2101,7 +2101,7 @@ constexpr int kRadixBits = 7;
 
 // Stable LSD radix sort of k[0, n), n <= kSmallW, keys < 2^bits, kRadixBits per pass, ping-ponging between
 // k and t; returns the buffer that holds the sorted keys.  Wave w owns positions [w P, (w + 1) P),
-// P = kSmallW / kWaves, 64 at a time: a lane's rank among equal digits is the popcount of the ballot
+// P = 64 ceil(n / (64 kWaves)) <= kSmallW / kWaves, 64 at a time: a lane's rank among equal digits is the popcount of the ballot
 // match below it plus the wave's running count h[digit][w]; one exclusive scan over (digit, wave) turns
 // the counts into the scatter bases.  Four LDS accesses per key per pass.
 template <int kThreads>
@@ -2114,7 +2114,10 @@ __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uin
   static_assert(kE * 64 <= 512 && kRadixBits <= 7, "rank and digit pack into 16 bits");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t below_mask = (1ull << lane) - 1ull;
-  const uint32_t base = uint32_t(wave) * uint32_t(kE * 64);
+  // wave w ranks the span [w P, (w + 1) P) ∩ [0, n): P the smallest multiple of 64 that covers n with every
+  // wave (a row of 1,500 keys: 192 positions per wave, not 512 for the first three waves and none for the rest)
+  const uint32_t P = ((n + uint32_t(kWaves * 64) - 1u) / uint32_t(kWaves * 64)) * 64u;
+  const uint32_t base = uint32_t(wave) * P, lim = min(n, base + P);
   for (int sh = 0; sh < bits; sh += kRadixBits) {
     reinterpret_cast<uint32_t *>(h)[tid] = 0u;
     __syncthreads();
@@ -2124,9 +2127,9 @@ __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uin
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const uint32_t p0 = base + uint32_t(e) * 64u;
-      if (p0 >= n) continue;  // (wave-uniform)
+      if (p0 >= lim) continue;  // (wave-uniform)
       const uint32_t p = p0 + uint32_t(lane);
-      const bool v = p < n;
+      const bool v = p < lim;
       const uint32_t d = v ? (k[p] >> sh) & uint32_t(kD - 1) : 0u;
       uint64_t m = __ballot(v);
 #pragma unroll
@@ -2156,7 +2159,7 @@ __device__ uint32_t *block_radix_sort(uint32_t *k, uint32_t *t, uint16_t *h, uin
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const uint32_t p = base + uint32_t(e) * 64u + uint32_t(lane);
-      if (p >= n) continue;
+      if (p >= lim) continue;
       const uint32_t x = (pk[e / 2] >> ((e & 1) * 16)) & 0xffffu, d = x >> 9;
       t[uint32_t(h[d * kWaves + uint32_t(wave)]) + (x & 511u)] = k[p];
     }
