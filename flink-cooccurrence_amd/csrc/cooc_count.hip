@@ -15,6 +15,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "cooc_device.h"
+#include "cooc_scan.h"
 
 namespace cooc {
 
@@ -546,11 +547,11 @@ __host__ __device__ inline int32_t inv_perm_rows(int32_t k, int32_t M, int32_t W
   return o + (k - owner_rows_before(o, M, W)) * W;
 }
 
-struct PermCount {  // row count of the k-th row in owner-major order
+struct PermCount {  // row count of the k-th row in owner-major order (a launch_scan input)
   const int32_t *rcnt;
   int32_t M, W;
-  __host__ __device__ int64_t operator()(int32_t k) const {
-    return int64_t(rcnt[W == 1 ? k : inv_perm_rows(k, M, W)]);
+  __device__ int64_t operator()(int64_t k) const {
+    return int64_t(rcnt[W == 1 ? int32_t(k) : inv_perm_rows(int32_t(k), M, W)]);
   }
 };
 
@@ -1115,7 +1116,7 @@ void Counter::release() {
                    &order_, &ord_nch_, &ord_cbase_, &row_base_, &split_slot_, &split_row_, &chunks_, &tot_, &queue_,
                    &col_, &cnt_, &staging_, &row_nnz_, &rowsum_, &pk_row_ptr_, &pk_col_, &pk_cnt_,
                    &split_sum_, &tarena_, &bump_, &seg_off_, &plen_, &poff_, &send_, &witems_, &sp_arena_, &sp_arena0_, &sp_defer_, &sr_keys_, &sr_ukeys_, &sr_ucnt_, &sr_aux_, &sp_tb_,
-                   &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_, &sp_pbase_, &sp_scr_, &sp_scr_mid_, &sp_hz_, &sp_spre_};
+                   &sp_roww_, &sp_pstart_, &sp_pdense_, &sp_est_, &sp_queue_, &sp_ownc_, &sp_ownoff_, &sp_pbase_, &sp_scr_, &sp_scr_mid_, &sp_hz_, &sp_spre_, &scan_state_, &sp_ulen_};
   for (DevBuf *b : all) b->release();
   if (h_tot_) (void)hipHostFree(h_tot_);
   h_tot_ = nullptr;
@@ -1202,20 +1203,11 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
     k_batch_users<<<blocks_for(U, 256), 256, 0, s>>>(U, up, old, plen, tot);
     COOC_HIP_TRY(hipGetLastError());
   }
-  // row counts in owner-major order -> row_ptr (prefix); the identity order when W == 1
-  hipcub::CountingInputIterator<int32_t> rows(0);
-  hipcub::TransformInputIterator<int64_t, PermCount, hipcub::CountingInputIterator<int32_t>> cnt_perm(
-      rows, PermCount{rcnt, M, W});
-  size_t tmp = 0, q = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, poff + 1, int(U1), s));
-  tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, cnt_perm, row_ptr + 1, M, s));
-  tmp = std::max(tmp, q);
-  COOC_TRY(sort_tmp_.reserve(tmp));
-  if (U > 0) {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, poff + 1, int(U), s));
-  }
+  // prefix sums (cooc_scan.h): the users' padded lengths -> poff; row counts in owner-major order -> row_ptr
+  // (the identity order when W == 1)
+  COOC_TRY(scan_state_.reserve(sizeof(unsigned long long) * size_t(scan_state_words(std::max<int64_t>(U1, M)))));
+  unsigned long long *scan_st = scan_state_.as<unsigned long long>();
+  if (U > 0) COOC_TRY(launch_scan<true>(ScanI64{plen}, poff + 1, U, scan_st, &tot->err, s));
   // padded arena: every list 16-B aligned and padded to 8 ids with the sink id M; one pad group
   // at the end (never referenced by a segment, keeps the last 16-B load in bounds)
   const size_t lds_m = sizeof(uint32_t) * size_t(M);
@@ -1233,10 +1225,7 @@ Status Counter::plan_local(int64_t U, const int64_t *up, const int32_t *items, i
     COOC_HIP_TRY(hipMemsetAsync(rcnt, 0, sizeof(int32_t) * M, s));
   }
   COOC_HIP_TRY(hipGetLastError());
-  {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, cnt_perm, row_ptr + 1, M, s));
-  }
+  COOC_TRY(launch_scan<true>(PermCount{rcnt, M, W}, row_ptr + 1, M, scan_st, &tot->err, s));
   if (U > 0) {
     k_batch_scatter<<<B, kPlanThreads, lds_m, s>>>(n, B, up, items, uidx, poff, row_ptr, M, W, bh, old, desc);
     COOC_HIP_TRY(hipGetLastError());
@@ -1276,9 +1265,9 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
                                                             order_keys_.as<uint32_t>(), order_.as<int32_t>() + R1,
                                                             order_.as<int32_t>(), R1, 0, 32, s));
   tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, row_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1, R1, s));
-  tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
+  COOC_TRY(scan_state_.reserve(sizeof(unsigned long long) * size_t(scan_state_words(R1))));
+  unsigned long long *scan_st = scan_state_.as<unsigned long long>();
   // chunk plan: rows by contribution count, heaviest first
   int32_t *order = order_.as<int32_t>();
   if (R > 0) {
@@ -1291,12 +1280,9 @@ Status Counter::accumulate_rows(int32_t R, int32_t W, int32_t part, const int64_
     k_gather_i32<<<blocks_for(R, 256), 256, 0, s>>>(order, row_nch_.as<int32_t>(), R, ord_nch_.as<int32_t>());
   }
   if (R > 0) {
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>() + 1,
-                                                  R, s));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, row_split_.as<int32_t>(),
-                                                  split_slot_.as<int32_t>() + 1, R, s));
+    COOC_TRY(launch_scan<true>(ScanI32{ord_nch_.as<int32_t>()}, ord_cbase_.as<int32_t>() + 1, R, scan_st, &tot->err, s));
+    COOC_TRY(launch_scan<true>(ScanI32{row_split_.as<int32_t>()}, split_slot_.as<int32_t>() + 1, R, scan_st, &tot->err,
+                               s));
     k_split_rows<<<blocks_for(R, 256), 256, 0, s>>>(row_split_.as<int32_t>(), split_slot_.as<int32_t>(), R,
                                                     split_row_.as<int32_t>());
   }

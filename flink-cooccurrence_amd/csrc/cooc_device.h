@@ -243,6 +243,8 @@ class Counter {
   // large-universe path: tile-grouped arena, tile starts, per-row work and plan, estimates, queue
   DevBuf sp_arena_, sp_tb_, sp_roww_, sp_pstart_, sp_pdense_, sp_est_, sp_queue_, sp_ownc_, sp_ownoff_, sp_pbase_, sp_scr_, sp_hz_;
   DevBuf sp_spre_;  // streaming windows: prefix of the contributions' self flags
+  DevBuf sp_ulen_;     // the lists' lengths (u32) for the pair-work prefix
+  DevBuf scan_state_;  // the planner prefix sums' tile statuses (cooc_scan.h)
   DevBuf sp_arena0_;  // the lists' tile-0 ids as u16 (arena0; sp_arena_ holds the rest)
   // sort + segmented-reduce path of deferred rows: the deferred list, keys (x2), runs, per-batch tables
   DevBuf sp_defer_, sr_keys_, sr_ukeys_, sr_ucnt_, sr_aux_;

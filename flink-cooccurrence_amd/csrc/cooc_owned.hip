@@ -9,6 +9,7 @@
 
 #include "cooc_comm.h"
 #include "cooc_ctx.h"
+#include "cooc_scan.h"
 #include "cooc_stream_kernels.h"
 
 using cooc::Status;
@@ -125,13 +126,14 @@ Status cooc_ctx::count_owned(int64_t n_users, const int64_t *d_up, const int32_t
   COOC_TRY(C.alltoallv(lens, zero.data(), my_u.data(), lens_all, u_off.data(), u_bytes.data(), s));
   COOC_TRY(C.alltoallv(d_items, zero.data(), my_n.data(), it_all, n_off.data(), n_bytes.data(), s));
   COOC_HIP_TRY(hipMemsetAsync(up_all, 0, sizeof(int64_t), s));
-  if (U_all > 0) {
-    size_t b = 0;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, lens_all, up_all + 1, int(U_all), s));
-    COOC_TRY(own_tmp.reserve(std::max(b, tmp)));
-    b = own_tmp.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(own_tmp.p, b, lens_all, up_all + 1, int(U_all), s));
-  }
+  // the gathered lengths' prefix (cooc_scan.h; own_tmp holds the tile statuses and, after them, the error word)
+  const int64_t scan_words = cooc::scan_state_words(std::max<int64_t>(U_all, 1));
+  COOC_TRY(own_tmp.reserve(sizeof(unsigned long long) * size_t(scan_words + 1)));
+  int64_t *scan_err = reinterpret_cast<int64_t *>(own_tmp.as<unsigned long long>() + scan_words);
+  COOC_HIP_TRY(hipMemsetAsync(scan_err, 0, sizeof(int64_t), s));
+  COOC_TRY(cooc::launch_scan<true>(cooc::ScanI64{lens_all}, up_all + 1, U_all, own_tmp.as<unsigned long long>(), scan_err, s));
+  int64_t h_scan_err = 0;
+  COOC_HIP_TRY(hipMemcpyAsync(&h_scan_err, scan_err, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   // (4) the owned rows over every user
   COOC_TRY(count_device_owned(U_all, up_all, it_all, N_all, owner, me, counts, N_all, s, out));
   // (5) the job's ordered pairs
@@ -142,6 +144,7 @@ Status cooc_ctx::count_owned(int64_t n_users, const int64_t *d_up, const int32_t
   int64_t obs_all = 0;
   COOC_HIP_TRY(hipMemcpyAsync(&obs_all, own_obs.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (h_scan_err & 8) return Status{COOC_ERR_STATE, "internal bounds check failed (gathered history prefix)"};
   info->part = me;
   info->n_parts = W;
   info->observed = obs_all;

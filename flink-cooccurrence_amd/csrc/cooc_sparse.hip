@@ -37,6 +37,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "cooc_device.h"
+#include "cooc_scan.h"
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -627,9 +628,6 @@ __global__ void k_relabel_hot(const int32_t *__restrict__ hot_col, const uint64_
   freq_col[c] = int64_t(freq_by_id[a]);
 }
 
-struct WidenCount {
-  __host__ __device__ int64_t operator()(int32_t v) const { return int64_t(v); }
-};
 
 __global__ void k_sp_row_ptr(const uint32_t *__restrict__ keys, int64_t n, int32_t M, int64_t *__restrict__ row_ptr) {
   const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -647,8 +645,25 @@ struct UserLen {  // list length of a contribution's list
   __host__ __device__ int64_t operator()(uint32_t u) const { return up[(u & kListMask) + 1] - up[u & kListMask]; }
 };
 
+struct ScanUserLen {  // the pair work of contribution i (its list's length, from the u32 table), for launch_scan
+  const uint32_t *vals;
+  const uint32_t *len;
+  __device__ int64_t operator()(int64_t i) const { return int64_t(len[vals[i] & kListMask]); }
+};
+
+// the lists' lengths as u32 (one 4-B gather per contribution in the pair-work prefix instead of two 8-B ones
+// from the CSR pointers: a 5-MB table at the 1/8 C3 share)
+__global__ void k_list_len32(int64_t U, const int64_t *__restrict__ up, uint32_t *__restrict__ len) {
+  const int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (u < U) len[u] = uint32_t(up[u + 1] - up[u]);
+}
+
 struct SelfFlag {  // 1 for a contribution whose walk includes its own position
   __host__ __device__ int64_t operator()(uint32_t u) const { return int64_t(u >> 31); }
+};
+struct ScanSelfFlag {  // SelfFlag of contribution i, for launch_scan
+  const uint32_t *vals;
+  __device__ int64_t operator()(int64_t i) const { return int64_t(vals[i] >> 31); }
 };
 
 // est[t][k] = sum over the columns b of tile t of 1 - exp(-2^(k/2) f_b / N); gmass[t] = tile t's
@@ -2909,6 +2924,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(sp_arena_.reserve(sizeof(uint4) * size_t(n_groups1)));   // arena1: lists padded to 4 ids
   COOC_TRY(sp_arena0_.reserve(sizeof(uint4) * size_t(n_groups0)));  // arena0: tile-0 ids padded to 8
   COOC_TRY(sp_pbase_.reserve(sizeof(uint64_t) * size_t(2 * U1 + 1)));  // packed region lengths, their prefix
+  COOC_TRY(sp_ulen_.reserve(sizeof(uint32_t) * size_t(U1)));  // list lengths (u32) for the pair-work prefix
   COOC_TRY(sp_tb_.reserve(sizeof(int32_t) * size_t(U1) * size_t(T + 2)));
   if (8 * n_groups0 > int64_t(INT32_MAX)) return Status{1, "more than 2^31 arena positions in one window"};
   COOC_TRY(epre_.reserve(sizeof(int64_t) * (n1 + 1)));
@@ -2940,19 +2956,19 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   size_t tmp = 0, q = 0;
   COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n1), 0, kb, s));
   tmp = std::max(tmp, q);
-  hipcub::TransformInputIterator<int64_t, UserLen, const uint32_t *> len_it(vals, UserLen{up});
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, len_it, epre + 1, int(n1), s));
-  tmp = std::max(tmp, q);
   COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, order_keys_.as<uint64_t>(),
                                                             order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
                                                             order_.as<int32_t>() + M, M, 0, 64, s));
   tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, q, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(), M, s));
-  tmp = std::max(tmp, q);
   uint64_t *plen = sp_pbase_.as<uint64_t>(), *pbase = plen + U1;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, q, plen, pbase + 1, int(U1), s));
-  tmp = std::max(tmp, q);
   COOC_TRY(sort_tmp_.reserve(tmp));
+  // the planner's prefix sums (cooc_scan.h): tile statuses for the largest of them, reserved once up front
+  COOC_TRY(scan_state_.reserve(sizeof(unsigned long long) *
+                               size_t(scan_state_words(std::max({n1, U1, int64_t(M), win ? win->n_contrib : int64_t(0)})))));
+  unsigned long long *scan_st = scan_state_.as<unsigned long long>();
+  int64_t *scan_err = &tot->err;
+  uint32_t *ulen = sp_ulen_.as<uint32_t>();
+  if (U > 0) k_list_len32<<<nblocks(U, 256), 256, 0, s>>>(U, up, ulen);
 
   const int64_t waves = std::min<int64_t>(std::max<int64_t>(U, 1), 65536);
   int32_t *hot_col = nullptr, *pos_of = nullptr;
@@ -2974,8 +2990,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       if (n > 0) {
         size_t b = sort_tmp_.cap;
         COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, kb, s));
-        b = sort_tmp_.cap;
-        COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, len_it, epre + 1, int(n), s));
+        COOC_TRY(launch_scan<true>(ScanUserLen{vals, ulen}, epre + 1, n, scan_st, scan_err, s));
       }
       k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
       sorted_early = true;
@@ -3043,19 +3058,13 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   if (U > 0) {
     k_sp_tile_counts<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, plen, owner, part,
                                                              sp_ownc_.as<int32_t>(), pos_of, hotbm, minebm);
-    size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, plen, pbase + 1, int(U), s));
+    COOC_TRY(launch_scan<true>(ScanU64{plen}, pbase + 1, U, scan_st, scan_err, s));
   }
   int64_t *ownoff = owner ? sp_ownoff_.as<int64_t>() : nullptr;
   if (owner) {  // owned contributions per user -> their offsets
     COOC_HIP_TRY(hipMemsetAsync(ownoff, 0, sizeof(int64_t), s));
     if (U > 0) {
-      hipcub::TransformInputIterator<int64_t, WidenCount, const int32_t *> oc(sp_ownc_.as<int32_t>(), WidenCount{});
-      size_t b = 0;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, oc, ownoff + 1, int(U), s));
-      COOC_TRY(sort_tmp_.reserve(std::max(b, tmp)));
-      b = sort_tmp_.cap;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, oc, ownoff + 1, int(U), s));
+      COOC_TRY(launch_scan<true>(ScanI32{sp_ownc_.as<int32_t>()}, ownoff + 1, U, scan_st, scan_err, s));
     }
   }
   if (U > 0) {
@@ -3082,8 +3091,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   if (n_c > 0 && !sorted_early) {
     size_t b = sort_tmp_.cap;
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n_c), 0, kb, s));
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, len_it, epre + 1, int(n_c), s));
+    COOC_TRY(launch_scan<true>(ScanUserLen{vals, ulen}, epre + 1, n_c, scan_st, scan_err, s));
   }
   int64_t *spre = nullptr;  // a window's self flags, prefix in row order
   if (win) {
@@ -3091,12 +3099,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     spre = sp_spre_.as<int64_t>();
     COOC_HIP_TRY(hipMemsetAsync(spre, 0, sizeof(int64_t), s));
     if (n_c > 0) {
-      hipcub::TransformInputIterator<int64_t, SelfFlag, const uint32_t *> sf(vals, SelfFlag{});
-      size_t b = 0;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, sf, spre + 1, int(n_c), s));
-      COOC_TRY(sort_tmp_.reserve(b));
-      b = sort_tmp_.cap;
-      COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(sort_tmp_.p, b, sf, spre + 1, int(n_c), s));
+      COOC_TRY(launch_scan<true>(ScanSelfFlag{vals}, spre + 1, n_c, scan_st, scan_err, s));
     }
   }
   SPT("sort+scan");
@@ -3119,6 +3122,7 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_HIP_TRY(hipMemcpyAsync(h_tot_, tot, sizeof(PlanTotals), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
   if (h_tot_->err & 1) return Status{1, "item id outside [0, n_items)"};
+  if (h_tot_->err & 8) return Status{2, "internal bounds check failed (planner prefix sum)"};
   const int64_t n_split = h_tot_->n_split;
   const int64_t n_work = h_tot_->n_chunks;
   const int64_t work_total = h_tot_->work_total, self_total = h_tot_->self_total;
@@ -3145,15 +3149,16 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_TRY(split_row_.reserve(sizeof(int32_t) * std::max<int64_t>(n_split, 1)));
   COOC_TRY(split_slot_.reserve(sizeof(int32_t) * M));
   {
+    // the keys are the rows' pair work, at most work_total: only its bits are sorted (C3's 1/8 share: 35 of 64,
+    // five 8-bit passes instead of eight; the same order)
     size_t b = sort_tmp_.cap;
+    const int wb = std::min(64, bits_for(work_total + 1));
     COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, order_keys_.as<uint64_t>(),
                                                               order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
-                                                              order_.as<int32_t>() + M, M, 0, 64, s));
+                                                              order_.as<int32_t>() + M, M, 0, wb, s));
     k_sp_gather_nwork<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, row_nch_.as<int32_t>(), M,
                                                       ord_nch_.as<int32_t>());
-    b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(sort_tmp_.p, b, ord_nch_.as<int32_t>(), ord_cbase_.as<int32_t>(),
-                                                  M, s));
+    COOC_TRY(launch_scan<false>(ScanI32{ord_nch_.as<int32_t>()}, ord_cbase_.as<int32_t>(), M, scan_st, scan_err, s));
     k_sp_queue<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, order_keys_.as<uint64_t>() + M,
                                               ord_cbase_.as<int32_t>(), gmass, row_ptr, sp_pstart_.as<uint64_t>(),
                                               sp_pdense_.as<uint64_t>(), sp_hz_.as<uint64_t>(), M, T, tot,

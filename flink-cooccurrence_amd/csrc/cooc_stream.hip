@@ -12,6 +12,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "cooc_stream_kernels.h"
+#include "cooc_scan.h"
 
 namespace cooc {
 namespace {
@@ -720,15 +721,13 @@ Status launch_pack_rows(hipStream_t s, int32_t M, const int64_t *base, const int
                         const uint32_t *cnt, DevBuf &rp, DevBuf &out_col, DevBuf &out_cnt, DevBuf &tmp, int64_t *total) {
   COOC_TRY(rp.reserve(sizeof(int64_t) * (size_t(M) + 1)));
   int64_t *d_rp = rp.as<int64_t>();
-  hipcub::TransformInputIterator<int64_t, WidenI64, const int32_t *> n64(nnz, WidenI64{});
-  size_t b = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, n64, d_rp + 1, M, s));
-  COOC_TRY(tmp.reserve(b));
-  b = tmp.cap;
+  COOC_TRY(tmp.reserve(scan_ws_bytes(M)));
   COOC_HIP_TRY(hipMemsetAsync(d_rp, 0, sizeof(int64_t), s));
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, n64, d_rp + 1, M, s));
+  int64_t serr = 0;
+  COOC_TRY(launch_scan_ws<true>(ScanI32{nnz}, d_rp + 1, M, tmp.as<unsigned long long>(), &serr, s));
   COOC_HIP_TRY(hipMemcpyAsync(total, d_rp + M, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (serr & 8) return Status{2, "internal bounds check failed (row prefix)"};
   COOC_TRY(out_col.reserve(sizeof(int32_t) * size_t(*total + 1)));
   COOC_TRY(out_cnt.reserve(sizeof(uint32_t) * size_t(*total + 1)));
   k_pack_rows<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
@@ -746,21 +745,20 @@ Status launch_user_cut(hipStream_t s, int64_t n_users, const int64_t *up, const 
   }
   // tmp = [capped lengths int64[n_users + 1] | scan workspace] (the scan is not in place)
   const size_t lens_bytes = (sizeof(int64_t) * size_t(n_users + 1) + 255) / 256 * 256;
-  size_t bytes = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, cut_ptr, cut_ptr + 1, int(n_users), s));
-  COOC_TRY(tmp.reserve(lens_bytes + bytes));
+  COOC_TRY(tmp.reserve(lens_bytes + scan_ws_bytes(n_users)));
   int64_t *lens = tmp.as<int64_t>();
   k_cut_lens<<<blocks_for(n_users, 256), 256, 0, s>>>(n_users, up, cut, lens);
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemsetAsync(cut_ptr, 0, sizeof(int64_t), s));
-  bytes = tmp.cap - lens_bytes;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(static_cast<char *>(tmp.p) + lens_bytes, bytes, lens + 1,
-                                                cut_ptr + 1, int(n_users), s));
+  int64_t serr = 0;
+  COOC_TRY(launch_scan_ws<true>(ScanI64{lens + 1}, cut_ptr + 1, n_users,
+                                reinterpret_cast<unsigned long long *>(static_cast<char *>(tmp.p) + lens_bytes), &serr, s));
   const int64_t waves = std::min<int64_t>(n_users, int64_t(1) << 16);
   k_cut_copy<<<blocks_for(waves * 64, 256), 256, 0, s>>>(n_users, up, items, cut_ptr, cut_items);
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipMemcpyAsync(n_cut, cut_ptr + n_users, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (serr & 8) return Status{2, "internal bounds check failed (capped list prefix)"};
   return Status::Ok();
 }
 
@@ -855,18 +853,16 @@ Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32
   int64_t *chunk_pre = g.chunk_pre.as<int64_t>();
   int32_t *chunks = reinterpret_cast<int32_t *>(chunk_pre + M + 1);
   COOC_HIP_TRY(hipMemsetAsync(newpre, 0, sizeof(int64_t), s));
+  int64_t serr = 0, serr2 = 0;
   if (nnz > 0) {
     k_gs_flags<<<blocks_for(nnz, 256), 256, 0, s>>>(M, nnz, drp, dcol, g.base.as<int64_t>(), g.len.as<int32_t>(),
                                                   g.col.as<int32_t>(), flag, opos);
-    hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> f64(flag, WidenLen{});
-    size_t b = 0;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, f64, newpre + 1, int(nnz), s));
-    COOC_TRY(tmp.reserve(b));
-    b = tmp.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, f64, newpre + 1, int(nnz), s));
+    COOC_TRY(tmp.reserve(scan_ws_bytes(nnz)));
+    COOC_TRY(launch_scan_ws<true>(ScanI32{flag}, newpre + 1, nnz, tmp.as<unsigned long long>(), &serr, s));
   }
   COOC_HIP_TRY(hipMemcpyAsync(new_cols, newpre + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (serr & 8) return Status{2, "internal bounds check failed (new-column prefix)"};
   // 2. room for the moved rows' new slabs (at most live + nnz entries): compact, then grow
   const int64_t need = g.live + nnz;
   if (g.bump + need > g.cap) {
@@ -878,14 +874,8 @@ Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32
                                                 g.bump_dev.as<unsigned long long>(), chunks);
   // 3. the moved rows' old entries in kGsChunk pieces, then every delta entry
   COOC_HIP_TRY(hipMemsetAsync(chunk_pre, 0, sizeof(int64_t), s));
-  {
-    hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> c64(chunks, WidenLen{});
-    size_t b = 0;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, c64, chunk_pre + 1, M, s));
-    COOC_TRY(tmp.reserve(b));
-    b = tmp.cap;
-    COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, c64, chunk_pre + 1, M, s));
-  }
+  COOC_TRY(tmp.reserve(scan_ws_bytes(M)));
+  COOC_TRY(launch_scan_ws<true>(ScanI32{chunks}, chunk_pre + 1, M, tmp.as<unsigned long long>(), &serr2, s));
   // (the chunk total is not read back: a fixed grid strides over chunk_pre[M] chunks)
   k_gs_move_all<<<2048, 256, 0, s>>>(M, chunk_pre, drp, dcol, dcnt, newpre, g.nbase.as<int64_t>(), g.base.as<int64_t>(),
                                     g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>());
@@ -898,6 +888,7 @@ Status launch_gs_merge(hipStream_t s, int32_t M, const int64_t *drp, const int32
   int64_t bump = 0;
   COOC_HIP_TRY(hipMemcpyAsync(&bump, g.bump_dev.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (serr2 & 8) return Status{2, "internal bounds check failed (moved-chunk prefix)"};
   g.bump = bump;
   g.live += *new_cols;
   return Status::Ok();
@@ -910,18 +901,20 @@ Status compact_global(hipStream_t s, int32_t M, GlobalSparse &g, DevBuf &tmp, in
   COOC_TRY(g.nbase.reserve(sizeof(int64_t) * size_t(M + 1)));
   int64_t *nb = g.nbase.as<int64_t>();
   COOC_HIP_TRY(hipMemsetAsync(nb, 0, sizeof(int64_t), s));
-  hipcub::TransformInputIterator<int64_t, WidenLen, const int32_t *> l64(g.len.as<int32_t>(), WidenLen{});
-  size_t b = 0;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b, l64, nb + 1, M, s));
-  COOC_TRY(tmp.reserve(b));
-  b = tmp.cap;
-  COOC_HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, b, l64, nb + 1, M, s));
+  COOC_TRY(tmp.reserve(scan_ws_bytes(M)));
+  int64_t serr = 0;
+  COOC_TRY(launch_scan_ws<true>(ScanI32{g.len.as<int32_t>()}, nb + 1, M, tmp.as<unsigned long long>(), &serr, s));
   if (g.col.p)
     k_gs_compact<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
         M, nb, g.base.as<int64_t>(), g.len.as<int32_t>(), g.col.as<int32_t>(), g.cnt.as<uint32_t>(), col2.as<int32_t>(),
         cnt2.as<uint32_t>());
   COOC_HIP_TRY(hipGetLastError());
   COOC_HIP_TRY(hipStreamSynchronize(s));
+  if (serr & 8) {
+    col2.release();
+    cnt2.release();
+    return Status{2, "internal bounds check failed (row slab prefix)"};
+  }
   g.col.release();
   g.cnt.release();
   g.col = col2;
