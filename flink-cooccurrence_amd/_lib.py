@@ -152,7 +152,8 @@ _SIGS = {
     "cooc_count_owned_host": (ctypes.c_int, [vp, ctypes.c_int64, i64p, i32p, ctypes.POINTER(CoocOwnedInfo),
                                              ctypes.POINTER(CoocWindowInfo)]),
     "cooc_topk_owned_host": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
-    "cooc_copy_topk_batch_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, i32p, i32p, f64p]),
+    "cooc_copy_topk_batch_range": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p, i32p,
+                                                  f64p]),
     "cooc_comm_allgather_i64": (ctypes.c_int, [vp, ctypes.c_int64, i64p]),
     "cooc_snake_owner": (ctypes.c_int, [i64p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p]),
     "cooc_shard_plan": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp,
@@ -168,6 +169,7 @@ _SIGS = {
     "cooc_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int32]),
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
     "cooc_last_sort_rows": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "cooc_selftest_scan": (ctypes.c_int, [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), vp]),
 }
 
 _lib = None

@@ -398,8 +398,8 @@ class CooccurrenceCore:
         """cooc_copy_topk_batch_range: (sizes [n], values [n, k], scores [n, k]) of rows [r0, r1)."""
         n = int(r1) - int(r0)
         sizes, vals, scores = np.zeros(n, np.int32), np.zeros((n, topk), np.int32), np.zeros((n, topk), np.float64)
-        check(_lib.load().cooc_copy_topk_batch_range(self._h, int(r0), int(r1), _p(sizes, i32p), _p(vals, i32p),
-                                                     _p(scores, f64p)), self._h)
+        check(_lib.load().cooc_copy_topk_batch_range(self._h, int(r0), int(r1), int(topk), _p(sizes, i32p),
+                                                     _p(vals, i32p), _p(scores, f64p)), self._h)
         return sizes, vals, scores
 
     def comm_allgather_i64(self, value: int) -> np.ndarray:

@@ -11,6 +11,10 @@
 
 using cooc::Status;
 
+namespace cooc {
+Status selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, hipStream_t s, int64_t *h_err);  // cooc_verify.hip
+}
+
 namespace {
 
 int fail(cooc_ctx *ctx, const Status &s) {
@@ -179,11 +183,11 @@ int cooc_copy_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int
   });
 }
 
-int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *sizes, int32_t *values,
-                               double *scores) {
+int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t topk, int32_t *sizes,
+                               int32_t *values, double *scores) {
   return guarded(ctx, [&]() -> int {
     if (!ctx) return COOC_ERR_ARG;
-    Status s = ctx->copy_topk_batch_range(row_begin, row_end, sizes, values, scores);
+    Status s = ctx->copy_topk_batch_range(row_begin, row_end, topk, sizes, values, scores);
     return s.ok() ? COOC_OK : fail(ctx, s);
   });
 }
@@ -566,6 +570,16 @@ int cooc_verify_batch(cooc_ctx *ctx, int32_t flags, uint64_t *d_row_checksum, in
     if (flags & ~COOC_VERIFY_SYMMETRY) return fail(ctx, COOC_ERR_ARG, "unknown cooc_verify_batch flags");
     Status s = ctx->verify_batch(flags, d_row_checksum, out8, static_cast<hipStream_t>(hip_stream));
     return s.ok() ? COOC_OK : fail(ctx, s);
+  });
+}
+
+int cooc_selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, int64_t *diag, void *hip_stream) {
+  return guarded(nullptr, [&]() -> int {
+    if (!d_in || !d_out || n < 0 || (flags & ~15)) return COOC_ERR_ARG;
+    int64_t e = 0;
+    Status s = cooc::selftest_scan(d_in, d_out, n, flags, static_cast<hipStream_t>(hip_stream), &e);
+    if (diag) *diag = e;
+    return s.ok() ? COOC_OK : fail(nullptr, s);
   });
 }
 

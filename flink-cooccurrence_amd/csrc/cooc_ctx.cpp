@@ -299,8 +299,11 @@ Status cooc_ctx::copy_batch_range(int32_t r0, int32_t r1, int64_t cap, int32_t *
   return Status::Ok();
 }
 
-Status cooc_ctx::copy_topk_batch_range(int32_t r0, int32_t r1, int32_t *sizes, int32_t *values, double *scores) {
+Status cooc_ctx::copy_topk_batch_range(int32_t r0, int32_t r1, int32_t topk, int32_t *sizes, int32_t *values,
+                                       double *scores) {
   if (batch_topk <= 0) return Status{COOC_ERR_STATE, "cooc_topk_batch has not run"};
+  if (topk != batch_topk)  // the caller's buffers hold topk entries per row
+    return Status{COOC_ERR_ARG, "topk " + std::to_string(topk) + " != the scored top-k " + std::to_string(batch_topk)};
   const int32_t M = cfg.n_items;
   if (r0 < 0 || r1 > M || r0 > r1) return Status{COOC_ERR_ARG, "bad row range"};
   COOC_HIP_TRY(hipSetDevice(device));

@@ -113,14 +113,20 @@ class Operator {
                           int64_t *n_late);
   Status process_watermark(cooc_ctx &ctx, int64_t watermark, int32_t *fired, cooc_window_info *info);
 
-  int64_t watermark = INT64_MIN;  // timerService.currentWatermark()
+  int64_t watermark = INT64_MIN;  // timerService.currentWatermark() (this subtask's own)
   int64_t late_elements = 0;      // UserInteractionCounterLateElements
 
  private:
   struct Pending {
     std::vector<int32_t> users, items;
   };
+  Status fire(cooc_ctx &ctx, int64_t max_ts, bool mine, int32_t *fired, cooc_window_info *info);
   std::map<int64_t, Pending> pending_;  // window.maxTimestamp() -> buffered interactions
+  // p > 1: the watermark every subtask has passed (the minimum of their watermarks at the last agreement
+  // step; identical on every subtask), and whether the last step fired a window (then the next call runs
+  // another step whatever its watermark, so that every subtask runs the same sequence of collectives)
+  int64_t agreed_ = INT64_MIN;
+  bool regather_ = false;
 };
 
 }  // namespace cooc
@@ -150,7 +156,8 @@ struct cooc_ctx {
   cooc::Status copy_topk_batch(int32_t *sizes, int32_t *values, double *scores);
   // row ranges of the batch result / its top-k (a JVM operator's copy-out: no single Java array holds a C3 share)
   cooc::Status copy_batch_range(int32_t r0, int32_t r1, int64_t cap, int32_t *cols, uint32_t *cnt, int16_t *cnt16);
-  cooc::Status copy_topk_batch_range(int32_t r0, int32_t r1, int32_t *sizes, int32_t *values, double *scores);
+  cooc::Status copy_topk_batch_range(int32_t r0, int32_t r1, int32_t topk, int32_t *sizes, int32_t *values,
+                                     double *scores);
   cooc::Status topk_owned_host(int32_t topk, int32_t flags);
   cooc::Status comm_allgather_i64(int64_t value, int64_t *out);
   // cooc_verify_batch: invariant checks + row fingerprints of the last batch result

@@ -7,8 +7,9 @@
 // tile's exclusive prefix.  A tile's status is one 64-bit word, (value << 2) | flag (1: the tile's own
 // sum, 2: the inclusive prefix through the tile), so value and flag travel together and relaxed
 // agent-scope atomics suffice.  Values must stay below 2^62 (the planner's prefixes: pair work < n^2 with
-// n < 2^31 contributions).  A look-back that sees no progress for ~2^24 polls gives up and sets bit 8 of
-// *err (COOC_ERR_STATE, "internal bounds check"), so a lost update can never hang the GPU.
+// n < 2^31 contributions).  A look-back that sees no progress for ~2^24 polls stops waiting and sums the
+// tile's prefix straight from the input (exact; it sets bit 16 of *err as a diagnostic, not an error), so a lost
+// update can neither hang the GPU nor hand a partial prefix to the kernels that index with it.
 //
 // Replaces the library scans of the planner's timed path (row-order pair-work prefix `epre` over the
 // contributions, the packed region prefix over users, the work-item prefix over rows): the keyBy(itemA)
@@ -116,7 +117,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_lookback(In in, Out *__re
         const uint64_t upto = first2 >= 63 ? ~0ull : ((2ull << first2) - 1ull);
         if (m0 & upto) {  // a tile in between has not published its sum yet
           if (++polls > (1u << 24)) {
-            if (lane == 0) atomicOr(reinterpret_cast<unsigned long long *>(err), 8ull);
+            // no progress: the prefix is summed from the input itself (exact, slow, never the common case),
+            // so no kernel downstream ever sees a partial prefix, and nothing waits any longer
+            int64_t v = 0;
+            for (int64_t i = lane; i < base; i += 64) v += int64_t(in(i));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            excl = v;
+            if (lane == 0) atomicOr(reinterpret_cast<unsigned long long *>(err), 16ull);  // (diagnostic only)
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -178,17 +186,19 @@ struct ScanI32 {
 inline int64_t scan_state_words(int64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
 // out[0, n) = the inclusive (kIncl) or exclusive prefix of in; state holds scan_state_words(n) words.
+// blocked: 1 vectorised loads (the default), 0 striped through LDS, -1 the COOC_SCAN_BLOCKED knob.
 template <bool kIncl, class In, class Out>
-Status launch_scan(In in, Out *out, int64_t n, unsigned long long *state, int64_t *err, hipStream_t s) {
+Status launch_scan(In in, Out *out, int64_t n, unsigned long long *state, int64_t *err, hipStream_t s,
+                   int blocked = -1) {
   if (n <= 0) return Status::Ok();
   const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
   if (n_tiles > int64_t(INT32_MAX)) return Status{1, "prefix sum over more than 2^31 tiles"};
   COOC_HIP_TRY(hipMemsetAsync(state, 0, sizeof(unsigned long long) * size_t(n_tiles + 1), s));
-  static const bool blocked = [] {  // (A/B knob: COOC_SCAN_BLOCKED=0 stages the tile through LDS)
+  static const bool env_blocked = [] {  // (A/B knob: COOC_SCAN_BLOCKED=0 stages the tile through LDS)
     const char *e = getenv("COOC_SCAN_BLOCKED");
     return !(e && e[0] == '0');
   }();
-  if (blocked)
+  if (blocked < 0 ? env_blocked : blocked != 0)
     k_scan_lookback<kIncl, true, In, Out><<<unsigned(n_tiles), kScanThreads, 0, s>>>(in, out, n, state, n_tiles, err);
   else
     k_scan_lookback<kIncl, false, In, Out><<<unsigned(n_tiles), kScanThreads, 0, s>>>(in, out, n, state, n_tiles, err);

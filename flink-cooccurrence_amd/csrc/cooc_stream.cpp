@@ -731,25 +731,48 @@ Status Operator::process_elements(cooc_ctx &ctx, int64_t n, const int32_t *users
 Status Operator::process_watermark(cooc_ctx &ctx, int64_t wm, int32_t *fired, cooc_window_info *info) {
   if (wm > watermark) watermark = wm;
   *fired = 0;
-  auto it = pending_.begin();
   if (ctx.comm && ctx.comm->world() > 1) {
-    // p > 1 subtasks see the same watermarks; they fire the earliest window due on ANY of them, together (a
-    // subtask with no record in it joins the window's exchange with no user)
-    const int64_t mine = (it != pending_.end() && it->first <= watermark) ? it->first : INT64_MAX;
-    std::vector<int64_t> all(size_t(ctx.comm->world()));
-    COOC_TRY(ctx.comm_allgather_i64(mine, all.data()));
-    const int64_t due = *std::min_element(all.begin(), all.end());
-    if (due == INT64_MAX) return Status::Ok();
-    if (mine != due) {
-      COOC_TRY(ctx.stream_state.finish(ctx, due, info));
-      *fired = 1;
-      return Status::Ok();
+    // p > 1: Flink does not hand every subtask the same watermarks (each is the minimum over its own input
+    // channels, which arrive in their own order), so what fires is decided from all-gathered state only.  An
+    // agreement step all-gathers (this subtask's watermark, its earliest pending window); agreed_ becomes the
+    // minimum watermark -- every window ending at or before it is complete on every subtask, a record of it
+    // arriving later being late everywhere (:89-91) -- and the earliest pending window ending there fires on
+    // every subtask together (one without records in it joins with no user).  A subtask runs a step while its
+    // own watermark is ahead of agreed_ (it waits there for the others to catch up) and after a step that fired
+    // (more windows may be due): both conditions are functions of the all-gathered state and of watermarks that
+    // only grow, so every subtask runs the same sequence of collectives whatever order its watermarks came in.
+    const int world = ctx.comm->world();
+    std::vector<int64_t> all(static_cast<size_t>(world));
+    while (regather_ || watermark > agreed_) {
+      regather_ = false;
+      COOC_TRY(ctx.comm_allgather_i64(watermark, all.data()));
+      const int64_t wmin = *std::min_element(all.begin(), all.end());
+      const int64_t mine = pending_.empty() ? INT64_MAX : pending_.begin()->first;
+      COOC_TRY(ctx.comm_allgather_i64(mine, all.data()));
+      if (wmin > agreed_) agreed_ = wmin;
+      const int64_t due = *std::min_element(all.begin(), all.end());
+      if (due != INT64_MAX && due <= agreed_) {
+        regather_ = true;
+        return fire(ctx, due, mine == due, fired, info);
+      }
     }
+    return Status::Ok();
   }
+  auto it = pending_.begin();
   if (it == pending_.end() || it->first > watermark) return Status::Ok();
-  // onEventTime for every user of the window: group the buffered interactions by user, keeping
-  // each user's arrival order (windowState list order, :118).
-  const int64_t max_ts = it->first;
+  return fire(ctx, it->first, true, fired, info);
+}
+
+// onEventTime for every user of the window max_ts (mine: this subtask holds its records, the earliest pending
+// window; else it joins the p > 1 exchange with no user).
+Status Operator::fire(cooc_ctx &ctx, int64_t max_ts, bool mine, int32_t *fired, cooc_window_info *info) {
+  if (!mine) {
+    COOC_TRY(ctx.stream_state.finish(ctx, max_ts, info));
+    *fired = 1;
+    return Status::Ok();
+  }
+  // group the buffered interactions by user, keeping each user's arrival order (windowState list order, :118)
+  auto it = pending_.begin();
   Pending &p = it->second;
   std::unordered_map<int32_t, int32_t> idx;
   std::vector<int32_t> uids;

@@ -178,9 +178,60 @@ struct IsTouched {
 };
 
 // ---- LogLikelihood.java:41-61 (Java operation order, no contraction) -------------------------
+// Math.log (LogLikelihood.java:60) as Java's StrictMath.log pins it: fdlibm 5.3's __ieee754_log (Java's Math.log
+// may differ from it by at most one ulp; StrictMath.log is exactly this function).  x = 2^k (1 + f) with
+// sqrt(2)/2 <= 1 + f < sqrt(2), s = f / (2 + f), log(1 + f) = f - s (f - R(s^2)) with fdlibm's degree-14 Remez
+// polynomial (Lg1..Lg7), k ln2 as ln2_hi + ln2_lo, in fdlibm's operation order and without contraction, so the
+// device's scores equal the oracle's restatement (oracle/cooc_oracle.c, strict_log) bit for bit.
+__device__ inline double java_log(double x) {
+#pragma clang fp contract(off)
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                   two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                   Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                   Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+  uint64_t u = uint64_t(__double_as_longlong(x));
+  int32_t hx = int32_t(u >> 32);
+  int32_t k = 0;
+  if (hx < 0x00100000) {  // x < 2^-1022: zero, negative or subnormal
+    if (((hx & 0x7fffffff) | int32_t(uint32_t(u))) == 0) return -__builtin_inf();
+    if (hx < 0) return __builtin_nan("");
+    k -= 54;
+    u = uint64_t(__double_as_longlong(x * two54));
+    hx = int32_t(u >> 32);
+  }
+  if (hx >= 0x7ff00000) {
+    const double y = __longlong_as_double(int64_t(u));
+    return y + y;
+  }
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i0 = (hx + 0x95f64) & 0x100000;
+  u = (uint64_t(uint32_t(hx | (i0 ^ 0x3ff00000))) << 32) | (u & 0xffffffffull);  // x or x/2 into [sqrt2/2, sqrt2)
+  k += i0 >> 20;
+  const double f = __longlong_as_double(int64_t(u)) - 1.0;
+  const double dk = double(k);
+  if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20
+    if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+    const double R = f * f * (0.5 - 0.33333333333333333 * f);
+    return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const int32_t i = (hx - 0x6147a) | (0x6b851 - hx);
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  if (i > 0) {
+    const double hfsq = 0.5 * f * f;
+    return k == 0 ? f - (hfsq - s * (hfsq + R)) : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
 __device__ inline double xlogx(int64_t x) {
 #pragma clang fp contract(off)
-  return x == 0 ? 0.0 : double(x) * log(double(x));
+  return x == 0 ? 0.0 : double(x) * java_log(double(x));
 }
 
 __device__ inline double llr(int64_t k11, int64_t k12, int64_t k21, int64_t k22) {

@@ -14,6 +14,7 @@
 // that a test or the benchmark compares with an independent CPU restatement of the same rows
 // (oracle/cooc_oracle.c, oc_row_checksums) without copying the matrix out.
 #include "cooc_device.h"
+#include "cooc_scan.h"
 
 #include <algorithm>
 
@@ -178,6 +179,34 @@ Status launch_verify(hipStream_t s, int32_t M, const CountResult &r, bool symmet
   }
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
+}
+
+// The planner's device prefix sum (cooc_scan.h) on a caller's array, every variant the library uses: inclusive /
+// exclusive, vectorised or LDS-staged tiles, int64 / int32 input and output (cooc_selftest_scan).
+Status selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, hipStream_t s, int64_t *h_err) {
+  *h_err = 0;
+  if (n <= 0) return Status::Ok();
+  unsigned long long *ws = nullptr;
+  COOC_HIP_TRY(hipMalloc(&ws, scan_ws_bytes(n)));
+  const int blocked = (flags & 2) ? 0 : 1;
+  const bool incl = flags & 1, out32 = flags & 4, in32 = flags & 8;
+  int64_t *err = reinterpret_cast<int64_t *>(ws + scan_state_words(n));
+  Status st = Status::Ok();
+  if (hipMemsetAsync(err, 0, sizeof(int64_t), s) != hipSuccess) st = Status{3, "hipMemsetAsync"};
+  auto run = [&](auto in) {
+    if (!st.ok()) return;
+    if (incl && out32) st = launch_scan<true>(in, static_cast<int32_t *>(d_out), n, ws, err, s, blocked);
+    else if (incl) st = launch_scan<true>(in, static_cast<int64_t *>(d_out), n, ws, err, s, blocked);
+    else if (out32) st = launch_scan<false>(in, static_cast<int32_t *>(d_out), n, ws, err, s, blocked);
+    else st = launch_scan<false>(in, static_cast<int64_t *>(d_out), n, ws, err, s, blocked);
+  };
+  if (in32) run(ScanI32{static_cast<const int32_t *>(d_in)});
+  else run(ScanI64{static_cast<const int64_t *>(d_in)});
+  if (st.ok() && hipMemcpyAsync(h_err, err, sizeof(int64_t), hipMemcpyDeviceToHost, s) != hipSuccess)
+    st = Status{3, "hipMemcpyAsync"};
+  if (st.ok() && hipStreamSynchronize(s) != hipSuccess) st = Status{3, "hipStreamSynchronize"};
+  (void)hipFree(ws);
+  return st;
 }
 
 }  // namespace cooc

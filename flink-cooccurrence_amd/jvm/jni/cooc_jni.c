@@ -310,7 +310,7 @@ JNIEXPORT void JNICALL Java_com_github_uce_flinkcooccurrences_CoocNative_copyTop
   z.p = v.p = s.p = NULL;
   if (!scratch_get(env, &z, sizes, sizeof(jint), n, 0, 'I') && !scratch_get(env, &v, values, sizeof(jint), n * k, 0, 'I') &&
       !scratch_get(env, &s, scores, sizeof(jdouble), n * k, 0, 'D'))
-    check(env, H(h), cooc_copy_topk_batch_range(H(h), rowBegin, rowEnd, (int32_t *)z.p, (int32_t *)v.p, (double *)s.p));
+    check(env, H(h), cooc_copy_topk_batch_range(H(h), rowBegin, rowEnd, k, (int32_t *)z.p, (int32_t *)v.p, (double *)s.p));
   scratch_put(env, &s, 1, 'D', n * k);
   scratch_put(env, &v, 1, 'I', n * k);
   scratch_put(env, &z, 1, 'I', n);

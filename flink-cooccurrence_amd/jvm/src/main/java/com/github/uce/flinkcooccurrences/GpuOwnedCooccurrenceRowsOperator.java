@@ -2,6 +2,7 @@ package com.github.uce.flinkcooccurrences;
 
 import it.unimi.dsi.fastutil.ints.Int2ShortOpenHashMap;
 import java.util.concurrent.TimeUnit;
+import org.apache.flink.api.common.accumulators.IntCounter;
 import org.apache.flink.api.common.accumulators.LongCounter;
 import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple3;
@@ -41,6 +42,7 @@ public class GpuOwnedCooccurrenceRowsOperator
   private transient long handle;
   private transient OwnedExchange exchange;
   private transient CoocBatchReader reader;
+  private transient IntCounter lateElements;
   private transient LongCounter observedCooccurrences;
   private transient LongCounter rowSumCounter;
 
@@ -63,13 +65,16 @@ public class GpuOwnedCooccurrenceRowsOperator
     CoocNative.commInit(handle, commId, subtask, world);
     this.exchange = new OwnedExchange(handle, windowSizeMs, world);
     this.reader = new CoocBatchReader();
+    this.lateElements = getRuntimeContext().getIntCounter("UserInteractionCounterLateElements");
     this.observedCooccurrences = getRuntimeContext().getLongCounter("UserInteractionCounterObservedCooccurrences");
     this.rowSumCounter = getRuntimeContext().getLongCounter("RowSumProcessWindowRowSum");
   }
 
   @Override
   public void processElement(StreamRecord<Tuple3<Integer, Integer, Long>> element) throws Exception {
-    exchange.add(element.getValue().f0, element.getValue().f1, element.getTimestamp());
+    if (!exchange.add(element.getValue().f0, element.getValue().f1, element.getTimestamp())) {
+      lateElements.add(1);  // NonSampled...java:89-91
+    }
   }
 
   @Override

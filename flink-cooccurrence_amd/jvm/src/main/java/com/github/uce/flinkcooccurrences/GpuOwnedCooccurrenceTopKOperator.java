@@ -1,6 +1,7 @@
 package com.github.uce.flinkcooccurrences;
 
 import java.util.concurrent.TimeUnit;
+import org.apache.flink.api.common.accumulators.IntCounter;
 import org.apache.flink.api.common.accumulators.LongCounter;
 import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple3;
@@ -46,6 +47,7 @@ public class GpuOwnedCooccurrenceTopKOperator
   private transient IntDoublePriorityQueue topKReuse;
   private transient Tuple2<Integer, IntDoublePriorityQueue> itemTopKReuse;
   private transient StreamRecord<Tuple2<Integer, IntDoublePriorityQueue>> outputRecordReuse;
+  private transient IntCounter lateElements;
   private transient LongCounter observedCooccurrences;
   private transient LongCounter rescoredItems;
 
@@ -74,13 +76,16 @@ public class GpuOwnedCooccurrenceTopKOperator
     this.topKReuse = new IntDoublePriorityQueue(topK);
     this.itemTopKReuse = new Tuple2<>();
     this.outputRecordReuse = new StreamRecord<>(itemTopKReuse);
+    this.lateElements = getRuntimeContext().getIntCounter("UserInteractionCounterLateElements");
     this.observedCooccurrences = getRuntimeContext().getLongCounter("UserInteractionCounterObservedCooccurrences");
     this.rescoredItems = getRuntimeContext().getLongCounter("ItemRowRescorerRescoredItems");
   }
 
   @Override
   public void processElement(StreamRecord<Tuple3<Integer, Integer, Long>> element) throws Exception {
-    exchange.add(element.getValue().f0, element.getValue().f1, element.getTimestamp());
+    if (!exchange.add(element.getValue().f0, element.getValue().f1, element.getTimestamp())) {
+      lateElements.add(1);  // NonSampled...java:89-91
+    }
   }
 
   @Override

@@ -20,13 +20,22 @@ import java.util.Arrays;
  * GPUs of a node share one TaskManager host, so a node-local directory serves; a restarted attempt rendezvous
  * under its own attempt number with a fresh id.
  *
- * <p><b>One window, agreed.</b> Every subtask of a keyBy receives the same watermarks (each is the minimum over
- * the same input channels), so all subtasks cross the same window ends in the same order.  At every watermark
- * that passes a window end not yet checked, each subtask all-gathers its window start (Long.MIN_VALUE while it
- * holds no record) through the library's communicator (cooc_comm_allgather_i64); the window fires on EVERY
- * subtask once its end has passed -- a subtask without records joins the same collectives with an empty shard
- * -- and records of two different windows fail every subtask alike (IllegalStateException).  Multi-window
- * streams use the library's per-window exchange instead (GpuCooccurrenceJob.topKStreamOwned), which shares
+ * <p><b>Late records.</b> As in NonSampledUserInteractionCounterOneInputStreamOperator.processElement (:84-91), a
+ * record whose timestamp is at or below this subtask's current watermark is dropped and counted in the
+ * {@code UserInteractionCounterLateElements} accumulator ({@link #add} returns false); the watermark is the
+ * subtask's own, as the reference's timerService.currentWatermark() is.
+ *
+ * <p><b>One window, agreed.</b> Flink does not hand every subtask the same watermarks: each subtask's is the
+ * minimum over its own input channels, which arrive in their own order.  So what fires is decided from
+ * all-gathered state only.  An agreement step all-gathers (cooc_comm_allgather_i64) every subtask's watermark and
+ * window start (Long.MIN_VALUE while it holds no record); {@code agreed} becomes the minimum watermark -- a record
+ * of a window ending at or below it is late on every subtask -- and the window fires on EVERY subtask once its
+ * end is at or below {@code agreed} (a subtask without records joins the same collectives with an empty shard).
+ * A subtask runs steps while its own watermark is ahead of {@code agreed}, waiting in the collective for the
+ * others to catch up; both the condition and the outcome depend only on all-gathered values and on watermarks
+ * that only grow, so every subtask runs the same sequence of collectives.  Records of two different windows
+ * fail every subtask alike (IllegalStateException).  Multi-window streams use the library's per-window exchange
+ * instead (GpuCooccurrenceJob.topKStreamOwned, the same agreement inside cooc_op_process_watermark), which shares
  * {@link #rendezvous}.
  */
 final class OwnedExchange {
@@ -40,7 +49,8 @@ final class OwnedExchange {
   private int[] users = new int[1 << 16];
   private int[] items = new int[1 << 16];
   private long windowStart = Long.MIN_VALUE;
-  private long lastCheckedEnd = Long.MIN_VALUE;
+  private long watermark = Long.MIN_VALUE;  // this subtask's own (timerService.currentWatermark())
+  private long agreed = Long.MIN_VALUE;     // the minimum watermark over the subtasks at the last step
   private boolean fired;
 
   OwnedExchange(long handle, long windowSizeMs, int world) {
@@ -70,8 +80,15 @@ final class OwnedExchange {
     return Files.readAllBytes(path);
   }
 
-  /** processElement: the record joins the shard; it must fall in the shard's window (offset 0 tumbling). */
-  void add(int user, int item, long ts) {
+  /**
+   * processElement: false for a late record (ts at or below this subtask's watermark: dropped, the caller counts
+   * it, NonSampled...java:89-91); otherwise the record joins the shard, and it must fall in the shard's window
+   * (offset 0 tumbling).
+   */
+  boolean add(int user, int item, long ts) {
+    if (ts <= watermark) {
+      return false;
+    }
     final long start = ts - Math.floorMod(ts, windowSizeMs);
     if (windowStart == Long.MIN_VALUE) {
       windowStart = start;
@@ -85,38 +102,39 @@ final class OwnedExchange {
     users[buffered] = user;
     items[buffered] = item;
     buffered++;
+    return true;
   }
 
   /**
-   * processWatermark: the maxTimestamp of the window every subtask fires now, or Long.MIN_VALUE.  Collective:
-   * every subtask calls it with the same watermarks.
+   * processWatermark: the maxTimestamp of the window every subtask fires now, or Long.MIN_VALUE.  Collective (see
+   * the class comment): it may wait for the other subtasks' watermarks to catch up with this one.
    */
-  long fireAt(long watermark) {
-    if (fired) {
-      return Long.MIN_VALUE;
+  long fireAt(long mark) {
+    if (mark > watermark) {
+      watermark = mark;
     }
-    // the latest window end (start + size - 1) at or before the watermark; Long.MAX_VALUE ends a bounded input
-    final long end = watermark == Long.MAX_VALUE ? Long.MAX_VALUE
-        : watermark - Math.floorMod(watermark + 1, windowSizeMs);
-    if (end <= lastCheckedEnd) {
-      return Long.MIN_VALUE;
-    }
-    lastCheckedEnd = end;
-    long start = Long.MIN_VALUE;
-    for (long s : CoocNative.commAllGather(handle, windowStart, world)) {
-      if (s == Long.MIN_VALUE) {
-        continue;
+    while (!fired && watermark > agreed) {
+      long wmin = Long.MAX_VALUE;
+      for (long w : CoocNative.commAllGather(handle, watermark, world)) {
+        wmin = Math.min(wmin, w);
       }
-      if (start != Long.MIN_VALUE && s != start) {
-        throw new IllegalStateException("subtasks hold records of two windows: " + start + " and " + s);
+      long start = Long.MIN_VALUE;
+      for (long s : CoocNative.commAllGather(handle, windowStart, world)) {
+        if (s == Long.MIN_VALUE) {
+          continue;
+        }
+        if (start != Long.MIN_VALUE && s != start) {
+          throw new IllegalStateException("subtasks hold records of two windows: " + start + " and " + s);
+        }
+        start = s;
       }
-      start = s;
+      agreed = Math.max(agreed, wmin);
+      if (start != Long.MIN_VALUE && start + windowSizeMs - 1 <= agreed) {
+        fired = true;
+        return start + windowSizeMs - 1;
+      }
     }
-    if (start == Long.MIN_VALUE || start + windowSizeMs - 1 > watermark) {
-      return Long.MIN_VALUE;
-    }
-    fired = true;
-    return start + windowSizeMs - 1;
+    return Long.MIN_VALUE;
   }
 
   /** The shard as CSR (users ascending, each user's items in arrival order) through countOwned. */

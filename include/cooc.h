@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define COOC_ABI_VERSION 6
+#define COOC_ABI_VERSION 7
 
 #if defined(__GNUC__)
 #define COOC_API __attribute__((visibility("default")))
@@ -257,8 +257,9 @@ COOC_API int cooc_topk_items(cooc_ctx *ctx, int32_t k, int32_t flags, int32_t n,
  * its resident global rows and rescores them against the job's row sums.  The window's outputs on a rank
  * are its owned rows (every row of the job on exactly one rank); info->observed is this rank's users' pairs
  * (the ObservedCooccurrences accumulator; the ranks' values add up to the job's).  Every rank finishes the
- * same windows in the same order: cooc_op_process_watermark fires the earliest window due on ANY rank
- * (agreed by an all-gather), so a rank without records in it still joins. */
+ * same windows in the same order: cooc_op_process_watermark decides from all-gathered state only (the ranks'
+ * watermarks and earliest pending windows), so ranks that receive different watermark sequences still run the
+ * same collectives, and a rank without records in a window still joins it. */
 COOC_API int cooc_submit_batch(cooc_ctx *ctx, int64_t window_ts, int32_t n_users, const int32_t *user_ids,
                       const int64_t *user_ptr, const int32_t *items);
 COOC_API int cooc_finish_window(cooc_ctx *ctx, int64_t window_ts, cooc_window_info *info);
@@ -295,7 +296,11 @@ COOC_API int cooc_global_row(cooc_ctx *ctx, int32_t item, int32_t *cols, uint32_
  * cooc_op_process_watermark: advances the watermark and fires AT MOST ONE pending window with
  * maxTimestamp <= watermark (the earliest); sets *fired = 1 and fills *info if one fired (its
  * outputs are then readable with cooc_copy_window_*), *fired = 0 when nothing is due.  Callers
- * loop until *fired == 0, which mirrors the Flink timer service firing timers in timestamp order. */
+ * loop until *fired == 0, which mirrors the Flink timer service firing timers in timestamp order.
+ * With a communicator of world > 1 the call is collective and a window is due when its maxTimestamp is at or
+ * below the MINIMUM watermark over the ranks (agreed by an all-gather of the watermarks and of the earliest
+ * pending windows); a rank whose watermark is ahead of that minimum waits inside the call until the other
+ * ranks' watermarks catch up (every rank receives Long.MAX_VALUE at the end of a bounded input). */
 COOC_API int cooc_op_process_elements(cooc_ctx *ctx, int64_t n, const int32_t *users, const int32_t *items,
                              const int64_t *ts, int64_t *n_late);
 COOC_API int cooc_op_process_watermark(cooc_ctx *ctx, int64_t watermark, int32_t *fired, cooc_window_info *info);
@@ -395,9 +400,11 @@ COOC_API int cooc_topk_owned(cooc_ctx *ctx, int32_t topk, int32_t flags, int32_t
  * FlinkCooccurrences.java:162-167 (ItemRowRescorerTwoInputStreamOperator.java:195-226) for a one-window job. */
 COOC_API int cooc_topk_owned_host(cooc_ctx *ctx, int32_t topk, int32_t flags);
 /* Heaps of rows [row_begin, row_end) of the last cooc_topk_batch / cooc_topk_owned_host: sizes int32[n],
- * values int32[n*topk], scores double[n*topk] (n = row_end - row_begin, layout as cooc_copy_topk_batch). */
-COOC_API int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t *sizes,
-                                        int32_t *values, double *scores);
+ * values int32[n*topk], scores double[n*topk] (n = row_end - row_begin, layout as cooc_copy_topk_batch).  topk
+ * is the caller's buffer width and must equal the topk of that call: anything else is COOC_ERR_ARG and nothing
+ * is written (the buffers are sized from it). */
+COOC_API int cooc_copy_topk_batch_range(cooc_ctx *ctx, int32_t row_begin, int32_t row_end, int32_t topk,
+                                        int32_t *sizes, int32_t *values, double *scores);
 /* Every rank's `value` (collective over the communicator): out int64[world] in rank order.  The JVM operators
  * agree on the window they fire with it (a subtask with no records of its own joins the same window). */
 COOC_API int cooc_comm_allgather_i64(cooc_ctx *ctx, int64_t value, int64_t *out);
@@ -485,6 +492,13 @@ COOC_API int cooc_last_kernel_ms(cooc_ctx *ctx, float *accumulate_ms);
 /* Rows (and their ordered pairs) that the last large-universe count sent through the sort +
  * segmented-reduce path (hash table overflow, or COOC_FLAG_SORT_ROWS). */
 COOC_API int cooc_last_sort_rows(cooc_ctx *ctx, int64_t *rows, int64_t *pairs);
+/* Self-test of the planner's single-pass device prefix sum (no context): d_out[i] = d_in[0] + .. + d_in[i]
+ * (flags & 1) or + .. + d_in[i-1] over device arrays of n elements, on hip_stream (then synchronised).
+ * flags: 1 inclusive, 2 tiles staged through LDS (else vectorised loads), 4 int32 output (else int64), 8 int32
+ * input (else int64).  *diag (may be NULL) gets the scan's diagnostic word (bit 16: a look-back stopped waiting
+ * and summed its prefix from the input). */
+COOC_API int cooc_selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, int64_t *diag,
+                                void *hip_stream);
 
 #ifdef __cplusplus
 }

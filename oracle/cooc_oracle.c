@@ -162,8 +162,70 @@ static int32_t *rowmap_sorted_slots(const rowmap *r) {
 /* ------------------------------------------------------------------------------------------ */
 /* LogLikelihood.java:41-61 (9-log form).  Compiled with -ffp-contract=off: Java never fuses.  */
 /* ------------------------------------------------------------------------------------------ */
+/* Math.log as Java's StrictMath.log pins it: fdlibm 5.3's __ieee754_log (e_log.c; the JDK's StrictMath.log is
+ * that function, and Java's Math.log may differ from it by at most an ulp).  Third-party arithmetic, not in
+ * /root/reference: restated from fdlibm's published method -- x = 2^k (1 + f) with sqrt(2)/2 < 1 + f < sqrt(2),
+ * s = f / (2 + f), log(1 + f) = f - s (f - R(s^2)) with fdlibm's degree-14 Remez polynomial R (Lg1..Lg7), and
+ * k ln2 split in ln2_hi + ln2_lo -- in its operation order.  The device's rescoring kernel computes the same
+ * function (cooc_stream.hip, java_log), so every LLR score is reproducible bit for bit. */
+static double strict_log(double x) {
+  static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                      two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                      Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                      Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01,
+                      Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+  union { double d; uint64_t u; } v = {x};
+  int32_t hx = (int32_t)(v.u >> 32);
+  const uint32_t lx = (uint32_t)v.u;
+  int32_t k = 0;
+  if (hx < 0x00100000) {                           /* x < 2^-1022 */
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -INFINITY;  /* log(+-0) */
+    if (hx < 0) return NAN;                         /* log(negative) */
+    k -= 54;                                        /* subnormal: scale up */
+    v.d *= two54;
+    hx = (int32_t)(v.u >> 32);
+  }
+  if (hx >= 0x7ff00000) return v.d + v.d;          /* inf or NaN */
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i0 = (hx + 0x95f64) & 0x100000;
+  v.u = ((uint64_t)(uint32_t)(hx | (i0 ^ 0x3ff00000)) << 32) | (v.u & 0xffffffffu); /* x or x/2 into [sqrt2/2, sqrt2) */
+  k += i0 >> 20;
+  const double f = v.d - 1.0;
+  if ((0x000fffff & (2 + hx)) < 3) {               /* |f| < 2^-20 */
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      const double dk = (double)k;
+      return dk * ln2_hi + dk * ln2_lo;
+    }
+    const double R = f * f * (0.5 - 0.33333333333333333 * f);
+    if (k == 0) return f - R;
+    const double dk = (double)k;
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s;
+  int32_t i = hx - 0x6147a;
+  const double w = z * z;
+  const int32_t j = 0x6b851 - hx;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  i |= j;
+  const double R = t2 + t1;
+  if (i > 0) {
+    const double hfsq = 0.5 * f * f;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  if (k == 0) return f - s * (f - R);
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+EXPORT double oc_strict_log(double x) { return strict_log(x); }
+
 static double xlogx(int64_t x) { /* LogLikelihood.java:59-61 */
-  return x == 0 ? 0.0 : (double)x * log((double)x);
+  return x == 0 ? 0.0 : (double)x * strict_log((double)x);
 }
 
 EXPORT double oc_llr(int64_t k11, int64_t k12, int64_t k21, int64_t k22) {

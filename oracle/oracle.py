@@ -59,6 +59,7 @@ def lib():
     vp = ctypes.c_void_p
     sig = {
         "oc_llr": (ctypes.c_double, [ctypes.c_int64] * 4),
+        "oc_strict_log": (ctypes.c_double, [ctypes.c_double]),
         "oc_score_item": (ctypes.c_double, [ctypes.c_int16, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]),
         "oc_pq_create": (vp, [ctypes.c_int32]),
         "oc_pq_destroy": (None, [vp]),
@@ -119,6 +120,11 @@ def _p(a: np.ndarray, t):
 # ---------------------------------------------------------------------------------------------
 # LogLikelihood / IntDoublePriorityQueue / java.util.Random restatements
 # ---------------------------------------------------------------------------------------------
+def strict_log(x: float) -> float:
+    """Java's StrictMath.log (fdlibm 5.3 __ieee754_log), the log of the LLR restatement."""
+    return lib().oc_strict_log(x)
+
+
 def llr(k11: int, k12: int, k21: int, k22: int) -> float:
     """LogLikelihood.logLikelihoodRatio, LogLikelihood.java:41-57."""
     return lib().oc_llr(k11, k12, k21, k22)

@@ -5,9 +5,10 @@
 # (tests/test_stream_asan_gpu.py).  The release library is untouched.
 set -e
 cd "$(dirname "$0")/.."
-B=/tmp/cooc_asan_build
+B=$(mktemp -d "${TMPDIR:-/tmp}/cooc_asan_build.XXXXXX")  # per invocation: concurrent builds do not collide
+trap 'rm -rf "$B"' EXIT
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer -Xarch_host -g"
-rm -rf $B && mkdir -p $B/flink-cooccurrence_amd && cp -r flink-cooccurrence_amd/csrc $B/flink-cooccurrence_amd/ && cp -r include $B/ \
+mkdir -p $B/flink-cooccurrence_amd && cp -r flink-cooccurrence_amd/csrc $B/flink-cooccurrence_amd/ && cp -r include $B/ \
   && rm -f $B/flink-cooccurrence_amd/csrc/*.o $B/flink-cooccurrence_amd/csrc/*.so
 make -s -j${MAKE_JOBS:-8} -C $B/flink-cooccurrence_amd/csrc CXXFLAGS="-O2 -std=c++17 -fPIC -Wall -Wno-unused-result $SAN" \
   cooc_count.o cooc_sparse.o cooc_verify.o cooc_stream_k.o cooc_shard.o cooc_owned.o cooc_stream.o cooc_ctx.o \

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol(pkg):
     assert declared == _exported(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(L, name)
-    assert L.cooc_abi_version() == 6
+    assert L.cooc_abi_version() == 7
 
 
 def test_status_strings(pkg):

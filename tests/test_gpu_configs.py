@@ -35,9 +35,34 @@ def test_device_llr_known_answers(pkg, oracle, torch_cuda):
     # the reference's own tolerance (0.1) on its three cases ...
     assert got[:3] == pytest.approx([270.72, 263.90, 48.94], abs=0.1)
     assert got[3] == 0.0 and got[4] == 0.0 and got[5] > 0.0
-    # ... and the oracle's restatement (same operation order, contraction off) to a few ulp
+    # ... and the oracle's restatement bit for bit: the same operation order, contraction off, and the same log
+    # (Java's StrictMath.log, fdlibm's __ieee754_log, on both sides)
     want = np.array([oracle.llr(*map(int, r)) for r in k])
-    np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_device_llr_bit_exact_vs_oracle(pkg, oracle, torch_cuda):
+    """200,000 contingency tables spanning the rescorer's ranges (k11 from the int16 view, row sums up to the
+    int32 range, observed totals up to 3e11, negative cells from wrapped views -> NaN): the device LLR
+    (LogLikelihood.java:41-57 with fdlibm's log) equals the oracle's bit for bit, NaN where NaN."""
+    rng = np.random.default_rng(5)
+    n = 200_000
+    k11 = rng.integers(-32768, 32768, n)
+    k11[: n // 2] = rng.integers(0, 64, n // 2)  # (most entries: small counts)
+    rs_a = rng.integers(-(1 << 31), 1 << 31, n)
+    rs_b = rng.integers(-(1 << 31), 1 << 31, n)
+    rs_a[: n // 2] = np.abs(rs_a[: n // 2]) // 1024 + 64
+    rs_b[: n // 2] = np.abs(rs_b[: n // 2]) // 1024 + 64
+    obs = rng.integers(0, 3 * 10 ** 11, n)
+    k12, k21 = rs_a - k11, rs_b - k11
+    k = np.stack([k11, k12, k21, obs + k11 - k12 - k21], 1).astype(np.int64)
+    with pkg.CooccurrenceCore(n_items=10, device=0) as core:
+        got = core.llr(k)
+    want = np.array([oracle.llr(*map(int, r)) for r in k])
+    nan = np.isnan(want)
+    assert np.array_equal(np.isnan(got), nan) and nan.any() and (~nan).sum() > n // 2
+    bad = np.flatnonzero(got[~nan].view(np.uint64) != want[~nan].view(np.uint64))
+    assert len(bad) == 0, f"{len(bad)} scores differ, e.g. {got[~nan][bad[:3]]} vs {want[~nan][bad[:3]]}"
 
 
 def test_c1_full_size_vs_oracle_stream(pkg, oracle, torch_cuda):

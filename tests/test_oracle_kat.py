@@ -88,3 +88,24 @@ def test_pq_overflow_and_bad_size(oracle):
         q.add(2, 2.0)
     with pytest.raises(ValueError):
         oracle.PriorityQueue(0)
+
+
+def test_strict_log_is_fdlibm_within_an_ulp_of_libm(oracle):
+    """The restated fdlibm log (Java's StrictMath.log, the LLR's Math.log up to an ulp): within one ulp of the C
+    library's log everywhere it is finite, equal to it on the vast majority of inputs, IEEE special cases as Java
+    specifies them (log(0) = -inf, log(negative) = NaN, log(inf) = inf, log(1) = 0)."""
+    import math
+
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([np.arange(1, 20001, dtype=np.float64), rng.integers(1, 1 << 62, 20000).astype(np.float64),
+                         rng.random(20000) * 10, [5e-324, 1e-310, 0.5, 2.0, 10.0, 1 + 2 ** -30]])
+    n_diff = 0
+    for x in xs.tolist():
+        a, b = oracle.strict_log(x), math.log(x)
+        if a != b:
+            n_diff += 1
+            assert abs(a - b) <= math.ulp(b), (x, a, b)
+    assert n_diff < 0.05 * len(xs)
+    assert oracle.strict_log(0.0) == -math.inf and math.isnan(oracle.strict_log(-1.0))
+    assert oracle.strict_log(math.inf) == math.inf and oracle.strict_log(1.0) == 0.0
+    assert oracle.strict_log(2.0) == 0.6931471805599453 and oracle.strict_log(math.e) == 1.0

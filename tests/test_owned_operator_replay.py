@@ -68,16 +68,22 @@ def _records(up, it, seed=7):
 
 
 class _OwnedSubtask:
-    """The Java operators' state and calls (GpuOwnedCooccurrence{Rows,TopK}Operator) on one handle."""
+    """The Java operators' state and calls (GpuOwnedCooccurrence{Rows,TopK}Operator, OwnedExchange) on one
+    handle."""
 
     def __init__(self, core, n_items, topk):
         self.core, self.n_items, self.topk = core, n_items, topk
         self.users, self.items = [], []
         self.window_start = LONG_MIN
-        self.last_checked_end = LONG_MIN
+        self.watermark = LONG_MIN  # this subtask's own (timerService.currentWatermark())
+        self.agreed = LONG_MIN     # the minimum watermark over the subtasks at the last agreement step
         self.fired = False
+        self.late = 0              # UserInteractionCounterLateElements
 
     def process_element(self, user, item, ts):
+        if ts <= self.watermark:  # NonSampled...java:89-91: dropped and counted
+            self.late += 1
+            return
         start = ts - ts % WINDOW_MS
         if self.window_start == LONG_MIN:
             self.window_start = start
@@ -87,22 +93,20 @@ class _OwnedSubtask:
         self.items.append(item)
 
     def process_watermark(self, mark):
-        """-> the fired window's outputs, or None."""
-        if self.fired:
-            return None
-        # the latest window end (start + size - 1) <= mark (Long.MAX_VALUE, the end of a bounded input: any)
-        end = mark if mark == (1 << 63) - 1 else mark - (mark + 1) % WINDOW_MS
-        if end <= self.last_checked_end:
-            return None
-        self.last_checked_end = end
-        starts = self.core.comm_allgather_i64(self.window_start)  # (collective: every subtask calls it here)
-        known = sorted({int(s) for s in starts if s != LONG_MIN})
-        if len(known) > 1:
-            raise RuntimeError(f"subtasks hold records of different windows: {known}")
-        if not known or known[0] + WINDOW_MS - 1 > mark:
-            return None
-        self.fired = True
-        return self._fire(known[0] + WINDOW_MS - 1)
+        """-> the fired window's outputs, or None.  Collective: runs agreement steps while this subtask's
+        watermark is ahead of the agreed minimum (OwnedExchange.fireAt)."""
+        self.watermark = max(self.watermark, mark)
+        while not self.fired and self.watermark > self.agreed:
+            wmin = min(int(w) for w in self.core.comm_allgather_i64(self.watermark))
+            starts = self.core.comm_allgather_i64(self.window_start)
+            known = sorted({int(s) for s in starts if s != LONG_MIN})
+            if len(known) > 1:
+                raise RuntimeError(f"subtasks hold records of different windows: {known}")
+            self.agreed = max(self.agreed, wmin)
+            if known and known[0] + WINDOW_MS - 1 <= self.agreed:
+                self.fired = True
+                return self._fire(known[0] + WINDOW_MS - 1)
+        return None
 
     def _fire(self, timestamp):
         u = np.asarray(self.users, np.int64)
@@ -139,7 +143,26 @@ class _OwnedSubtask:
             for j in np.flatnonzero(sz):
                 heaps[r0 + int(j)] = (vals[j, :sz[j]].copy(), scores[j, :sz[j]].copy())
         return dict(timestamp=timestamp, rows=rows, rowsums=rowsums, heaps=heaps, observed=int(winfo.observed),
-                    job_observed=int(info.observed), n_ranges=n_ranges, order=self.core.column_order())
+                    job_observed=int(info.observed), n_ranges=n_ranges, order=self.core.column_order(),
+                    late=self.late)
+
+
+# the watermarks of the job; subtask 1 does not receive those at SKIPPED_BY_1 (Flink's per-subtask minimum over
+# its own input channels), so the two subtasks run process_watermark different numbers of times
+MARKS = [999, 4000, 4999, 5500, 5998, 5999, 7000, (1 << 63) - 1]
+SKIPPED_BY_1 = {1, 4, 6}
+
+
+def _late_records(j):
+    """Records arriving just after watermark MARKS[j] with timestamps at or below it (late on every subtask that
+    received that watermark, and on the single-stream oracle): none after a watermark subtask 1 skipped, where
+    they would not be late on subtask 1.  After 5500 they fall inside the open window [5000, 6000)."""
+    if j in SKIPPED_BY_1 or MARKS[j] >= 7000:
+        return []
+    rng = np.random.default_rng(100 + j)
+    w = MARKS[j]
+    return [(int(u), int(i), int(t)) for u, i, t in
+            zip(rng.integers(0, 2500, 40), rng.integers(0, 1000, 40), rng.integers(w - 499, w + 1, 40))]
 
 
 def _worker(rank, world, port, out_dir, n_users, topk):
@@ -164,19 +187,23 @@ def _worker(rank, world, port, out_dir, n_users, topk):
         sharding.init_comm_torch_ops(core)
         op = _OwnedSubtask(core, M, topk)
         out = None
-        # the same watermark sequence reaches every subtask (the minimum over the keyBy's input channels)
-        marks = [999, 4000, 4999, 5500, 5998, 5999, 7000, (1 << 63) - 1]
         k, n = 0, len(users)
-        for w in marks:
+        for j, w in enumerate(MARKS):
             while k < n and ts[k] <= w:
                 if mine[k]:
                     op.process_element(int(users[k]), int(items[k]), int(ts[k]))
                 k += 1
+            if rank == 1 and j in SKIPPED_BY_1:  # subtask 1's input channels hand it fewer watermarks
+                continue
             r = op.process_watermark(w)
             if r is not None:
                 assert out is None
                 out = r
+            for lu, li, lt in _late_records(j):  # late records after the watermark: dropped and counted
+                if lu % world == rank:
+                    op.process_element(lu, li, lt)
         assert out is not None and out["timestamp"] == 5999
+        assert out["late"] == sum(1 for j in range(len(MARKS)) for lu, _, _ in _late_records(j) if lu % world == rank)
     with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as f:
         pickle.dump(out, f)
     dist.barrier()
@@ -199,6 +226,22 @@ def test_owned_operators_call_sequence_vs_oracle(pkg, oracle, torch_cuda, tmp_pa
     P = int(np.sum(lens * (lens - 1)))
     assert observed == P
     assert all(p["job_observed"] == P for p in parts) and sum(p["observed"] for p in parts) == P
+    # the single-stream oracle (every record, every watermark): the same drops, the same accumulators
+    users, items, ts = _records(up, it)
+    ref = oracle.OracleStream(WINDOW_MS, topk=0)
+    k, n, fired = 0, len(users), []
+    for j, w in enumerate(MARKS):
+        e = int(np.searchsorted(ts, w, side="right"))
+        ref.process_elements(users[k:e], items[k:e], ts[k:e])
+        k = e
+        fired += ref.process_watermark(w)
+        for lu, li, lt in _late_records(j):
+            assert ref.process_element(lu, li, lt), "an injected record must be late for the oracle"
+    assert [wo.ts for wo in fired] == [5999]
+    acc = ref.counters()
+    n_late = sum(len(_late_records(j)) for j in range(len(MARKS)))
+    assert n_late > 0 and sum(p["late"] for p in parts) == acc["UserInteractionCounterLateElements"] == n_late
+    assert acc["UserInteractionCounterObservedCooccurrences"] == P == fired[0].observed
     assert all(p["n_ranges"] > 10 for p in parts), "the forced range limit must split the copy-out"
     # rows: each row on exactly one subtask, int16 view of the closed form
     seen = {}
