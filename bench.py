@@ -14,6 +14,11 @@ list is a function of (seed, user id)) directly on each GPU.  Rank r of N holds 
 rows it owns (sharding.count_owned, the keyBy(itemA) of FlinkCooccurrences.java:152); the
 all-gather, the item-frequency all-reduce and the owner map are inside the timed step.
 --config c2: the MovieLens-20M-shaped log (configs[1]) per rank, records exchange for N > 1.
+--config c5 (configs[4], LLR + per-item top-k): at N = 1 the unit one rank of the 8-GPU job computes -- the whole
+1B log resident (the state after the histories' all-gather), the rows rank --c5-part owns under the snake owner map
+of the whole log's item frequencies counted over every user (cooc_count_device_owned), then every owned row scored
+against the WHOLE log's row sums and observed total (what the row-sum all-reduce hands every owner) and its top-k
+kept (cooc_topk_batch_device).  N > 1: the same through the library's exchange (sharding.count_owned / topk_owned).
 
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on the stream
 it runs on) and a CPU baseline (the oracle's multithreaded record-by-record restatement on a
@@ -154,6 +159,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=["c3", "c5", "c2"], default="c3")
     ap.add_argument("--topk", type=int, default=50)
+    ap.add_argument("--c5-part", type=int, default=0, help="C5 at N=1: the rank of the 8-GPU job whose unit is timed")
+    ap.add_argument("--c5-world", type=int, default=8, help="C5 at N=1: the job's GPU count (owner map)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--permute-items", action="store_true",
                     help="C3/C5: item ids through the fixed bijection datagen.c3_item_perm (ids not in popularity order)")
@@ -181,7 +188,30 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     large = args.config in ("c3", "c5")
-    if large:
+    owner_unit = args.config == "c5" and world == 1
+    if owner_unit:
+        # C5 at N = 1: rank c5_part's unit of the c5_world-GPU job (module docstring)
+        up, it = datagen.c3_log_device(dev, u1=args.c5_world * (datagen.C3_USERS // 8), permute=args.permute_items)
+        M = datagen.C3_ITEMS
+        tmp_core = pkg.CooccurrenceCore(n_items=M, device=local_rank)
+        freq = tmp_core.item_counts(it)
+        tmp_core.close()
+        owner = sharding.snake_owner(freq, args.c5_world)
+        rs_global = datagen.closed_form_rowsums_device(up, it, M)
+        P_local = int(rs_global[owner == args.c5_part].sum().item())  # the owned rows' pairs (row sum = row's pairs)
+        u0, u1 = 0, int(up.numel()) - 1
+        kernel = "k_sp_main+k_sp_small+k_sp_tiny+k_sp_split_finalize"
+        pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_k_sp_main.json"))
+        workload = (f"C5 (BASELINE configs[4]) per-GPU unit of the {args.c5_world}-GPU job: the whole Zipf-skewed "
+                    f"1B log resident (datagen.c3_users seed {datagen.C3_SEED}, {args.c5_world} x 1.25e6 users, 1e6 "
+                    f"items, Zipf(1.0) with replacement, lognormal lengths of mean 100, one window; the state after "
+                    f"the histories' all-gather), the rows rank {args.c5_part} owns (snake_owner of the whole log's "
+                    f"item frequencies) counted over every user, each owned row scored by LLR against the whole "
+                    f"log's row sums and observed total (the all-reduced row sums) with its top-{args.topk} kept "
+                    f"(ItemRowRescorer...java:195-241)")
+        if args.permute_items:
+            workload += f"; item ids permuted by datagen.c3_item_perm (PCG64 seed {datagen.C3_PERM_SEED:#x})"
+    elif large:
         U8 = datagen.C3_USERS // 8
         # the job's users [0, N U/8): contiguous ranges balanced on sum n_u (n_u - 1)
         lens_all = datagen.c3_lengths(0, world * U8)
@@ -240,6 +270,8 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def count():
+        if owner_unit:
+            return core.count_device_owned(up, it, owner, args.c5_part, freq, N)
         if world == 1:
             return core.count_device(up, it)  # on torch's current stream; returns after it drained
         if large:
@@ -250,7 +282,9 @@ def main():
         r = count()
         if args.config == "c5":  # LLR + top-k of every (owned) row, resident on the device
             ev0.record()
-            if world == 1:
+            if owner_unit:
+                core.topk_batch_device(args.topk, tk_sizes, tk_vals, tk_scores, rowsum_global=rs_global)
+            elif world == 1:
                 core.topk_batch_device(args.topk, tk_sizes, tk_vals, tk_scores)
             else:
                 sharding.topk_owned(core, r, args.topk)
@@ -411,6 +445,17 @@ def main():
         # entries; D_read counts what it does read (1 GPU: from the heaps and row lengths), not D
         d_read = entries_read(res, M, args.topk, tk_sizes, tk_scores) if world == 1 else None
         D_rs = d_read if d_read is not None else D
+        # heaps whose root (the least score) is NaN: a wrapped int view makes a cell negative and its log NaN
+        # (ItemRowRescorer...java:207-216 treats any NaN as fatal in DEVELOPMENT_MODE); nan_root_frac says how far
+        # this unit is from that degenerate regime, entries_read / entries how much of the rows the kernel scored
+        filled = tk_sizes > 0
+        n_heaps = int(filled.sum().item())
+        n_nan = int((filled & torch.isnan(tk_scores[:, 0])).sum().item())
+        out["c5_regime"] = {"heaps": n_heaps, "nan_root_heaps": n_nan,
+                            "nan_root_frac": n_nan / max(n_heaps, 1),
+                            "entries_read_frac": (d_read / D) if (d_read is not None and D) else None,
+                            "row_sums": "whole-log (closed form = the all-reduced owned row sums)" if owner_unit
+                            else "this GPU's own result"}
         b_rs = 8.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
         a_rs = b_rs / (tk * 1e-3) / 1e9
         t_rs = pmc_rs.get("hbm_bytes_per_launch")

@@ -247,6 +247,36 @@ def c3_users(u0: int, u1: int, seed: int = C3_SEED, device=None, permute: bool =
     return user_ptr, items.to(torch.int32)
 
 
+def c3_log_device(device, u1: int = C3_USERS, shard: int = C3_USERS // 8, seed: int = C3_SEED, permute: bool = False):
+    """Users [0, u1) of the C3 log as one device CSR, generated shard by shard (bounded temporaries): the state of
+    every rank of an N-GPU run after the histories' all-gather (u1 = C3_USERS: the whole 1B log, 4 GB of ids)."""
+    import torch
+
+    ups, its, base = [], [], 0
+    for a in range(0, u1, shard):
+        up, it = c3_users(a, min(u1, a + shard), seed, device=device, permute=permute)
+        ups.append(up[:-1] + base)
+        its.append(it)
+        base += int(up[-1].item())
+        del up
+    user_ptr = torch.cat(ups + [torch.tensor([base], dtype=torch.int64, device=device)])
+    del ups
+    items = torch.cat(its)
+    return user_ptr, items
+
+
+def closed_form_rowsums_device(user_ptr, items, n_items: int):
+    """rowsum[a] = sum_u m_ua (n_u - 1) over a device CSR, exact int64: what the N-GPU run's owners
+    hold for their rows after the row-sum all-reduce (the broadcast of FlinkCooccurrences.java:163)."""
+    import torch
+
+    lens = user_ptr[1:] - user_ptr[:-1]
+    w = torch.repeat_interleave(lens - 1, lens, output_size=int(items.numel()))
+    rs = torch.zeros(n_items, dtype=torch.int64, device=items.device)
+    rs.index_add_(0, items.long(), w)
+    return rs
+
+
 def c3_ordered_pairs(u0: int, u1: int, seed: int = C3_SEED) -> int:
     n = c3_lengths(u0, u1, seed).astype(np.int64)
     return int(np.sum(n * (n - 1)))

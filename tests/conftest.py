@@ -12,6 +12,36 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
 
 
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """On a GPU box (GRAFT_REPO_ROOT set), a line per 30 s in gpurun_out/heartbeat.log while a test runs: the
+    oracle's CPU checks of the benchmark-sized tests run minutes without printing, and a silent run is taken
+    for a hung one."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if not root:
+        yield
+        return
+    import threading
+    import time
+
+    stop = threading.Event()
+    path = os.path.join(root, "gpurun_out", "heartbeat.log")
+
+    def beat():
+        t0 = time.time()
+        while not stop.wait(30.0):
+            try:
+                with open(path, "a") as f:
+                    f.write(f"{request.node.nodeid} running {time.time() - t0:.0f} s\n")
+            except OSError:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as o

@@ -203,6 +203,7 @@ def _worker(rank, world, port, out_dir, n_users, topk):
                 if lu % world == rank:
                     op.process_element(lu, li, lt)
         assert out is not None and out["timestamp"] == 5999
+        out["late"] = op.late  # (records after the window fired are late too)
         assert out["late"] == sum(1 for j in range(len(MARKS)) for lu, _, _ in _late_records(j) if lu % world == rank)
     with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as f:
         pickle.dump(out, f)
