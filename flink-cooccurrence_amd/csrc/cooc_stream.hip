@@ -531,6 +531,279 @@ __global__ void k_rescore(const int32_t *__restrict__ rows, const int64_t *__res
   }
 }
 
+// The same rescoring, software-pipelined one 64-entry step at a time (the default; COOC_RS_V2=0 runs k_rescore):
+// a row's step i is scored while the column terms of step i + 1 are gathered and the entries of step i + 2
+// loaded, every lane scoring its own entry -- one log for k11 == 1, the full formula otherwise (the lanes of a
+// step diverge over the two), both LogLikelihood.java:41-57 in Java's operation order with the same tables and
+// the same fdlibm log as k_rescore, so the same bits -- and the step's entries that can enter the heap are fed to
+// it in lane order (the sequential loop of ItemRowRescorer...java:199-223).  Without k_rescore's score ring and
+// slow-entry queue a wave needs about half the registers: twice the waves per SIMD, each with a step of column
+// terms in flight, where k_rescore's waves stalled on their gathers between scoring rounds.
+template <class Rows>
+__global__ __launch_bounds__(256) void k_rescore2(const int32_t *__restrict__ rows, const int64_t *__restrict__ n_rows_p,
+                                                  Rows src, const int64_t *__restrict__ grs,
+                                                  const ColTerms *__restrict__ cterm, const double *__restrict__ k11t,
+                                                  const int64_t *__restrict__ obs, int32_t exact,
+                                                  unsigned long long *__restrict__ row_ctr, int32_t topk,
+                                                  int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
+                                                  double *__restrict__ out_score, int32_t no_nan_exit, int32_t rbatch) {
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+  double *hs = smem + int64_t(wave) * (topk + 1);
+  int32_t *hv = reinterpret_cast<int32_t *>(smem + int64_t(waves) * (topk + 1)) + int64_t(wave) * (topk + 1);
+  double *tabs = smem + int64_t(waves) * (topk + 1) + (int64_t(waves) * (topk + 1) + 1) / 2;
+  double *tr12 = tabs + int64_t(wave) * 2 * kRsK, *tr2122 = tr12 + kRsK;
+  const int64_t n_rows = n_rows_p[0];
+  const int64_t observed = exact ? obs[1] : obs[0];
+  int64_t t_next = 0, t_end = 0;
+  for (;;) {
+    if (t_next == t_end) {
+      t_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, (unsigned long long)rbatch)) : 0ll, 0, 64);
+      t_end = t_next + rbatch;
+    }
+    const int64_t t = t_next++;
+    if (t >= n_rows) break;
+    const int32_t a = rows ? rows[t] : int32_t(t);
+    const RowTerms R(observed, rs_row_sum(grs, a, exact));
+    const int64_t n = src.size(a);
+    int32_t size = 0;
+    double least = 0.0;
+    const int64_t rb = n > 0 ? src.base(a) : 0;
+    if (lane < kRsK) {  // (the previous row's reads of them are behind its last step's wave barrier)
+      tr12[lane] = xlogx(R.rs_a - lane);
+      tr2122[lane] = xlogx(observed + 2 * int64_t(lane) - R.rs_a);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the pipeline: A = the step being scored (entry, column terms), B = the next (entry; terms in flight),
+    // C = the one after (entry in flight)
+    int32_t cA = 0, cB = 0;
+    uint32_t vA = 0u, vB = 0u;
+    if (lane < n) src.get_at(rb, lane, cA, vA);
+    if (64 + lane < n) src.get_at(rb, 64 + lane, cB, vB);
+    ColTerms tA{};
+    if (vA != 0u) tA = cterm[cA];
+    for (int64_t i0 = 0; i0 < n; i0 += 64) {
+      int32_t cC = 0;
+      uint32_t vC = 0u;
+      if (i0 + 128 + lane < n) src.get_at(rb, i0 + 128 + lane, cC, vC);
+      ColTerms tB{};
+      if (vB != 0u) tB = cterm[cB];
+      double score = 0.0;
+      if (vA != 0u) {
+        const int64_t k11 = exact ? int64_t(vA) : int64_t(int16_t(uint16_t(vA)));
+        if (k11 == 1) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+          const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (tA.rs - k11);
+          score = llr_terms(R.x_all1, R.x_a, R.x_r1, tA.x_rs, tA.x_or2, 0.0, R.x_a1, tA.x_rs1, xlogx(k22));
+        } else {  // LogLikelihood.java:41-57, the count-only and row-only terms from tables (as k_rescore)
+          const int64_t k12 = R.rs_a - k11;
+          const int64_t k21 = tA.rs - k11;
+          const int64_t k22 = R.observed + k11 - k12 - k21;
+          const bool in = k11 >= -32768 && k11 < 32768, inK = k11 >= 0 && k11 < kRsK;
+          const double x_all = in ? k11t[k11 + 32768 + 65536] : xlogx(k11 + k12 + (k21 + k22));
+          const double x_11 = in ? k11t[k11 + 32768] : xlogx(k11);
+          const double x_12 = inK ? tr12[k11] : xlogx(k12);
+          const double x_2122 = inK ? tr2122[k11] : xlogx(k21 + k22);
+          const double x_21 = (k21 >= -32768 && k21 < 32768) ? k11t[k21 + 32768] : xlogx(k21);
+          score = llr_terms(x_all, R.x_a, x_2122, tA.x_rs, xlogx(k12 + k22), x_11, x_12, x_21, xlogx(k22));
+        }
+      }
+      const int32_t c = vA != 0u ? cA : -1;
+      uint64_t m = __ballot(c >= 0 && (size < topk || score > least));
+      while (m) {  // in lane order: the reference's sequential offers
+        const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+        m &= m - 1;
+        const double sc = __shfl(score, l, 64);
+        const int32_t cl = __shfl(c, l, 64);
+        if (size < topk) {
+          heap_add(hv, hs, size, cl, sc);
+        } else if (sc > hs[1]) {
+          heap_update(hv, hs, size, cl, sc);
+        }
+        least = hs[1];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // a full heap whose root is NaN takes nothing more (score > NaN is false): the rest of the row is not read
+      if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
+      cA = cB;
+      vA = vB;
+      tA = tB;
+      cB = cC;
+      vB = vC;
+    }
+    out_size[t] = size;
+    for (int32_t i = lane; i < size; i += 64) {
+      out_val[t * topk + i] = hv[i + 1];
+      out_score[t * topk + i] = hs[i + 1];
+    }
+  }
+}
+
+// ---- k_rescore3: the same rescoring with every operand staged by LDS-DMA ------------------------------------
+// k_rescore2's register pipeline does not survive the compiler: a gather's destination registers are reused (and
+// zeroed for empty lanes) every step, so each step starts with s_waitcnt vmcnt(0) and at most one step of column
+// terms is ever in flight per wave (the PMC of the full-scoring pass: ~66 requests in flight per CU, 631-cycle
+// L2 latency, waves waiting 53% of their cycles).  Here a wave streams its row through a 4-slot LDS ring with
+// global_load_lds (no destination register): step j is scored while the column terms of steps j + 1 and j + 2 and
+// the entries of steps j + 1 .. j + 3 are in flight; counted waits (vmcnt(4), vmcnt(8): every step issues exactly 4
+// DMA instructions, the clamped tail included) order the ring, and the ring is read by inline ds_reads, which the
+// compiler does not pair with the DMA writes (it would otherwise wait vmcnt(0) before each).  The slow entries'
+// count-only log terms come from LDS tables over k11 < 256 instead of the global k11t.  Same scores, same heaps.
+constexpr int kR3Waves = 4, kR3Slots = 4, kR3L = 3, kR3G = 2, kR3K = 256;
+struct R3Slot {
+  uint32_t col[64];
+  uint32_t cnt[64];
+  uint4 lo[64];  // ColTerms bytes 0-15: rs, x_rs
+  uint4 hi[64];  // ColTerms bytes 16-31: x_rs1, x_or2
+};
+#define R3_LDS(p) ((__attribute__((address_space(3))) void *)(p))
+__device__ inline uint32_t r3_rd32(const void *p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(uint32_t(uintptr_t(R3_LDS(p)))) : "memory");
+  return v;
+}
+typedef uint32_t r3_u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline r3_u32x4 r3_rd128(const void *p) {
+  r3_u32x4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(uint32_t(uintptr_t(R3_LDS(p)))) : "memory");
+  return v;
+}
+template <int N>
+__device__ inline void r3_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(64 * kR3Waves) void k_rescore3(
+    const int32_t *__restrict__ rows, const int64_t *__restrict__ n_rows_p, CsrRows src, const int64_t *__restrict__ grs,
+    const ColTerms *__restrict__ cterm, const int64_t *__restrict__ obs, int32_t exact,
+    unsigned long long *__restrict__ row_ctr, int32_t topk, int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
+    double *__restrict__ out_score, int32_t no_nan_exit, int32_t rbatch, int32_t exp) {
+  __shared__ R3Slot ring[kR3Waves][kR3Slots];
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // dynamic LDS: [x11t kR3K][xallt kR3K] doubles, per wave [tr12 kRsK][tr2122 kRsK] doubles, the heaps
+  double *x11t = smem, *xallt = smem + kR3K;
+  double *tr12 = smem + 2 * kR3K + int64_t(wave) * 2 * kRsK, *tr2122 = tr12 + kRsK;
+  double *hs = smem + 2 * kR3K + kR3Waves * 2 * kRsK + int64_t(wave) * (topk + 1);
+  int32_t *hv = reinterpret_cast<int32_t *>(smem + 2 * kR3K + kR3Waves * 2 * kRsK + kR3Waves * (topk + 1)) +
+                int64_t(wave) * (topk + 1);
+  const int64_t n_rows = n_rows_p[0];
+  const int64_t observed = exact ? obs[1] : obs[0];
+  for (int k = threadIdx.x; k < kR3K; k += 64 * kR3Waves) {  // xlogx(k11) and xlogx(observed + 2 k11), k11 < 256
+    x11t[k] = xlogx(k);
+    xallt[k] = xlogx(observed + 2 * int64_t(k));
+  }
+  __syncthreads();
+  R3Slot *rg = ring[wave];
+  int64_t t_next = 0, t_end = 0;
+  for (;;) {
+    if (t_next == t_end) {
+      t_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, (unsigned long long)rbatch)) : 0ll, 0, 64);
+      t_end = t_next + rbatch;
+    }
+    const int64_t t = t_next++;
+    if (t >= n_rows) break;
+    const int32_t a = rows ? rows[t] : int32_t(t);
+    const RowTerms R(observed, rs_row_sum(grs, a, exact));
+    const int64_t n = src.size(a);
+    int32_t size = 0;
+    double least = 0.0;
+    if (n > 0) {
+      const int64_t rb = src.base(a);
+      if (lane < kRsK) {
+        tr12[lane] = xlogx(R.rs_a - lane);
+        tr2122[lane] = xlogx(observed + 2 * int64_t(lane) - R.rs_a);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int64_t nsteps = (n + 63) >> 6;
+      for (int64_t j = -kR3L; j < nsteps; j++) {
+        {  // entries of step j + L (clamped to the row's last entry past its end: every step issues 2 DMAs)
+          const int64_t jl = j + kR3L;
+          const int64_t e = min(jl * 64 + lane, n - 1);
+          R3Slot &sl = rg[jl & (kR3Slots - 1)];
+          __builtin_amdgcn_global_load_lds(src.col + rb + e, R3_LDS(sl.col), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(src.cnt + rb + e, R3_LDS(sl.cnt), 4, 0, 0);
+        }
+        r3_wait_vm<4>();  // the entries of step j + G (issued one step ago) have landed
+        {  // column terms of step j + G (outside the row: column 0's, never read)
+          const int64_t jg = j + kR3G;
+          R3Slot &sl = rg[jg & (kR3Slots - 1)];
+          const uint32_t c = (jg >= 0 && jg < nsteps) ? r3_rd32(&sl.col[lane]) : 0u;
+          const ColTerms *p = cterm + c;
+          __builtin_amdgcn_global_load_lds(p, R3_LDS(sl.lo), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(p) + 16, R3_LDS(sl.hi), 16, 0, 0);
+        }
+        if (j < 0) continue;
+        r3_wait_vm<8>();  // the column terms of step j (issued two steps ago) have landed
+        const R3Slot &sl = rg[j & (kR3Slots - 1)];
+        const bool in_row = j * 64 + lane < n;
+        const int32_t cA = int32_t(r3_rd32(&sl.col[lane]));
+        const uint32_t vA = in_row ? r3_rd32(&sl.cnt[lane]) : 0u;
+        double score = 0.0;
+        if (exp == 2) {  // (timing experiment, results invalid: no scoring)
+          score = vA != 0u ? double(vA) + double(cA) : 0.0;
+        } else if (vA != 0u) {
+          const r3_u32x4 lo = r3_rd128(&sl.lo[lane]), hi = r3_rd128(&sl.hi[lane]);
+          const int64_t rs_b = int64_t((uint64_t(lo.y) << 32) | lo.x);
+          const double x_rs = __longlong_as_double(int64_t((uint64_t(lo.w) << 32) | lo.z));
+          const double x_rs1 = __longlong_as_double(int64_t((uint64_t(hi.y) << 32) | hi.x));
+          const double x_or2 = __longlong_as_double(int64_t((uint64_t(hi.w) << 32) | hi.z));
+          const int64_t k11 = exact ? int64_t(vA) : int64_t(int16_t(uint16_t(vA)));
+          if (k11 == 1) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+            const int64_t k22 = R.observed + k11 - (R.rs_a - k11) - (rs_b - k11);
+            score = llr_terms(R.x_all1, R.x_a, R.x_r1, x_rs, x_or2, 0.0, R.x_a1, x_rs1, xlogx(k22));
+          } else {  // LogLikelihood.java:41-57 with the count-only and row-only terms from LDS tables
+            const int64_t k12 = R.rs_a - k11;
+            const int64_t k21 = rs_b - k11;
+            const int64_t k22 = R.observed + k11 - k12 - k21;
+            const bool inT = k11 >= 0 && k11 < kR3K, inK = k11 >= 0 && k11 < kRsK;
+            const double x_all = inT ? xallt[k11] : xlogx(k11 + k12 + (k21 + k22));
+            const double x_11 = inT ? x11t[k11] : xlogx(k11);
+            const double x_12 = inK ? tr12[k11] : xlogx(k12);
+            const double x_2122 = inK ? tr2122[k11] : xlogx(k21 + k22);
+            const double x_21 = (k21 >= 0 && k21 < kR3K) ? x11t[k21] : xlogx(k21);
+            score = llr_terms(x_all, R.x_a, x_2122, x_rs, xlogx(k12 + k22), x_11, x_12, x_21, xlogx(k22));
+          }
+        }
+        const int32_t c = vA != 0u ? cA : -1;
+        if (exp == 1) {  // (timing experiment, results invalid: no heap)
+          if (c >= 0 && score > least) least = score;
+          continue;
+        }
+        uint64_t m = __ballot(c >= 0 && (size < topk || score > least));
+        while (m) {  // in lane order: the reference's sequential offers
+          const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+          m &= m - 1;
+          const double sc = __shfl(score, l, 64);
+          const int32_t cl = __shfl(c, l, 64);
+          if (size < topk) {
+            heap_add(hv, hs, size, cl, sc);
+          } else if (sc > hs[1]) {
+            heap_update(hv, hs, size, cl, sc);
+          }
+          least = hs[1];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
+      }
+      r3_wait_vm<0>();  // (the ring's last DMAs: the next row reuses the slots)
+    }
+    out_size[t] = size;
+    for (int32_t i = lane; i < size; i += 64) {
+      out_val[t * topk + i] = hv[i + 1];
+      out_score[t * topk + i] = hs[i + 1];
+    }
+  }
+}
+
+size_t rescore3_lds_bytes(int32_t topk) {
+  return sizeof(double) * (2 * kR3K + kR3Waves * 2 * kRsK + kR3Waves * size_t(topk + 1) +
+                           (kR3Waves * size_t(topk + 1) + 1) / 2);
+}
+
 // The rescorer's observed total after one window from an empty state: sum of the int views of the
 // row-sum updates (ItemRowRescorer...java:154), and the exact total (out3 zeroed by the caller).
 __global__ void k_observed(const int64_t *__restrict__ rowsum, int32_t M, int64_t *__restrict__ out3) {
@@ -833,6 +1106,12 @@ size_t rescore_lds_bytes(int32_t topk) {
          + w * 2 * kRsK * sizeof(double);                 // + the per-wave row tables
 }
 
+// k_rescore2: per wave a heap (topk + 1 doubles and ints) and the row's two k11 tables
+size_t rescore2_lds_bytes(int32_t topk) {
+  const size_t w = 4;
+  return sizeof(double) * (w * size_t(topk + 1) + (w * size_t(topk + 1) + 1) / 2) + w * 2 * kRsK * sizeof(double);
+}
+
 template <class Rows>
 Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_rows_dev, int64_t max_rows, Rows src,
                            int32_t M, const int64_t *grs, const int64_t *obs, bool exact, int32_t topk,
@@ -853,12 +1132,43 @@ Status launch_rescore_rows(hipStream_t s, const int32_t *rows, const int64_t *n_
   const char *rbs = getenv("COOC_RS_BATCH");  // rows per counter grab (A/B knob)
   const int32_t rbatch = rbs ? std::max(1, atoi(rbs)) : 4;
   if (lds > 160 * 1024 - 256) return Status{1, "topk too large for the LDS heaps"};
-  if (lds > 64 * 1024)
-    COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore<Rows>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   int dev = 0, n_cu = 256;
   COOC_HIP_TRY(hipGetDevice(&dev));
   COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  // COOC_RS_V: 3 (default; CSR rows) k_rescore3, 2 k_rescore2, 1 k_rescore
+  static const int ver = getenv("COOC_RS_V") ? atoi(getenv("COOC_RS_V")) : 3;
+  if constexpr (std::is_same<Rows, CsrRows>::value) {
+    const size_t lds3 = rescore3_lds_bytes(topk);
+    if (ver >= 3 && topk <= 1024 && lds3 <= 64 * 1024) {
+      // (COOC_RS_EXP: timing experiments, results invalid -- 1 no heap feed, 2 no scoring)
+      static const int exp = getenv("COOC_RS_EXP") ? atoi(getenv("COOC_RS_EXP")) : 0;
+      auto kern = k_rescore3;
+      int per_cu = 1;
+      COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kR3Waves, lds3));
+      const int64_t want3 = (max_rows + kR3Waves - 1) / kR3Waves;
+      const unsigned grid3 = unsigned(std::max<int64_t>(1, std::min<int64_t>(want3, int64_t(n_cu) * std::max(1, per_cu))));
+      kern<<<grid3, 64 * kR3Waves, lds3, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), obs, exact ? 1 : 0,
+                                              row_ctr, topk, out_size, out_val, out_score, no_nan_exit, rbatch, exp);
+      COOC_HIP_TRY(hipGetLastError());
+      return Status::Ok();
+    }
+  }
+  const bool v2 = ver >= 2;
+  const size_t lds2 = rescore2_lds_bytes(topk);
+  if (v2 && topk <= 1024 && lds2 <= 64 * 1024) {
+    // k_rescore2: 4 waves per workgroup, as many workgroups as fit (about 6 waves per SIMD)
+    int per_cu = 1;
+    COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rescore2<Rows>, 256, lds2));
+    const int64_t want2 = (max_rows + 3) / 4;
+    const unsigned grid2 = unsigned(std::max<int64_t>(1, std::min<int64_t>(want2, int64_t(n_cu) * std::max(1, per_cu))));
+    k_rescore2<Rows><<<grid2, 256, lds2, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), k11t, obs, exact ? 1 : 0,
+                                              row_ctr, topk, out_size, out_val, out_score, no_nan_exit, rbatch);
+    COOC_HIP_TRY(hipGetLastError());
+    return Status::Ok();
+  }
+  if (lds > 64 * 1024)
+    COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_rescore<Rows>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   const int64_t want = (max_rows + waves - 1) / waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * 8)));
   k_rescore<Rows><<<grid, 64 * waves, lds, s>>>(rows, n_rows_dev, src, grs, terms.as<ColTerms>(), k11t, obs, exact ? 1 : 0,
