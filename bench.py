@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+LDS_ADD_PEAK = 6.89 * 256 * 2.4e9  # random-slot no-return ds_add lane-ops/s, measured (profiles/r02/micro/lds_atomics.txt)
 METRIC = "item-pair co-occurrences counted/sec (node) at 1/2/4/8 GPUs; achieved HBM GB/s"
 
 
@@ -47,7 +48,8 @@ def algorithmic_bytes(P: int, N: int, U: int, D: int) -> int:
     return 4 * P + 4 * N + 8 * (U + 1) + 12 * D
 
 
-def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: str, target_s: float = 20.0) -> dict:
+def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: str, target_s: float = 20.0,
+                 threads_override: int = 0) -> dict:
     """The oracle's multithreaded record-by-record restatement (threads own rows a mod T, every
     thread expands every user's records, NonSampled...java:129-161 -> ItemRowAggregator addTo) on
     the first users of the same log: a calibration run sizes the sample (its small size underestimates the
@@ -55,6 +57,8 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
     from oracle import oracle
 
     threads, nproc, avail = cpu_threads()
+    if threads_override > 0:
+        threads = threads_override
     n = np.diff(user_ptr)
     cum = np.cumsum(n * (n - 1))
 
@@ -75,6 +79,9 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
     assert pairs == P
     return {"value": P / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "nproc": nproc, "cpus_available": avail,
+            "threads_rule": ("the GPU box's CPU share per GPU (OMP_NUM_THREADS; the affinity mask lists the whole host's "
+                             "CPUs, shared by the node's GPUs); bench.py --cpu-threads N times another count"
+                             if not threads_override else "--cpu-threads"),
             "label": "CPU restatement, not the JVM reference (BASELINE.md)",
             "sample": f"first {nu} users of {what} ({len(it)} interactions, {P} ordered pairs, {nnz} keys), "
                       f"one window, {threads} threads, {dt:.1f} s"}
@@ -152,16 +159,133 @@ def load_pmc(path: str) -> dict:
     return {}
 
 
+def c4_batches(n_windows: int = 100):
+    """BASELINE configs[3]: the C2 log with event times over n_windows tumbling 1 s windows (datagen.config_c4,
+    seed 4) as per-window batches (window maxTimestamp, user ids, user_ptr, items; users ascending, each user's
+    new items in arrival order) -- what GpuNonSampledCooccurrenceRowsOperator hands cooc_submit_batch."""
+    from flink_cooccurrence_amd import datagen
+
+    d = datagen.config_c4(n_windows=n_windows)
+    up, it, ts, M = d["user_ptr"], d["items"], d["ts"], d["n_items"]
+    lens = np.diff(up)
+    owner = np.repeat(np.arange(len(lens), dtype=np.int32), lens)
+    win = ts // 1000
+    order = np.lexsort((ts, owner, win))
+    w_sorted, u_sorted, i_sorted = win[order], owner[order], it[order]
+    bounds = np.searchsorted(w_sorted, np.arange(n_windows + 1))
+    batches = []
+    for w in range(n_windows):
+        s0, e0 = bounds[w], bounds[w + 1]
+        uu = u_sorted[s0:e0]
+        starts = np.concatenate([[0], np.nonzero(np.diff(uu))[0] + 1]).astype(np.int64)
+        batches.append((w * 1000 + 999, uu[starts].astype(np.int32), np.concatenate([starts, [e0 - s0]]).astype(np.int64),
+                        i_sorted[s0:e0].astype(np.int32)))
+    return d, batches
+
+
+def run_c4(args):
+    """C4 (BASELINE configs[3]): streaming 1 s windows into resident device state on one GPU.  A step is one window:
+    cooc_submit_batch + cooc_finish_window -- the window's pairs expanded against the users' resident histories
+    (NonSampled...java:129-161), its delta rows and row sums reduced (ItemRowAggregator / RowSumAggregator), merged
+    into the resident global rows and row sums and every touched row rescored, LLR top-k (ItemRowRescorer...java:
+    144-228).  Warm-up: the whole stream once on a context that is then dropped; timed: the whole stream again on a
+    fresh context (state from empty, as a job starts), every window bracketed by device synchronisations."""
+    import torch
+
+    import __graft_entry__
+
+    pkg = __graft_entry__.load_package()
+    from flink_cooccurrence_amd import datagen
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--config c4 runs on one GPU (its multi-GPU streaming is tests/test_streaming_multiproc.py)")
+    n_windows = 100
+    d, batches = c4_batches(n_windows)
+    M, topk = d["n_items"], (args.topk if args.topk != 50 else 10)  # (the reference's default topK, Configuration.java:153)
+    torch.cuda.set_device(0)
+
+    def stream(core, timed):
+        lat, kms, pairs, nnz, users, inter = [], [], [], [], [], []
+        for ts_w, uid, uptr, items in batches:
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            core.submit_batch(ts_w, uid, uptr, items)
+            info = core.finish_window_info(ts_w)
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t1)
+            if timed:
+                kms.append(core.last_kernel_ms())
+                pairs.append(int(info.observed))
+                nnz.append(int(info.nnz))
+                users.append(len(uid))
+                inter.append(len(items))
+        return lat, kms, pairs, nnz, users, inter
+
+    for _ in range(max(1, args.warmup)):
+        with pkg.CooccurrenceCore(n_items=M, topk=topk, window_size_ms=1000, device=0) as warm:
+            stream(warm, False)
+    core = pkg.CooccurrenceCore(n_items=M, topk=topk, window_size_ms=1000, device=0)
+    core.set_kernel_timing(True)
+    lat, kms, pairs, nnz, users, inter = stream(core, True)
+    total_pairs = int(np.sum(pairs))
+    assert total_pairs == datagen.ordered_pairs(d["user_ptr"]), "the windows' pairs must add up to the whole log's"
+    lat_ms = np.array(lat) * 1e3
+    elapsed = float(np.sum(lat))
+    # the counting kernel per window (HIP events on its stream): window pairs / expansion against resident histories
+    b_alg = sum(algorithmic_bytes(p, n, u, k) for p, n, u, k in zip(pairs, inter, users, nnz))
+    k_total = float(np.sum(kms)) * 1e-3
+    achieved = b_alg / k_total / 1e9 if k_total > 0 else None
+    out = {
+        "metric": METRIC,
+        "value": total_pairs / elapsed,
+        "unit": "pairs/s",
+        "n_gpus": 1,
+        "steps": n_windows,
+        "warmup": max(1, args.warmup),
+        "ms_per_step": elapsed / n_windows * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": ("C4 (BASELINE configs[3]): the MovieLens-20M-shaped log (138,493 users x 26,744 items, 20,000,263 "
+                         "interactions, datagen.config_c4 seed 4) over 100 tumbling 1 s windows into resident device state "
+                         f"(histories, dense global rows, row sums), LLR top-{topk} of every touched row per window; a step "
+                         "is one window (submit + finish, synchronised), value = the windows' incremental ordered pairs / "
+                         "their summed latency"),
+            "items": M, "windows": n_windows, "topk": topk, "ordered_pairs_total": total_pairs,
+            "window_latency_ms": {"median": float(np.median(lat_ms)), "p90": float(np.percentile(lat_ms, 90)),
+                                  "max": float(lat_ms.max()), "first": float(lat_ms[0])},
+            "interactions_per_window_median": float(np.median(inter)),
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "k_acc_batch (each window's expansion against the resident histories)",
+            "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS if achieved else None, "traffic": None,
+            "kernel_ms_total": k_total * 1e3, "algorithmic_bytes_total": b_alg,
+            "note": "B_alg = sum over windows of 4P_w + 4N_w + 8(U_w+1) + 12D_w (the window's new pairs, new interactions, "
+                    "active users, delta keys), over the summed HIP-event time of the counting kernel; the window latency "
+                    "also holds the merge into the resident rows, the rescoring and the host bookkeeping (value)",
+        },
+        "cpu_baseline": None,
+    }
+    print(json.dumps(out), flush=True)
+    core.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["c3", "c5", "c2"], default="c3")
+    ap.add_argument("--config", choices=["c3", "c5", "c2", "c4"], default="c3")
     ap.add_argument("--topk", type=int, default=50)
     ap.add_argument("--c5-part", type=int, default=0, help="C5 at N=1: the rank of the 8-GPU job whose unit is timed")
     ap.add_argument("--c5-world", type=int, default=8, help="C5 at N=1: the job's GPU count (owner map)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (default: the box's CPU share, OMP_NUM_THREADS, else every CPU)")
     ap.add_argument("--permute-items", action="store_true",
                     help="C3/C5: item ids through the fixed bijection datagen.c3_item_perm (ids not in popularity order)")
     ap.add_argument("--no-permuted", action="store_true",
@@ -170,6 +294,8 @@ def main():
                     help="C3: rows in column order (without it the counting line runs with COOC_FLAG_ANY_ORDER: a "
                          "row's entries in no particular order, as the reference's Int2ShortOpenHashMap rows)")
     args = ap.parse_args()
+    if args.config == "c4":
+        return run_c4(args)
 
     import torch
     import torch.distributed as dist
@@ -428,6 +554,18 @@ def main():
     if permuted is not None:
         permuted["vs_rank_ordered"] = permuted["ms_per_step"] / ms_per_step
         out["permuted"] = permuted
+    if not large:
+        # C2's dense-row kernel is bound by LDS atomics, not HBM (its HBM frac above 1 is the partner lists' reuse
+        # from L2 / the Infinity Cache): one no-return ds_add_u32 per partner id a contribution walks -- sum_u n_u^2 =
+        # P + N adds -- against the chip's measured random-slot rate (scripts/micro/lds_atomics.hip,
+        # profiles/r02/micro/lds_atomics.txt: 6.89 lane-ops per CU-cycle, 4.23e12 adds/s at 2.4 GHz)
+        adds = float(P_counted + N_seen)
+        out["roofline_lds"] = {"bound": "lds_atomics", "kernel": "k_acc_batch", "achieved": adds / (k_ms * 1e-3),
+                               "peak": LDS_ADD_PEAK, "unit": "ds_add lane-ops/s",
+                               "frac": adds / (k_ms * 1e-3) / LDS_ADD_PEAK, "adds_per_launch": adds,
+                               "lds_bank_conflict_frac": pmc.get("lds_bank_conflict_frac"),
+                               "note": "sum_u n_u^2 no-return LDS adds per launch over the kernel's HIP-event time, against "
+                                       "the random-slot ds_add rate measured on this chip (profiles/r02/micro)"}
     if args.config == "c5":
         out["config"]["topk"] = args.topk
         out["config"]["output"] += f"; top-{args.topk} heaps (sizes, values, scores) per row in HBM"
@@ -477,9 +615,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if large:
             bu, bi = datagen.c3_users(0, 200_000, permute=args.permute_items)
-            out["cpu_baseline"] = cpu_baseline(bu, bi, M, "the same C3 log")
+            out["cpu_baseline"] = cpu_baseline(bu, bi, M, "the same C3 log", threads_override=args.cpu_threads)
         else:
-            out["cpu_baseline"] = cpu_baseline(d["user_ptr"], d["items"], M, "the same C2 log")
+            out["cpu_baseline"] = cpu_baseline(d["user_ptr"], d["items"], M, "the same C2 log",
+                                               threads_override=args.cpu_threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     core.close()

@@ -14,6 +14,9 @@ struct MergeResult {
   int64_t *rowsum = nullptr;
 };
 
+// Owned rows are merged in one dense LDS row of n_items counters up to this many bytes, by sorting above it.
+constexpr int64_t kMergeDenseMaxBytes = 160 * 1024 - 1024;
+
 class Sharder {
  public:
   // Entries of the last local result destined to every owner (host array of n_parts).
@@ -30,6 +33,7 @@ class Sharder {
  private:
   int32_t planned_parts_ = 0;
   DevBuf perm_nnz_, perm_off_, part_entries_, tmp_, recv_off_, cap_, row_base_, row_nnz_, col_, cnt_, rowsum_, err_;
+  DevBuf skeys_, svals_;  // large universes: the received entries' sort keys and counts (merge)
 };
 
 }  // namespace cooc

@@ -166,6 +166,62 @@ __global__ __launch_bounds__(kThreads) void k_merge_rows(
   }
 }
 
+// ---- large universes (n_items >= kMergeDenseMax: no dense LDS row) --------------------------------------
+// Every received entry as the sort key (owned row index << 32 | column) and its count: a segment k = (source,
+// owned row r) of the source-major buffers holds one source's partial row r, in column order.
+__global__ void k_merge_keys(const int32_t *__restrict__ recv_nnz, const int64_t *__restrict__ recv_off,
+                             const uint64_t *__restrict__ entries, int64_t K, int32_t R, uint64_t *__restrict__ keys,
+                             uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t k = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; k < K; k += n_waves) {
+    const uint64_t r = uint64_t(k % R);
+    const int64_t lo = recv_off[k], hi = lo + recv_nnz[k];
+    for (int64_t i = lo + lane; i < hi; i += 64) {
+      const uint64_t e = entries[i];
+      keys[i] = (r << 32) | (e >> 32);
+      vals[i] = uint32_t(e);
+    }
+  }
+}
+
+// Owned row r's entries among the merged (sorted, reduced) keys: [lower_bound(r << 32), lower_bound((r+1) << 32)).
+__global__ void k_merge_rows_from_keys(const uint64_t *__restrict__ ukeys, const uint32_t *__restrict__ usum,
+                                       const int64_t *__restrict__ n_runs_p, int32_t R, int32_t part, int32_t n_parts,
+                                       int64_t *__restrict__ row_base, int32_t *__restrict__ row_nnz,
+                                       int32_t *__restrict__ col_out, uint32_t *__restrict__ cnt_out,
+                                       const int64_t *__restrict__ rowsum_global, int64_t *__restrict__ rowsum_out,
+                                       int64_t *__restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t n = n_runs_p[0];
+  auto lb = [&](uint64_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ukeys[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  for (int64_t r = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < R; r += n_waves) {
+    const int64_t b = lb(uint64_t(r) << 32), e = lb(uint64_t(r + 1) << 32);
+    uint64_t sum = 0;
+    for (int64_t i = b + lane; i < e; i += 64) {
+      col_out[i] = int32_t(uint32_t(ukeys[i]));
+      cnt_out[i] = usum[i];
+      sum += usum[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) {
+      row_base[r] = b;
+      row_nnz[r] = int32_t(e - b);
+      rowsum_out[r] = int64_t(sum);
+      if (rowsum_global && int64_t(sum) != rowsum_global[part + r * n_parts])
+        atomicOr(reinterpret_cast<unsigned long long *>(err), 2ull);
+    }
+  }
+}
+
 }  // namespace
 
 Status Sharder::plan(const CountResult &r, int32_t M, int32_t n_parts, hipStream_t s, int64_t *h_entries) {
@@ -241,7 +297,40 @@ Status Sharder::merge(int32_t M, int32_t n_parts, int32_t part, const int32_t *d
   COOC_HIP_TRY(hipStreamSynchronize(s));
   COOC_TRY(col_.reserve(sizeof(int32_t) * (cap_total + 1)));
   COOC_TRY(cnt_.reserve(sizeof(uint32_t) * (cap_total + 1)));
-  if (R > 0) {
+  if (R > 0 && int64_t(M) * 4 > kMergeDenseMaxBytes) {
+    // a universe whose dense row does not fit the LDS: the received entries sorted by (owned row, column) and runs
+    // of equal keys summed (library radix sort + reduce-by-key; the exchange path of streaming windows at p > 1)
+    int64_t n_recv = 0;
+    COOC_HIP_TRY(hipMemcpyAsync(&n_recv, recv_off_.as<int64_t>() + K - 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    int32_t last = 0;
+    COOC_HIP_TRY(hipMemcpyAsync(&last, d_recv_nnz + K - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    COOC_HIP_TRY(hipStreamSynchronize(s));
+    n_recv += last;
+    COOC_TRY(skeys_.reserve(sizeof(uint64_t) * size_t(2 * n_recv + 2)));
+    COOC_TRY(svals_.reserve(sizeof(uint32_t) * size_t(2 * n_recv + 2) + sizeof(int64_t)));
+    uint64_t *k0 = skeys_.as<uint64_t>(), *k1 = k0 + n_recv + 1;
+    uint32_t *v0 = svals_.as<uint32_t>(), *v1 = v0 + n_recv + 1;
+    int64_t *n_runs = reinterpret_cast<int64_t *>(svals_.as<char>() + sizeof(uint32_t) * size_t(2 * n_recv + 2));
+    COOC_HIP_TRY(hipMemsetAsync(n_runs, 0, sizeof(int64_t), s));
+    if (n_recv > 0) {
+      k_merge_keys<<<std::min<unsigned>(blocks_for(K * 64, 256), 8192), 256, 0, s>>>(
+          d_recv_nnz, recv_off_.as<int64_t>(), d_entries, K, R, k0, v0);
+      int kb = 33;
+      while ((int64_t(1) << (kb - 32)) < int64_t(R) && kb < 64) kb++;
+      size_t bs = 0, br = 0;
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, bs, k0, k1, v0, v1, int(n_recv), 0, kb, s));
+      COOC_HIP_TRY(hipcub::DeviceReduce::ReduceByKey(nullptr, br, k1, k0, v1, v0, n_runs, hipcub::Sum(), int(n_recv), s));
+      COOC_TRY(tmp_.reserve(std::max(bs, br)));
+      bs = tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bs, k0, k1, v0, v1, int(n_recv), 0, kb, s));
+      br = tmp_.cap;
+      COOC_HIP_TRY(hipcub::DeviceReduce::ReduceByKey(tmp_.p, br, k1, k0, v1, v0, n_runs, hipcub::Sum(), int(n_recv), s));
+    }
+    k_merge_rows_from_keys<<<std::min<unsigned>(blocks_for(int64_t(R) * 64, 256), 8192), 256, 0, s>>>(
+        k0, v0, n_runs, R, part, n_parts, row_base_.as<int64_t>(), row_nnz_.as<int32_t>(), col_.as<int32_t>(),
+        cnt_.as<uint32_t>(), d_rowsum_global, rowsum_.as<int64_t>(), err_.as<int64_t>());
+    COOC_HIP_TRY(hipGetLastError());
+  } else if (R > 0) {
     const size_t lds = size_t(M) * 4;
     COOC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_merge_rows),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
@@ -269,7 +358,7 @@ Status Sharder::merge(int32_t M, int32_t n_parts, int32_t part, const int32_t *d
 
 void Sharder::release() {
   DevBuf *all[] = {&perm_nnz_, &perm_off_, &part_entries_, &tmp_, &recv_off_, &cap_,
-                   &row_base_, &row_nnz_, &col_, &cnt_, &rowsum_, &err_};
+                   &row_base_, &row_nnz_, &col_, &cnt_, &rowsum_, &err_, &skeys_, &svals_};
   for (DevBuf *b : all) b->release();
 }
 

@@ -204,8 +204,6 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   // p > 1 subtasks: every subtask takes part in every window's exchange, also with no user of its own
   const bool multi = ctx.comm && ctx.comm->world() > 1;
   owned_window_ = multi;
-  if (multi && ctx.counter.sparse())
-    return Status{COOC_ERR_STATE, "multi-GPU streaming windows need n_items < 40,320 (owners merge dense rows)"};
   if (multi && empty_window_) {
     int64_t obs_total = 0;
     COOC_TRY(exchange_window(ctx, s, nullptr, 0, &obs_total));
@@ -286,7 +284,7 @@ Status StreamState::finish(cooc_ctx &ctx, int64_t ts, cooc_window_info *info) {
   CountResult r;
   tr.mark("upload_append", s);
   if (ctx.counter.batch_ok())  // n_items < 40,320: the batch planner + k_acc_batch
-    COOC_TRY(ctx.counter.run_window(au, s, &r));
+    COOC_TRY(ctx.counter.run_window(au, s, &r, ctx.timer.enabled ? &ctx.timer : nullptr));  // (cooc_last_kernel_ms)
   else  // n_items >= 40,320 (or COOC_FLAG_GENERAL_PLANNER): the large-universe planner, old / new positions in one pass
     COOC_TRY(count_large_window(ctx, s, n_act, act_off, act_len, act_old, cbase[n_act], &r));
   tr.mark("count", s);
@@ -450,7 +448,18 @@ Status StreamState::finish_owned(cooc_ctx &ctx, hipStream_t s, int64_t ts, int64
   const int32_t M = ctx.cfg.n_items;
   int64_t *scal = d_scal_.as<int64_t>();
   COOC_TRY(launch_merge_owned(s, M, d_own_base_.as<int64_t>(), d_own_nnz_.as<int32_t>(), own_col_, own_cnt_,
-                              d_rs_win_.as<int64_t>(), d_global_.as<uint32_t>(), d_grs_.as<int64_t>(), scal, obs_total));
+                              d_rs_win_.as<int64_t>(), sparse_global_ ? nullptr : d_global_.as<uint32_t>(),
+                              d_grs_.as<int64_t>(), scal, obs_total));
+  int64_t nnz = 0;
+  // the owned delta rows packed (M-row CSR, ascending columns): the window's output, and for a large universe the
+  // delta merged into the resident row slabs (ItemRowRescorer...java:171-177)
+  COOC_TRY(launch_pack_rows(s, M, d_own_base_.as<int64_t>(), d_own_nnz_.as<int32_t>(), own_col_, own_cnt_, d_own_rp_,
+                            d_own_pcol_, d_own_pcnt_, d_scan_tmp_, &nnz));  // (synchronises s)
+  if (sparse_global_) {
+    int64_t new_cols = 0;
+    COOC_TRY(launch_gs_merge(s, M, d_own_rp_.as<int64_t>(), d_own_pcol_.as<int32_t>(), d_own_pcnt_.as<uint32_t>(), nnz,
+                             gs_, d_scan_tmp_, &new_cols));
+  }
   COOC_TRY(d_touched_.reserve(sizeof(int32_t) * M));
   COOC_TRY(launch_touched(s, M, d_own_nnz_.as<int32_t>(), d_touched_.as<int32_t>(), scal, d_scan_tmp_));
   const int32_t topk = ctx.cfg.topk;
@@ -458,15 +467,18 @@ Status StreamState::finish_owned(cooc_ctx &ctx, hipStream_t s, int64_t ts, int64
     COOC_TRY(d_topk_size_.reserve(sizeof(int32_t) * M));
     COOC_TRY(d_topk_val_.reserve(sizeof(int32_t) * size_t(M) * topk));
     COOC_TRY(d_topk_score_.reserve(sizeof(double) * size_t(M) * topk));
-    COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
-                            (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
-                            d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+    if (sparse_global_)
+      COOC_TRY(launch_rescore_sparse(s, d_touched_.as<int32_t>(), scal, M, gs_, d_grs_.as<int64_t>(),
+                                     (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
+                                     d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
+    else
+      COOC_TRY(launch_rescore(s, d_touched_.as<int32_t>(), scal, M, d_global_.as<uint32_t>(), d_grs_.as<int64_t>(),
+                              (ctx.cfg.flags & COOC_FLAG_EXACT_SCORES) != 0, topk, M, d_llr_terms_,
+                              d_topk_size_.as<int32_t>(), d_topk_val_.as<int32_t>(), d_topk_score_.as<double>()));
   }
   int64_t h_scal[8];
   COOC_HIP_TRY(hipMemcpyAsync(h_scal, scal, sizeof(h_scal), hipMemcpyDeviceToHost, s));
-  int64_t nnz = 0;
-  COOC_TRY(launch_pack_rows(s, M, d_own_base_.as<int64_t>(), d_own_nnz_.as<int32_t>(), own_col_, own_cnt_, d_own_rp_,
-                            d_own_pcol_, d_own_pcnt_, d_scan_tmp_, &nnz));  // (synchronises s)
+  COOC_HIP_TRY(hipStreamSynchronize(s));
   PlanTotals t;
   COOC_TRY(ctx.counter.read_totals(&t));
   if (t.err & 8) return Status{COOC_ERR_STATE, "internal bounds check failed"};
@@ -526,7 +538,8 @@ Status StreamState::count_large_window(cooc_ctx &ctx, hipStream_t s, int64_t n_a
   w.old = d_act_old_.as<int32_t>();
   w.cbase = d_cbase_.as<int64_t>();
   w.n_contrib = n_full;
-  return ctx.counter.run_sparse(2 * n_act, d_lw_up2_.as<int64_t>(), lists, o, s, r, nullptr, nullptr, 0, nullptr, 0, &w);
+  return ctx.counter.run_sparse(2 * n_act, d_lw_up2_.as<int64_t>(), lists, o, s, r,
+                                ctx.timer.enabled ? &ctx.timer : nullptr, nullptr, 0, nullptr, 0, &w);
 }
 
 Status StreamState::copy_delta(cooc_ctx &ctx, int32_t *rows, int64_t *row_ptr, int32_t *cols, uint32_t *cnt,

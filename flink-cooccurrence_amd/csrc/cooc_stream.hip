@@ -1032,9 +1032,11 @@ Status launch_merge_owned(hipStream_t s, int32_t M, const int64_t *base, const i
                           int64_t observed_window) {
   COOC_HIP_TRY(hipMemsetAsync(scal + 1, 0, sizeof(int64_t), s));
   COOC_HIP_TRY(hipMemsetAsync(scal + 4, 0, sizeof(int64_t), s));
-  // the owned rows' entries into the dense global rows (k_merge_global with no row sums: zero deltas)
-  k_merge_global<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
-      M, base, nnz, col, cnt, nullptr, G, nullptr, nullptr);
+  // the owned rows' entries into the dense global rows (k_merge_global with no row sums: zero deltas); G == NULL: a
+  // large universe, whose sparse row slabs the caller merges (launch_gs_merge)
+  if (G)
+    k_merge_global<<<std::min<unsigned>(blocks_for(int64_t(M) * 64, 256), 8192), 256, 0, s>>>(
+        M, base, nnz, col, cnt, nullptr, G, nullptr, nullptr);
   k_add_rowsums<<<std::min<unsigned>(blocks_for(M, 256), 1024), 256, 0, s>>>(M, rs_all, nnz, grs, scal);
   k_finish_scalars<<<1, 1, 0, s>>>(scal, observed_window);
   COOC_HIP_TRY(hipGetLastError());

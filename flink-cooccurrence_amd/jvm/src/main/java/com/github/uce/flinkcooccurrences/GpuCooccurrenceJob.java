@@ -83,7 +83,7 @@ final class GpuCooccurrenceJob {
   }
 
   /**
-   * p > 1 subtasks, a multi-window stream (n_items < 40,320): the keyBy(item) merge of partial rows replaced by
+   * p > 1 subtasks, a multi-window stream (any n_items): the keyBy(item) merge of partial rows replaced by
    * the library's exchange per window (cooc.h, cooc_finish_window across GPUs).  Each subtask keeps its users'
    * histories and the global rows it owns resident; gpuRescore: GpuNonSampledCooccurrenceTopKOperator rescores
    * the owned rows on the device at parallelism p; otherwise the rows operator's complete owned rows and their

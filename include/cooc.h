@@ -249,8 +249,8 @@ COOC_API int cooc_topk_items(cooc_ctx *ctx, int32_t k, int32_t flags, int32_t n,
  * window append.  cooc_finish_window expands every staged user against its resident history,
  * reduces the window's delta rows and row sums, merges them into the global state and, if
  * topk > 0, rescores every touched row (ItemRowRescorer...java:144-228).
- * Across GPUs (a communicator of world > 1 on ctx, cooc_comm_init / cooc_comm_init_ops; item universes below
- * 40,320): each context holds the resident histories of ITS users (a keyBy(user) shard,
+ * Across GPUs (a communicator of world > 1 on ctx, cooc_comm_init / cooc_comm_init_ops; any item universe: below
+ * 40,320 items the owners keep dense global rows, above it sorted row slabs): each context holds the resident histories of ITS users (a keyBy(user) shard,
  * FlinkCooccurrences.java:70) and cooc_finish_window is collective: every rank expands its own users, the
  * partial delta rows go to their owners (row a on rank a mod world: the keyBy(item) of :152), the row-sum
  * deltas and the window's pairs are all-reduced (the broadcast of :163), and each owner merges its rows into

@@ -8,8 +8,9 @@ rescores them (ItemRowRescorer...java:144-228).  The subtasks agree on every win
 on any of them, by an all-gather), so a subtask with no record in a window still joins its exchange.
 
 Two processes on the box's one GPU, the communicator over gloo (cooc_comm_ops; RCCL refuses two ranks on one
-GPU), 20+ windows of a C1-shaped click log and of a C4-shaped log (C2 lengths and popularity, without
-replacement): the union of the two subtasks' outputs equals OracleStream's, window by window (delta rows exact
+GPU), 20+ windows of a C1-shaped click log, of a C4-shaped log (C2 lengths and popularity, without
+replacement) and of a C1-shaped log over a 1e6-item universe (sparse resident rows; the owners merge
+the partial rows by sorting), with the same or with different watermark sequences on the two subtasks: the union of the two subtasks' outputs equals OracleStream's, window by window (delta rows exact
 and int16, row sums exact and int32, observed, top-k heaps), and the accumulators add up.  Needs an MI355X.
 """
 import os
@@ -42,6 +43,9 @@ def _records(kind):
     if kind == "c1":
         d = datagen.config_c1(seed=1, U=2000, M=300, mean=20.0)
         M = 300
+    elif kind == "wide":  # a large universe (1e6 items: sparse resident rows, owners merge partial rows by sorting)
+        M = 1_000_000
+        d = datagen.config_c1(seed=5, U=2000, M=M, mean=20.0)
     else:
         d = datagen.config_c4(seed=4, n_windows=20, U=3000, M=2000, N=60_000)
         M = 2000
@@ -121,7 +125,7 @@ def _union(parts):
         topk_scores=np.array([parts[j].topk_scores[i] for _, i, j in tk], np.float64).reshape(len(tk), k))
 
 
-@pytest.mark.parametrize("kind,lag", [("c1", False), ("c4", False), ("c1", True)])
+@pytest.mark.parametrize("kind,lag", [("c1", False), ("c4", False), ("c1", True), ("wide", False), ("wide", True)])
 def test_two_subtasks_stream_vs_oracle(pkg, oracle, torch_cuda, tmp_path, kind, lag):
     """lag: the subtasks receive different watermark sequences; the windows still fire together, in order."""
     import torch.multiprocessing as mp
