@@ -83,6 +83,9 @@ def cpu_baseline(user_ptr: np.ndarray, items: np.ndarray, n_items: int, what: st
                              "CPUs, shared by the node's GPUs); bench.py --cpu-threads N times another count"
                              if not threads_override else "--cpu-threads"),
             "label": "CPU restatement, not the JVM reference (BASELINE.md)",
+            # the figure for every CPU in the affinity mask, by linear scaling of the measured one (an upper bound:
+            # the restatement is memory-bound and shares the host with the node's other GPUs' processes); not timed
+            "all_cpus_linear_upper_bound": {"value": P / dt * avail / threads, "cpus": avail, "measured": False},
             "sample": f"first {nu} users of {what} ({len(it)} interactions, {P} ordered pairs, {nnz} keys), "
                       f"one window, {threads} threads, {dt:.1f} s"}
 
@@ -597,8 +600,14 @@ def main():
         b_rs = 8.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M
         a_rs = b_rs / (tk * 1e-3) / 1e9
         t_rs = pmc_rs.get("hbm_bytes_per_launch")
+        # whole-log row sums (the owner unit): the two passes (cooc_stream.hip, k_rs_score then k_rs_heap) unless
+        # COOC_RS_TWO_PASS=0; a GPU's own row sums: k_rescore3 (one pass; its rows end at a NaN heap root)
+        tp_env = os.environ.get("COOC_RS_TWO_PASS")
+        two_pass = (tp_env != "0") if owner_unit else (tp_env == "1")
+        rs_kernel = ("k_col_terms+k_rs_tables+k_rs_bounds+k_rs_items+k_rs_score+k_rs_heap" if two_pass
+                     else "k_col_terms+k_rescore3")
         out["roofline_rescore"] = {
-            "bound": "hbm", "kernel": "k_col_terms+k_rescore", "achieved": a_rs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "bound": "hbm", "kernel": rs_kernel, "achieved": a_rs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": a_rs / HBM_PEAK_GBPS, "traffic": t_rs, "kernel_ms": tk, "algorithmic_bytes_per_launch": b_rs,
             "units_per_launch": {"entries": D, "entries_read": d_read, "rows": M, "topk": args.topk},
             "traffic_gbps": (t_rs / (tk * 1e-3) / 1e9) if t_rs else None,
@@ -606,6 +615,10 @@ def main():
             "valu_busy": pmc_rs.get("valu_busy"), "limiter": limiter(pmc_rs, t_rs, tk),
             "pmc_source_digest": pmc_rs.get("source_digest") or pmc_rs.get("stale_source_digest"),
             "pmc_stale": rs_stale,
+            # what the two passes move by design: pass 1 reads every entry (8 B) and writes its score (8 B), pass 2
+            # reads the column and score (12 B) of the entries it feeds (rows end at a NaN root)
+            "two_pass_bytes_model": (16.0 * D + 12.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M)
+            if two_pass else None,
             "note": "B = 8D_read + 20M + M(4 + 12k) + 32M per launch (entries read: rows behind a NaN heap root "
                     "end early; row headers and sums, heaps, 32-B column terms), over the HIP-event time of the "
                     "rescoring call; the PMC (traffic, L2 hit) "

@@ -371,7 +371,8 @@ Status cooc_ctx::topk_batch_device(int32_t topk, int32_t flags, const int64_t *d
   const cooc::CountResult &r = batch_result;
   return cooc::launch_rescore_batch(s, M, r.row_base, r.row_nnz, r.col, r.cnt, r.dense,
                                     d_rowsum_global ? d_rowsum_global : r.rowsum, (flags & COOC_FLAG_EXACT_SCORES) != 0,
-                                    topk, b_obs3.as<int64_t>(), b_llr_terms, d_sizes, d_values, d_scores);
+                                    topk, b_obs3.as<int64_t>(), b_llr_terms, d_sizes, d_values, d_scores, r.rank_of,
+                                    r.unordered, r.nnz, d_rowsum_global != nullptr);
 }
 
 Status cooc_ctx::llr(int64_t n, const int64_t *k, double *out) {

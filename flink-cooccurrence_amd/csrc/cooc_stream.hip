@@ -799,6 +799,417 @@ __global__ __launch_bounds__(64 * kR3Waves) void k_rescore3(
   }
 }
 
+// ---- k_rs_score + k_rs_heap: the rescoring in two passes (owned rows against whole-log row sums) ------------------
+// k_rescore3 is bound by its column-term gathers: every entry reads a 32-B ColTerms of a table (32 MB at 1e6 items)
+// that no XCD's 4 MB L2 holds, so its lines come from the Infinity Cache at ~600 cycles each (the C5 owner unit's
+// PMC: L2 hit 31%, waves waiting 53% of their cycles).  Here pass 1 (k_rs_score) scores the entries column block by
+// column block -- kRsB blocks of the row order's columns (ascending rank_of[col], or col), block b's work queued on
+// counter b % 8 in block order and taken first by the workgroups with blockIdx % 8 == b % 8 (one XCD under the
+// round-robin placement; speed only, any workgroup may take any item), so at any time an XCD gathers from the terms
+// of about one block (~0.5 MB) -- and writes every score (8 B) to a dense array beside the entries; pass 2
+// (k_rs_heap) streams each row's columns and scores in order through an LDS-DMA ring and feeds the heap exactly as
+// k_rescore3 does (the sequential loop of ItemRowRescorer...java:199-223; NaN roots end the row).  The scores are
+// k_rescore3's bit for bit: the same formulas over the same integers (the row-only and count-only terms through
+// xlogx or the k11 tables of the same argument).  Pass 1 scores every entry (no NaN-root exit), so this is the
+// path for whole-log row sums, whose heaps are numeric (the C5 owner unit: 2.7% NaN roots); k_rescore3 keeps the
+// local-row-sum case, whose roots are NaN almost everywhere and whose rows end after one step.
+constexpr int kRsB = 64;                                  // column blocks
+constexpr uint64_t kRsZero = 0x7FF0000000000DEAull;      // pass 1's mark of a zero count (a signalling NaN: no
+                                                          // arithmetic result has these bits)
+__device__ inline int32_t rs_blk(const int32_t *__restrict__ rank_of, int32_t c, int32_t bw) {
+  return min(kRsB - 1, (rank_of ? rank_of[c] : c) / bw);
+}
+
+// bp[t (kRsB + 1) + b] = the first entry of row t whose block is >= b (bp[.. + kRsB] = the row's length): one wave
+// per row, lane b binary-searching bound b over the row's block ids (about log2(n) probes per bound instead of a
+// rank lookup per entry)
+__global__ __launch_bounds__(256) void k_rs_bounds(int64_t n_rows, CsrRows src, const int32_t *__restrict__ rank_of,
+                                                   int32_t bw, int32_t *__restrict__ bp) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; t < n_rows; t += n_waves) {
+    int32_t *o = bp + t * (kRsB + 1);
+    const int32_t n = int32_t(src.size(int32_t(t)));
+    int32_t lo = 0;
+    if (n > 0 && lane > 0) {
+      const int64_t rb = src.base(int32_t(t));
+      int32_t hi = n;
+      while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (rs_blk(rank_of, src.col[rb + mid], bw) < lane) lo = mid + 1; else hi = mid;
+      }
+    }
+    o[lane] = lo;
+    if (lane == 0) o[kRsB] = max(n, 0);
+  }
+}
+
+// The slow entries' terms that depend on a row or a column and the count only, for counts k11 < kRsTK: per row t
+// trow[t][k] = {xlogx(rs_a - k) = x(k12), xlogx(observed + 2k - rs_a) = x(k21 + k22)}, per column b
+// tcol[b][k] = {xlogx(observed + 2k - rs_b) = x(k12 + k22), xlogx(rs_b - k) = x(k21)} (the same integers as the
+// formula's, so the same bits): a slow entry then takes one log (x(k22)) instead of four
+constexpr int kRsTK = 8;
+__global__ void k_rs_tables(int32_t M, const int32_t *__restrict__ row_nnz, const int64_t *__restrict__ grs,
+                            const int64_t *__restrict__ obs, int32_t exact, double *__restrict__ trow,
+                            double *__restrict__ tcol) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= int64_t(M) * kRsTK) return;
+  const int32_t a = int32_t(i / kRsTK);
+  const int64_t k = i % kRsTK;
+  const int64_t observed = exact ? obs[1] : obs[0];
+  const int64_t rs = rs_row_sum(grs, a, exact);
+  if (row_nnz[a] > 0) {
+    trow[2 * i] = xlogx(rs - k);
+    trow[2 * i + 1] = xlogx(observed + 2 * k - rs);
+  }
+  tcol[2 * i] = xlogx(observed + 2 * k - rs);
+  tcol[2 * i + 1] = xlogx(rs - k);
+}
+
+// pass 1: one wave per work item = (64 consecutive rows, one block): the item's entries, concatenated over its
+// rows (a wave prefix of the rows' block lengths), are scored in rounds of 64 x kRsU, the next round's entries
+// loaded while the current one's column terms are gathered and scored (a two-stage register pipeline).  Entries
+// with k11 == 1 (one log) are scored in place; the others are queued in LDS with their column terms and scored 64
+// at a time (one log each with the row / column tables), so that no wave runs both paths for a few lanes.
+#ifndef COOC_RS_U
+#define COOC_RS_U 2  // (A/B builds: scripts/build_variant.sh)
+#endif
+constexpr int kRsU = COOC_RS_U;
+#ifndef COOC_RS_GRAB
+#define COOC_RS_GRAB 8  // (A/B builds)
+#endif
+constexpr int kRsGrab = COOC_RS_GRAB;  // work units per counter grab
+constexpr int kRsQ = 128;  // queue capacity: < 64 left over + one sub-round's 64
+constexpr int kRsXT = 256; // LDS tables of x(k11) and x(observed + 2 k11), k11 < kRsXT
+struct RsItem {
+  int64_t t0;        // the item's first row
+  int32_t off[65];   // exclusive prefix of the rows' block lengths (off[64] = the item's entries)
+  int64_t src[64];   // a row's first entry of the block in the CSR arena
+  int64_t dst[64];   // ... and its score slot
+  int64_t rs[64];    // the row's sum
+  double rt[64][4];  // RowTerms: x_a, x_all1, x_r1, x_a1
+  int32_t qk[kRsQ];  // queued entries: item-relative index, count, column's row sum and x(rs_b), column
+  uint32_t qv[kRsQ];
+  int64_t qrs[kRsQ];
+  double qxrs[kRsQ];
+  int32_t qc[kRsQ];
+};
+__device__ inline int rs_item_row(const RsItem &it, int32_t k) {
+  int r = 0;
+#pragma unroll
+  for (int st = 32; st > 0; st >>= 1)
+    if (it.off[r + st] <= k) r += st;
+  return r;
+}
+// the full formula (LogLikelihood.java:41-57) for queue slot j (lanes past the queue: l >= n)
+__device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const double *xt,
+                                     const double *__restrict__ k11t, const double *__restrict__ trow,
+                                     const double *__restrict__ tcol, int64_t observed, int32_t exact,
+                                     uint64_t *__restrict__ score) {
+#pragma clang fp contract(off)
+  if (!on) return;
+  const int32_t k = it.qk[j];
+  const uint32_t v = it.qv[j];
+  const int64_t rs_b = it.qrs[j];
+  const int32_t c = it.qc[j];
+  const int r = rs_item_row(it, k);
+  const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+  const int64_t rs_a = it.rs[r];
+  const int64_t k12 = rs_a - k11;
+  const int64_t k21 = rs_b - k11;
+  const int64_t k22 = observed + k11 - k12 - k21;
+  const bool inX = k11 >= 0 && k11 < kRsXT;
+  const bool in = k11 >= -32768 && k11 < 32768;
+  const double x_all = inX ? xt[kRsXT + k11] : in ? k11t[k11 + 32768 + 65536] : xlogx(k11 + k12 + (k21 + k22));
+  const double x_11 = inX ? xt[k11] : in ? k11t[k11 + 32768] : xlogx(k11);
+  const bool inT = k11 >= 0 && k11 < kRsTK;
+  double x_12, x_2122, x_1222, x_21;
+  if (inT) {
+    const double *tr = trow + ((it.t0 + r) * kRsTK + k11) * 2;
+    const double *tc = tcol + (int64_t(c) * kRsTK + k11) * 2;
+    x_12 = tr[0];
+    x_2122 = tr[1];
+    x_1222 = tc[0];
+    x_21 = tc[1];
+  } else {
+    x_12 = xlogx(k12);
+    x_2122 = xlogx(k21 + k22);
+    x_1222 = xlogx(k12 + k22);
+    x_21 = (k21 >= -32768 && k21 < 32768) ? k11t[k21 + 32768] : xlogx(k21);
+  }
+  const double sc = llr_terms(x_all, it.rt[r][0], x_2122, it.qxrs[j], x_1222, x_11, x_12, x_21, xlogx(k22));
+  score[it.dst[r] + (k - it.off[r])] = uint64_t(__double_as_longlong(sc));
+}
+// Work units of pass 1: the items (64 consecutive rows x one block; queue q = block % 8 holds its blocks' items in
+// block order, so item g = q per_q + (b / 8) n_chunks + chunk) cut into pieces of at most kRsP entries, so that
+// no wave is left alone with the hot rows' items (the Zipf head: ~1e5 entries per item).  units[g] = the item's
+// pieces (units[n] = 0: ubase[n], the exclusive prefix, is the total); umap[u] = the item of unit u.
+#ifndef COOC_RS_P
+#define COOC_RS_P 4096  // (A/B builds)
+#endif
+constexpr int32_t kRsP = COOC_RS_P;
+__global__ __launch_bounds__(256) void k_rs_items(int64_t n_rows, const int32_t *__restrict__ bp, int64_t per_q,
+                                                  int32_t *__restrict__ units) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_chunks = (n_rows + 63) >> 6;
+  const int64_t n = per_q * 8;
+  const int64_t g = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (g > n) return;
+  if (g == n) {
+    if (lane == 0) units[n] = 0;
+    return;
+  }
+  const int64_t i = g % per_q;
+  const int b = int(g / per_q) + 8 * int(i / n_chunks);
+  const int64_t t = ((i % n_chunks) << 6) + lane;
+  int32_t len = t < n_rows ? bp[t * (kRsB + 1) + b + 1] - bp[t * (kRsB + 1) + b] : 0;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) len += __shfl_xor(len, d, 64);
+  if (lane == 0) units[g] = (len + kRsP - 1) / kRsP;
+}
+__global__ void k_rs_unit_map(int64_t n, const int32_t *__restrict__ units, const int64_t *__restrict__ ubase,
+                              int32_t *__restrict__ umap) {
+  const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  for (int32_t p = 0; p < units[g]; p++) umap[ubase[g] + p] = int32_t(g);
+}
+
+__global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, const int32_t *__restrict__ bp,
+                                                  const int64_t *__restrict__ sbase, const int64_t *__restrict__ grs,
+                                                  const ColTerms *__restrict__ cterm, const double *__restrict__ k11t,
+                                                  const double *__restrict__ trow, const double *__restrict__ tcol,
+                                                  const int64_t *__restrict__ obs, int32_t exact,
+                                                  const int64_t *__restrict__ ubase, const int32_t *__restrict__ umap,
+                                                  unsigned long long *__restrict__ qctr, uint64_t *__restrict__ score,
+                                                  int32_t exp) {
+#pragma clang fp contract(off)
+  __shared__ RsItem items[4];
+  __shared__ double xt[2 * kRsXT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t n_chunks = (n_rows + 63) >> 6;
+  const int64_t per_q = n_chunks * (kRsB / 8);
+  const int64_t observed = exact ? obs[1] : obs[0];
+  for (int k = threadIdx.x; k < kRsXT; k += 256) {
+    xt[k] = k11t[k + 32768];
+    xt[kRsXT + k] = k11t[k + 32768 + 65536];
+  }
+  __syncthreads();
+  RsItem &it = items[wave];
+  const int q0 = int(blockIdx.x & 7);
+  for (int qi = 0; qi < 8; qi++) {
+    const int q = (q0 + qi) & 7;
+    const int64_t u_lo = ubase[q * per_q], n_units = ubase[(q + 1) * per_q] - u_lo;
+    int64_t j_next = 0, j_end = 0;
+    for (;;) {
+      if (j_next == j_end) {  // kRsGrab units per counter grab (one counter serves a quarter of the chip's waves)
+        j_next = __shfl(lane == 0 ? int64_t(atomicAdd(qctr + q, (unsigned long long)kRsGrab)) : 0ll, 0, 64);
+        j_end = min(j_next + kRsGrab, n_units);
+      }
+      if (j_next >= n_units) break;
+      const int64_t u = u_lo + j_next++;
+      const int64_t g = umap[u];
+      const int32_t kb = int32_t(u - ubase[g]) * kRsP;  // the unit's piece of the item
+      const int64_t item = g - q * per_q;
+      const int b = q + 8 * int(item / n_chunks);
+      const int64_t t = ((item % n_chunks) << 6) + lane;
+      int32_t e0 = 0, len = 0;
+      if (t < n_rows) {
+        e0 = bp[t * (kRsB + 1) + b];
+        len = bp[t * (kRsB + 1) + b + 1] - e0;
+      }
+      int32_t incl = len;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+      }
+      const int32_t T = __shfl(incl, 63, 64);
+      if (T == 0) continue;
+      it.off[lane] = incl - len;
+      if (lane == 63) it.off[64] = T;
+      if (lane == 0) it.t0 = t;
+      if (len > 0) {
+        const int32_t a = int32_t(t);
+        const int64_t rs_a = rs_row_sum(grs, a, exact);
+        const RowTerms R(observed, rs_a);
+        it.src[lane] = src.base(a) + e0;
+        it.dst[lane] = sbase[t] + e0;
+        it.rs[lane] = rs_a;
+        it.rt[lane][0] = R.x_a;
+        it.rt[lane][1] = R.x_all1;
+        it.rt[lane][2] = R.x_r1;
+        it.rt[lane][3] = R.x_a1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (exp & 32) continue;  // (timing experiment: the items' overhead alone)
+      const int32_t ke = min(T, kb + kRsP);
+      int32_t nq = 0;  // queued entries (wave-uniform)
+      int32_t cA[kRsU];
+      uint32_t vA[kRsU];
+#pragma unroll
+      for (int u = 0; u < kRsU; u++) {  // round 0's entries
+        const int32_t k = kb + u * 64 + lane;
+        const int r = rs_item_row(it, k);
+        cA[u] = 0;
+        vA[u] = 0u;
+        if (k < ke) {
+          cA[u] = src.col[it.src[r] + (k - it.off[r])];
+          vA[u] = src.cnt[it.src[r] + (k - it.off[r])];
+        }
+      }
+      for (int32_t k0 = kb; k0 < ke; k0 += 64 * kRsU) {
+        ColTerms h[kRsU];
+#pragma unroll
+        for (int u = 0; u < kRsU; u++)  // the current round's column terms
+          if (k0 + u * 64 + lane < ke && vA[u] != 0u) h[u] = (exp & 4) ? ColTerms{cA[u], 1.0, 2.0, 3.0} : cterm[cA[u]];
+        int32_t cB[kRsU];
+        uint32_t vB[kRsU];
+#pragma unroll
+        for (int u = 0; u < kRsU; u++) {  // the next round's entries (the row of entry k: the last with off <= k)
+          const int32_t k = k0 + (kRsU + u) * 64 + lane;
+          cB[u] = 0;
+          vB[u] = 0u;
+          if (k < ke) {
+            const int r = rs_item_row(it, k);
+            cB[u] = src.col[it.src[r] + (k - it.off[r])];
+            vB[u] = src.cnt[it.src[r] + (k - it.off[r])];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kRsU; u++) {
+          const int32_t k = k0 + u * 64 + lane;
+          const int r = rs_item_row(it, k);
+          const int64_t k11 = exact ? int64_t(vA[u]) : int64_t(int16_t(uint16_t(vA[u])));
+          const bool valid = k < ke;
+          const bool slow = valid && vA[u] != 0u && k11 != 1;
+          if (valid && !slow) {
+            uint64_t bits = kRsZero;
+            if (vA[u] != 0u) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
+              const int64_t rs_a = it.rs[r];
+              const int64_t k22 = observed + k11 - (rs_a - k11) - (h[u].rs - k11);
+              bits = uint64_t(__double_as_longlong(llr_terms(it.rt[r][1], it.rt[r][0], it.rt[r][2], h[u].x_rs,
+                                                             h[u].x_or2, 0.0, it.rt[r][3], h[u].x_rs1,
+                                                             (exp & 2) ? double(k22) : xlogx(k22))));
+            }
+            if (!(exp & 8) || bits == 0x1234ull) score[it.dst[r] + (k - it.off[r])] = bits;
+          }
+          const uint64_t sm = __ballot(slow);
+          if (slow) {
+            const int j = nq + int32_t(__popcll(sm & lt));
+            it.qk[j] = k;
+            it.qv[j] = vA[u];
+            it.qrs[j] = h[u].rs;
+            it.qxrs[j] = h[u].x_rs;
+            it.qc[j] = cA[u];
+          }
+          nq += int32_t(__popcll(sm));
+          if (exp & 1) nq = 0;  // (timing experiments, results invalid: 1 no slow entries, 2 no fast-path log,
+                                //  4 no gather, 8 no store)
+          if (nq >= 64) {       // a full batch of queued entries
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            nq -= 64;
+            rs_score_slow(it, nq + lane, true, xt, k11t, trow, tcol, observed, exact, score);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kRsU; u++) {
+          cA[u] = cB[u];
+          vA[u] = vB[u];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      rs_score_slow(it, lane, lane < nq, xt, k11t, trow, tcol, observed, exact, score);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// pass 2: one wave per row, its columns and scores streamed through a kR5Slots-slot LDS-DMA ring (3 DMAs per step of
+// 64 entries, issued kR5L steps ahead; counted waits as in k_rescore3), the heap fed in column order
+constexpr int kR5Waves = 4, kR5Slots = 8, kR5L = 6;
+struct R5Slot {
+  uint32_t col[64];
+  uint32_t slo[64];
+  uint32_t shi[64];
+};
+__global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRows src,
+                                                          const int64_t *__restrict__ sbase,
+                                                          const uint64_t *__restrict__ score,
+                                                          unsigned long long *__restrict__ row_ctr, int32_t topk,
+                                                          int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
+                                                          double *__restrict__ out_score, int32_t no_nan_exit) {
+  __shared__ R5Slot ring[kR5Waves][kR5Slots];
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double *hs = smem + int64_t(wave) * (topk + 1);
+  int32_t *hv = reinterpret_cast<int32_t *>(smem + kR5Waves * (topk + 1)) + int64_t(wave) * (topk + 1);
+  R5Slot *rg = ring[wave];
+  int64_t t_next = 0, t_end = 0;
+  for (;;) {
+    if (t_next == t_end) {
+      t_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 4ull)) : 0ll, 0, 64);
+      t_end = t_next + 4;
+    }
+    const int64_t t = t_next++;
+    if (t >= n_rows) break;
+    const int64_t n = src.size(int32_t(t));
+    int32_t size = 0;
+    double least = 0.0;
+    if (n > 0) {
+      const int64_t rb = src.base(int32_t(t)), sb = sbase[t];
+      const int64_t nsteps = (n + 63) >> 6;
+      for (int64_t j = -kR5L; j < nsteps; j++) {
+        {  // step j + L (clamped to the row's last entry past its end: every step issues 3 DMAs)
+          const int64_t jl = j + kR5L;
+          const int64_t e = min(jl * 64 + lane, n - 1);
+          R5Slot &sl = rg[jl & (kR5Slots - 1)];
+          const uint32_t *sp = reinterpret_cast<const uint32_t *>(score + sb + e);
+          __builtin_amdgcn_global_load_lds(src.col + rb + e, R3_LDS(sl.col), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(sp, R3_LDS(sl.slo), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(sp + 1, R3_LDS(sl.shi), 4, 0, 0);
+        }
+        if (j < 0) continue;
+        r3_wait_vm<3 * kR5L>();  // step j's DMAs (issued L steps ago) have landed
+        const R5Slot &sl = rg[j & (kR5Slots - 1)];
+        const bool in_row = j * 64 + lane < n;
+        const uint64_t bits = in_row ? (uint64_t(r3_rd32(&sl.shi[lane])) << 32) | uint64_t(r3_rd32(&sl.slo[lane]))
+                                     : kRsZero;
+        const int32_t c = bits != kRsZero ? int32_t(r3_rd32(&sl.col[lane])) : -1;
+        const double sc = __longlong_as_double(int64_t(bits));
+        uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
+        while (m) {  // in lane order: the reference's sequential offers
+          const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+          m &= m - 1;
+          const double s_l = __shfl(sc, l, 64);
+          const int32_t c_l = __shfl(c, l, 64);
+          if (size < topk) {
+            heap_add(hv, hs, size, c_l, s_l);
+          } else if (s_l > hs[1]) {
+            heap_update(hv, hs, size, c_l, s_l);
+          }
+          least = hs[1];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
+      }
+      r3_wait_vm<0>();  // (the ring's last DMAs: the next row reuses the slots)
+    }
+    out_size[t] = size;
+    for (int32_t i = lane; i < size; i += 64) {
+      out_val[t * topk + i] = hv[i + 1];
+      out_score[t * topk + i] = hs[i + 1];
+    }
+  }
+}
+
 size_t rescore3_lds_bytes(int32_t topk) {
   return sizeof(double) * (2 * kR3K + kR3Waves * 2 * kRsK + kR3Waves * size_t(topk + 1) +
                            (kR3Waves * size_t(topk + 1) + 1) / 2);
@@ -1187,10 +1598,86 @@ Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal
                              out_size, out_val, out_score);
 }
 
+// The two passes (k_rs_bounds, k_rs_score, k_rs_heap) over the batch's CSR rows in row order (rank_of or id).
+// terms: [ColTerms x M][counters][k11 tables][scan state][sbase x M][bp x M (kRsB + 1)][scores x nnz]
+Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int32_t *rank_of, const int64_t *grs,
+                               const int64_t *obs, bool exact, int32_t topk, int64_t nnz, DevBuf &terms,
+                               int32_t *out_size, int32_t *out_val, double *out_score) {
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_ctr = al(sizeof(ColTerms) * size_t(std::max(M, 1)));
+  const size_t o_k11 = o_ctr + 256;
+  const size_t o_state = o_k11 + sizeof(double) * 2 * 65536;
+  const size_t o_sbase = al(o_state + sizeof(unsigned long long) * size_t(scan_state_words(M) + 1));
+  const size_t o_bp = al(o_sbase + sizeof(int64_t) * size_t(M));
+  const size_t o_trow = al(o_bp + sizeof(int32_t) * size_t(M) * (kRsB + 1));
+  const size_t o_tcol = al(o_trow + sizeof(double) * size_t(M) * kRsTK * 2);
+  const int64_t n_items_ = (((int64_t(M) + 63) >> 6) * (kRsB / 8)) * 8;
+  const size_t o_units = al(o_tcol + sizeof(double) * size_t(M) * kRsTK * 2);
+  const size_t o_ubase = al(o_units + sizeof(int32_t) * size_t(n_items_ + 1));
+  const size_t o_ustate = al(o_ubase + sizeof(int64_t) * size_t(n_items_ + 1));
+  const size_t o_umap = al(o_ustate + sizeof(unsigned long long) * size_t(scan_state_words(n_items_ + 1) + 1));
+  const size_t o_score = al(o_umap + sizeof(int32_t) * size_t(n_items_ + std::max<int64_t>(nnz, 0) / kRsP + 1));
+  COOC_TRY(terms.reserve(o_score + sizeof(uint64_t) * size_t(std::max<int64_t>(nnz, 1))));
+  char *base = static_cast<char *>(terms.p);
+  auto *ctr = reinterpret_cast<unsigned long long *>(base + o_ctr);  // [0, 8) pass-1 queues, [8] pass-2 rows
+  auto *k11t = reinterpret_cast<double *>(base + o_k11);
+  auto *state = reinterpret_cast<unsigned long long *>(base + o_state);
+  auto *sbase = reinterpret_cast<int64_t *>(base + o_sbase);
+  auto *bp = reinterpret_cast<int32_t *>(base + o_bp);
+  auto *score = reinterpret_cast<uint64_t *>(base + o_score);
+  auto *trow = reinterpret_cast<double *>(base + o_trow);
+  auto *units = reinterpret_cast<int32_t *>(base + o_units);
+  auto *ubase = reinterpret_cast<int64_t *>(base + o_ubase);
+  auto *ustate = reinterpret_cast<unsigned long long *>(base + o_ustate);
+  auto *umap = reinterpret_cast<int32_t *>(base + o_umap);
+  auto *tcol = reinterpret_cast<double *>(base + o_tcol);
+  COOC_HIP_TRY(hipMemsetAsync(ctr, 0, 256, s));
+  k_col_terms<<<blocks_for(M, 256), 256, 0, s>>>(M, grs, obs, exact ? 1 : 0, terms.as<ColTerms>());
+  k_k11_terms<<<256, 256, 0, s>>>(obs, exact ? 1 : 0, k11t);
+  COOC_HIP_TRY(hipGetLastError());
+  if (M <= 0) return Status::Ok();
+  // sbase = the exclusive prefix of the row lengths (the scan's error word after its state; a timed-out look-back
+  // is repaired in-kernel and only flagged)
+  COOC_HIP_TRY(hipMemsetAsync(state + scan_state_words(M), 0, sizeof(int64_t), s));
+  COOC_TRY(launch_scan<false>(ScanI32{src.row_nnz}, sbase, M, state,
+                              reinterpret_cast<int64_t *>(state + scan_state_words(M)), s));
+  int dev = 0, n_cu = 256;
+  COOC_HIP_TRY(hipGetDevice(&dev));
+  COOC_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int32_t bw = int32_t((int64_t(M) + kRsB - 1) / kRsB);
+  k_rs_tables<<<unsigned((int64_t(M) * kRsTK + 255) / 256), 256, 0, s>>>(M, src.row_nnz, grs, obs, exact ? 1 : 0, trow,
+                                                                          tcol);
+  k_rs_bounds<<<unsigned(std::min<int64_t>((int64_t(M) + 3) / 4, int64_t(n_cu) * 8)), 256, 0, s>>>(M, src, rank_of, bw, bp);
+  // the work units (k_rs_items, a scan, k_rs_unit_map): at most n_items + nnz / kRsP of them
+  const int64_t n_chunks = (int64_t(M) + 63) >> 6, per_q = n_chunks * (kRsB / 8), n_items = per_q * 8;
+  k_rs_items<<<unsigned((n_items + 1 + 3) / 4), 256, 0, s>>>(M, bp, per_q, units);
+  COOC_HIP_TRY(hipMemsetAsync(ustate + scan_state_words(n_items + 1), 0, sizeof(int64_t), s));
+  COOC_TRY(launch_scan<false>(ScanI32{units}, ubase, n_items + 1, ustate,
+                              reinterpret_cast<int64_t *>(ustate + scan_state_words(n_items + 1)), s));
+  k_rs_unit_map<<<unsigned((n_items + 255) / 256), 256, 0, s>>>(n_items, units, ubase, umap);
+  int per_cu1 = 1;  // (a persistent grid: the work comes from the queues)
+  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, k_rs_score, 256, 0));
+  k_rs_score<<<unsigned(n_cu) * unsigned(std::max(1, per_cu1)), 256, 0, s>>>(M, src, bp, sbase, grs, terms.as<ColTerms>(), k11t, trow, tcol, obs, exact ? 1 : 0,
+                                                 ubase, umap, ctr, score, getenv("COOC_RS_EXP") ? atoi(getenv("COOC_RS_EXP")) : 0);
+  COOC_HIP_TRY(hipGetLastError());
+  const char *nx = getenv("COOC_RS_NO_NAN_EXIT");
+  const int32_t no_nan_exit = (nx && nx[0] == '1') ? 1 : 0;
+  const size_t lds = sizeof(double) * kR5Waves * size_t(topk + 1) + sizeof(int32_t) * kR5Waves * size_t(topk + 1);
+  int per_cu = 1;
+  COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rs_heap, 64 * kR5Waves, lds));
+  const int64_t want = (int64_t(M) + kR5Waves - 1) / kR5Waves;
+  const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * std::max(1, per_cu))));
+  k_rs_heap<<<grid, 64 * kR5Waves, lds, s>>>(M, src, sbase, score, ctr + 8, topk, out_size, out_val, out_score,
+                                             no_nan_exit);
+  COOC_HIP_TRY(hipGetLastError());
+  return Status::Ok();
+}
+
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                             const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
                             bool exact, int32_t topk, int64_t *obs3, DevBuf &terms, int32_t *out_size,
-                            int32_t *out_val, double *out_score) {
+                            int32_t *out_val, double *out_score, const int32_t *rank_of, bool unordered, int64_t nnz,
+                            bool whole_log) {
   COOC_HIP_TRY(hipMemsetAsync(obs3, 0, sizeof(int64_t) * 2, s));
   k_observed<<<std::min<unsigned>(blocks_for(M, 256), 1024), 256, 0, s>>>(rowsum, M, obs3);
   COOC_HIP_TRY(hipGetLastError());
@@ -1198,6 +1685,12 @@ Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, c
   if (dense)
     return launch_rescore_rows(s, nullptr, obs3 + 2, M, DenseRows{dense, M}, M, rowsum, obs3, exact, topk, terms,
                                out_size, out_val, out_score);
+  // the two passes for whole-log row sums (numeric heaps), k_rescore3 otherwise; COOC_RS_TWO_PASS=1 / 0 forces
+  static const int tp_env = getenv("COOC_RS_TWO_PASS") ? atoi(getenv("COOC_RS_TWO_PASS")) : -1;
+  const bool two_pass = (tp_env < 0 ? whole_log : tp_env != 0) && !unordered && nnz >= 0 && topk <= 1024;
+  if (two_pass)
+    return launch_rescore_two_pass(s, M, CsrRows{row_base, row_nnz, col, cnt}, rank_of, rowsum, obs3, exact, topk, nnz,
+                                   terms, out_size, out_val, out_score);
   return launch_rescore_rows(s, nullptr, obs3 + 2, M, CsrRows{row_base, row_nnz, col, cnt}, M, rowsum, obs3, exact,
                              topk, terms, out_size, out_val, out_score);
 }

@@ -46,7 +46,9 @@ Status launch_rescore(hipStream_t s, const int32_t *touched, const int64_t *scal
 Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, const int32_t *row_nnz,
                             const int32_t *col, const uint32_t *cnt, const uint32_t *dense, const int64_t *rowsum,
                             bool exact, int32_t topk,
-                            int64_t *obs3, DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score);
+                            int64_t *obs3, DevBuf &terms, int32_t *out_size, int32_t *out_val, double *out_score,
+                            const int32_t *rank_of = nullptr, bool unordered = true, int64_t nnz = -1,
+                            bool whole_log = false);
 
 // Sparse global rows (n_items >= 40,320; the rescorer's itemRows, ItemRowRescorer...java:35,171-177):
 // row a = len[a] (column, count) entries in ascending column order at base[a] of the arena (col, cnt).
