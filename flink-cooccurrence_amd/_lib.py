@@ -170,6 +170,9 @@ _SIGS = {
     "cooc_last_kernel_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
     "cooc_last_sort_rows": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "cooc_selftest_scan": (ctypes.c_int, [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), vp]),
+    "cooc_selftest_radix": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32, vp]),
+    "cooc_selftest_select": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp, vp]),
 }
 
 _lib = None

@@ -13,6 +13,9 @@ using cooc::Status;
 
 namespace cooc {
 Status selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, hipStream_t s, int64_t *h_err);  // cooc_verify.hip
+Status selftest_radix(const void *kin, const void *vin, void *kout, void *vout, int64_t n, int32_t key_bytes,
+                      int32_t bit0, int32_t bit1, int32_t desc, hipStream_t s);  // cooc_verify.hip
+Status selftest_select(const uint8_t *flag, int64_t n, int32_t *out, int32_t *n_sel, hipStream_t s);
 }
 
 namespace {
@@ -579,6 +582,26 @@ int cooc_selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, 
     int64_t e = 0;
     Status s = cooc::selftest_scan(d_in, d_out, n, flags, static_cast<hipStream_t>(hip_stream), &e);
     if (diag) *diag = e;
+    return s.ok() ? COOC_OK : fail(nullptr, s);
+  });
+}
+
+int cooc_selftest_radix(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out, int64_t n,
+                        int32_t key_bytes, int32_t bit0, int32_t bit1, int32_t descending, void *hip_stream) {
+  return guarded(nullptr, [&]() -> int {
+    if (n < 0 || (n > 0 && (!d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out)) ||
+        (key_bytes != 4 && key_bytes != 8) || bit0 < 0 || bit1 > 8 * key_bytes || bit0 > bit1)
+      return COOC_ERR_ARG;
+    Status s = cooc::selftest_radix(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n, key_bytes, bit0, bit1, descending,
+                                    static_cast<hipStream_t>(hip_stream));
+    return s.ok() ? COOC_OK : fail(nullptr, s);
+  });
+}
+
+int cooc_selftest_select(const uint8_t *d_flags, int64_t n, int32_t *d_out, int32_t *d_n_sel, void *hip_stream) {
+  return guarded(nullptr, [&]() -> int {
+    if (n < 0 || !d_n_sel || (n > 0 && (!d_flags || !d_out))) return COOC_ERR_ARG;
+    Status s = cooc::selftest_select(d_flags, n, d_out, d_n_sel, static_cast<hipStream_t>(hip_stream));
     return s.ok() ? COOC_OK : fail(nullptr, s);
   });
 }

@@ -38,6 +38,7 @@
 
 #include "cooc_device.h"
 #include "cooc_scan.h"
+#include "cooc_radix.h"
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -2951,15 +2952,25 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   COOC_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(PlanTotals), s));
   COOC_HIP_TRY(hipMemsetAsync(epre, 0, sizeof(int64_t), s));
 
-  // temp storage of the hipCUB calls
+  // the planner's sorts and its select: hand-written (cooc_radix.h) unless COOC_LIB_SORTS=1 (the hipCUB calls,
+  // an A/B knob)
+  static const bool lib_sorts = [] {
+    const char *e = getenv("COOC_LIB_SORTS");
+    return e && e[0] == '1';
+  }();
   const int kb = bits_for(M);
   size_t tmp = 0, q = 0;
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n1), 0, kb, s));
-  tmp = std::max(tmp, q);
-  COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, order_keys_.as<uint64_t>(),
-                                                            order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
-                                                            order_.as<int32_t>() + M, M, 0, 64, s));
-  tmp = std::max(tmp, q);
+  if (lib_sorts) {
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, q, keys_in, keys, vals_in, vals, int(n1), 0, kb, s));
+    tmp = std::max(tmp, q);
+    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, q, order_keys_.as<uint64_t>(),
+                                                              order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
+                                                              order_.as<int32_t>() + M, M, 0, 64, s));
+    tmp = std::max(tmp, q);
+  } else {
+    tmp = std::max({radix_sort_tmp_bytes<uint32_t, uint32_t>(n1), radix_sort_tmp_bytes<uint64_t, int32_t>(M),
+                    select_tmp_bytes(M)});
+  }
   uint64_t *plen = sp_pbase_.as<uint64_t>(), *pbase = plen + U1;
   COOC_TRY(sort_tmp_.reserve(tmp));
   // the planner's prefix sums (cooc_scan.h): tile statuses for the largest of them, reserved once up front
@@ -2989,7 +3000,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
       if (U > 0) k_sp_contribs<<<nblocks(waves * 64, 256), 256, 0, s>>>(U, up, items, M, keys_in, vals_in);
       if (n > 0) {
         size_t b = sort_tmp_.cap;
-        COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, kb, s));
+        if (lib_sorts)
+          COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n), 0, kb, s));
+        else
+          COOC_TRY(radix_sort_pairs(keys_in, vals_in, keys, vals, n, 0, kb, false, sort_tmp_.p, s));
         COOC_TRY(launch_scan<true>(ScanUserLen{vals, ulen}, epre + 1, n, scan_st, scan_err, s));
       }
       k_sp_row_ptr<<<nblocks(int64_t(M) + 1, 256), 256, 0, s>>>(keys, n, M, row_ptr);
@@ -3000,15 +3014,23 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     k_rank_keys<<<nblocks(M, 256), 256, 0, s>>>(row_ptr, owner ? freq : nullptr, M, rk_in, ids, hot);
     size_t b = 0, b2 = 0;
     const int fb = bits_for(std::max<int64_t>(n_tot, 1) + 1);
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, rk_in, rk_out, ids, order, M, 0, fb, s));
     hipcub::CountingInputIterator<int32_t> from0(0);
-    COOC_HIP_TRY(hipcub::DeviceSelect::If(nullptr, b2, from0, hot_col, n_sel, M, IsHot{hot}, s));
+    if (lib_sorts) {
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, rk_in, rk_out, ids, order, M, 0, fb, s));
+      COOC_HIP_TRY(hipcub::DeviceSelect::If(nullptr, b2, from0, hot_col, n_sel, M, IsHot{hot}, s));
+    }
     COOC_TRY(sort_tmp_.reserve(std::max({b, b2, tmp})));
     b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, rk_in, rk_out, ids, order, M, 0, fb, s));
+    if (lib_sorts)
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, rk_in, rk_out, ids, order, M, 0, fb, s));
+    else
+      COOC_TRY(radix_sort_pairs(rk_in, ids, rk_out, order, M, 0, fb, true, sort_tmp_.p, s));
     k_hot_mark<<<nblocks(kTW, 256), 256, 0, s>>>(order, kTW, hot);
     b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceSelect::If(sort_tmp_.p, b, from0, hot_col, n_sel, M, IsHot{hot}, s));  // kTW of them
+    if (lib_sorts)
+      COOC_HIP_TRY(hipcub::DeviceSelect::If(sort_tmp_.p, b, from0, hot_col, n_sel, M, IsHot{hot}, s));  // kTW of them
+    else
+      COOC_TRY(select_flagged(hot, M, hot_col, n_sel, sort_tmp_.p, s));
     // ids that already put (nearly) every hot item in tile 0 keep their order: the relabel would only add
     // its lookups (an item-ranked log; measured 4 ms per C3 share)
     {
@@ -3090,7 +3112,10 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
   // 2. regroup by row (the keyBy(itemA) of FlinkCooccurrences.java:152); 3. row pointer; 4. pair work
   if (n_c > 0 && !sorted_early) {
     size_t b = sort_tmp_.cap;
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n_c), 0, kb, s));
+    if (lib_sorts)
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, b, keys_in, keys, vals_in, vals, int(n_c), 0, kb, s));
+    else
+      COOC_TRY(radix_sort_pairs(keys_in, vals_in, keys, vals, n_c, 0, kb, false, sort_tmp_.p, s));
     COOC_TRY(launch_scan<true>(ScanUserLen{vals, ulen}, epre + 1, n_c, scan_st, scan_err, s));
   }
   int64_t *spre = nullptr;  // a window's self flags, prefix in row order
@@ -3153,9 +3178,13 @@ Status Counter::run_sparse(int64_t U, const int64_t *up, const int32_t *items, i
     // five 8-bit passes instead of eight; the same order)
     size_t b = sort_tmp_.cap;
     const int wb = std::min(64, bits_for(work_total + 1));
-    COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, order_keys_.as<uint64_t>(),
-                                                              order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
-                                                              order_.as<int32_t>() + M, M, 0, wb, s));
+    if (lib_sorts)
+      COOC_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(sort_tmp_.p, b, order_keys_.as<uint64_t>(),
+                                                                order_keys_.as<uint64_t>() + M, order_.as<int32_t>(),
+                                                                order_.as<int32_t>() + M, M, 0, wb, s));
+    else
+      COOC_TRY(radix_sort_pairs(order_keys_.as<uint64_t>(), order_.as<int32_t>(), order_keys_.as<uint64_t>() + M,
+                                order_.as<int32_t>() + M, M, 0, wb, true, sort_tmp_.p, s));
     k_sp_gather_nwork<<<nblocks(M, 256), 256, 0, s>>>(order_.as<int32_t>() + M, row_nch_.as<int32_t>(), M,
                                                       ord_nch_.as<int32_t>());
     COOC_TRY(launch_scan<false>(ScanI32{ord_nch_.as<int32_t>()}, ord_cbase_.as<int32_t>(), M, scan_st, scan_err, s));

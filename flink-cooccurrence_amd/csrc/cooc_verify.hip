@@ -15,6 +15,7 @@
 // (oracle/cooc_oracle.c, oc_row_checksums) without copying the matrix out.
 #include "cooc_device.h"
 #include "cooc_scan.h"
+#include "cooc_radix.h"
 
 #include <algorithm>
 
@@ -206,6 +207,34 @@ Status selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, hi
     st = Status{3, "hipMemcpyAsync"};
   if (st.ok() && hipStreamSynchronize(s) != hipSuccess) st = Status{3, "hipStreamSynchronize"};
   (void)hipFree(ws);
+  return st;
+}
+
+// The planner's radix sort (cooc_radix.h) on a caller's arrays: 32- or 64-bit keys, 32-bit values, any bit range,
+// ascending or descending (cooc_selftest_radix); and its flag compaction (cooc_selftest_select).
+Status selftest_radix(const void *kin, const void *vin, void *kout, void *vout, int64_t n, int32_t key_bytes,
+                      int32_t bit0, int32_t bit1, int32_t desc, hipStream_t s) {
+  if (n <= 0) return Status::Ok();
+  void *tmp = nullptr;
+  const size_t bytes = key_bytes == 8 ? radix_sort_tmp_bytes<uint64_t, uint32_t>(n) : radix_sort_tmp_bytes<uint32_t, uint32_t>(n);
+  COOC_HIP_TRY(hipMalloc(&tmp, bytes));
+  Status st = key_bytes == 8
+                  ? radix_sort_pairs(static_cast<const uint64_t *>(kin), static_cast<const uint32_t *>(vin),
+                                     static_cast<uint64_t *>(kout), static_cast<uint32_t *>(vout), n, bit0, bit1,
+                                     desc != 0, tmp, s)
+                  : radix_sort_pairs(static_cast<const uint32_t *>(kin), static_cast<const uint32_t *>(vin),
+                                     static_cast<uint32_t *>(kout), static_cast<uint32_t *>(vout), n, bit0, bit1,
+                                     desc != 0, tmp, s);
+  if (st.ok() && hipStreamSynchronize(s) != hipSuccess) st = Status{3, "hipStreamSynchronize"};
+  (void)hipFree(tmp);
+  return st;
+}
+Status selftest_select(const uint8_t *flag, int64_t n, int32_t *out, int32_t *n_sel, hipStream_t s) {
+  void *tmp = nullptr;
+  COOC_HIP_TRY(hipMalloc(&tmp, select_tmp_bytes(std::max<int64_t>(n, 1))));
+  Status st = select_flagged(flag, n, out, n_sel, tmp, s);
+  if (st.ok() && hipStreamSynchronize(s) != hipSuccess) st = Status{3, "hipStreamSynchronize"};
+  (void)hipFree(tmp);
   return st;
 }
 

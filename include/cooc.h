@@ -499,6 +499,16 @@ COOC_API int cooc_last_sort_rows(cooc_ctx *ctx, int64_t *rows, int64_t *pairs);
  * and summed its prefix from the input). */
 COOC_API int cooc_selftest_scan(const void *d_in, void *d_out, int64_t n, int32_t flags, int64_t *diag,
                                 void *hip_stream);
+/* Self-test of the planner's radix sort (no context): (d_keys_out, d_vals_out)[0, n) = (d_keys_in, d_vals_in)
+ * stably sorted by key bits [bit0, bit1) (descending != 0: by the complemented bits, equal keys in input order),
+ * keys of key_bytes (4 or 8) bytes, 32-bit values; device arrays, on hip_stream (then synchronised). */
+COOC_API int cooc_selftest_radix(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out,
+                                 int64_t n, int32_t key_bytes, int32_t bit0, int32_t bit1, int32_t descending,
+                                 void *hip_stream);
+/* Self-test of the planner's flag compaction: d_out[0, *d_n_sel) = the indices i < n with d_flags[i] != 0,
+ * ascending (device arrays; *d_n_sel is a device int32). */
+COOC_API int cooc_selftest_select(const uint8_t *d_flags, int64_t n, int32_t *d_out, int32_t *d_n_sel,
+                                  void *hip_stream);
 
 #ifdef __cplusplus
 }
