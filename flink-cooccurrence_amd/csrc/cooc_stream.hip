@@ -1046,12 +1046,13 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
       if (exp & 32) continue;  // (timing experiment: the items' overhead alone)
       const int32_t ke = min(T, kb + kRsP);
       int32_t nq = 0;  // queued entries (wave-uniform)
-      int32_t cA[kRsU];
+      int32_t cA[kRsU], rA[kRsU];
       uint32_t vA[kRsU];
 #pragma unroll
       for (int u = 0; u < kRsU; u++) {  // round 0's entries
         const int32_t k = kb + u * 64 + lane;
         const int r = rs_item_row(it, k);
+        rA[u] = r;
         cA[u] = 0;
         vA[u] = 0u;
         if (k < ke) {
@@ -1064,15 +1065,17 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
 #pragma unroll
         for (int u = 0; u < kRsU; u++)  // the current round's column terms
           if (k0 + u * 64 + lane < ke && vA[u] != 0u) h[u] = (exp & 4) ? ColTerms{cA[u], 1.0, 2.0, 3.0} : cterm[cA[u]];
-        int32_t cB[kRsU];
+        int32_t cB[kRsU], rB[kRsU];
         uint32_t vB[kRsU];
 #pragma unroll
         for (int u = 0; u < kRsU; u++) {  // the next round's entries (the row of entry k: the last with off <= k)
           const int32_t k = k0 + (kRsU + u) * 64 + lane;
           cB[u] = 0;
           vB[u] = 0u;
+          rB[u] = 0;
           if (k < ke) {
             const int r = rs_item_row(it, k);
+            rB[u] = r;
             cB[u] = src.col[it.src[r] + (k - it.off[r])];
             vB[u] = src.cnt[it.src[r] + (k - it.off[r])];
           }
@@ -1080,7 +1083,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
 #pragma unroll
         for (int u = 0; u < kRsU; u++) {
           const int32_t k = k0 + u * 64 + lane;
-          const int r = rs_item_row(it, k);
+          const int r = rA[u];  // (found when the entry was loaded)
           const int64_t k11 = exact ? int64_t(vA[u]) : int64_t(int16_t(uint16_t(vA[u])));
           const bool valid = k < ke;
           const bool slow = valid && vA[u] != 0u && k11 != 1;
@@ -1120,6 +1123,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
         for (int u = 0; u < kRsU; u++) {
           cA[u] = cB[u];
           vA[u] = vB[u];
+          rA[u] = rB[u];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -78,10 +78,20 @@ def main():
                 kms.append(core.last_kernel_ms())
         P_all += int(res.observed)
         out["parts"][part] = {"ms": float(np.median(ms)), "k_sp_main_ms": float(np.median(kms)),
+                              "outside_counting_span_ms": float(np.median(ms)) - float(np.median(kms)),
                               "ordered_pairs": int(res.observed), "nnz": int(res.nnz),
                               "pairs_per_s": int(res.observed) / (float(np.median(ms)) * 1e-3)}
     out["interactions"] = N
     out["item_counts_ms_per_rank_share"] = freq_ms
+    # the all-gather each rank would run first (not measured here): the other ranks' item ids (4 B each) and
+    # user pointers (8 B per user), modelled over xGMI at LINK_GBPS per link (MI355X: 7 links per GPU in an
+    # 8-GPU node) -- received from all 7 peers at once (direct / mesh) or one link per step (ring)
+    link_gbps = float(os.environ.get("LINK_GBPS", "153"))
+    recv = (N - N // args.world) * 4 + (args.world * U8 - U8) * 8
+    out["allgather_model"] = {"bytes_received_per_rank": recv, "link_GBps": link_gbps,
+                              "mesh_ms": recv / (min(7, args.world - 1) * link_gbps * 1e9) * 1e3,
+                              "ring_ms": recv / (link_gbps * 1e9) * 1e3,
+                              "note": "modelled, not measured: bytes / bandwidth, no latency or protocol overhead"}
     print(json.dumps(out), flush=True)
     core.close()
 
