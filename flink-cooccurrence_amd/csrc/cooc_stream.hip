@@ -1136,8 +1136,16 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
 }
 
 // pass 2: one wave per row, its columns and scores streamed through a kR5Slots-slot LDS-DMA ring (3 DMAs per step of
-// 64 entries, issued kR5L steps ahead; counted waits as in k_rescore3), the heap fed in column order
-constexpr int kR5Waves = 4, kR5Slots = 8, kR5L = 6;
+// 64 entries, issued kR5L steps ahead, 9 KB in flight per wave: the Zipf head's rows of ~1e6 entries run on one wave
+// each; counted waits as in k_rescore3), the heap fed in column order
+#ifndef COOC_R5_SLOTS
+#define COOC_R5_SLOTS 16  // (A/B builds; 8 slots / 6 ahead: 13.0 ms on the owner unit, 16 / 10-14: 11.8)
+#define COOC_R5_L 12
+#endif
+#ifndef COOC_R5_WAVES
+#define COOC_R5_WAVES 4
+#endif
+constexpr int kR5Waves = COOC_R5_WAVES, kR5Slots = COOC_R5_SLOTS, kR5L = COOC_R5_L;
 struct R5Slot {
   uint32_t col[64];
   uint32_t slo[64];
@@ -1148,7 +1156,8 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
                                                           const uint64_t *__restrict__ score,
                                                           unsigned long long *__restrict__ row_ctr, int32_t topk,
                                                           int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
-                                                          double *__restrict__ out_score, int32_t no_nan_exit) {
+                                                          double *__restrict__ out_score, int32_t no_nan_exit,
+                                                          int64_t exp_skip) {
   __shared__ R5Slot ring[kR5Waves][kR5Slots];
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1163,7 +1172,7 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
     }
     const int64_t t = t_next++;
     if (t >= n_rows) break;
-    const int64_t n = src.size(int32_t(t));
+    const int64_t n = (exp_skip > 0 && src.size(int32_t(t)) > exp_skip) ? 0 : src.size(int32_t(t));  // (timing experiment)
     int32_t size = 0;
     double least = 0.0;
     if (n > 0) {
@@ -1672,7 +1681,7 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   const int64_t want = (int64_t(M) + kR5Waves - 1) / kR5Waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * std::max(1, per_cu))));
   k_rs_heap<<<grid, 64 * kR5Waves, lds, s>>>(M, src, sbase, score, ctr + 8, topk, out_size, out_val, out_score,
-                                             no_nan_exit);
+                                             no_nan_exit, getenv("COOC_RS_HEAP_SKIP") ? atoll(getenv("COOC_RS_HEAP_SKIP")) : 0);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }
