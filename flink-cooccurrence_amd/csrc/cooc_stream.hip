@@ -905,7 +905,7 @@ __device__ inline int rs_item_row(const RsItem &it, int32_t k) {
 __device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const double *xt,
                                      const double *__restrict__ k11t, const double *__restrict__ trow,
                                      const double *__restrict__ tcol, int64_t observed, int32_t exact,
-                                     uint64_t *__restrict__ score) {
+                                     uint64_t *__restrict__ score, int32_t *__restrict__ nanrow) {
 #pragma clang fp contract(off)
   if (!on) return;
   const int32_t k = it.qk[j];
@@ -938,6 +938,7 @@ __device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const dou
     x_21 = (k21 >= -32768 && k21 < 32768) ? k11t[k21 + 32768] : xlogx(k21);
   }
   const double sc = llr_terms(x_all, it.rt[r][0], x_2122, it.qxrs[j], x_1222, x_11, x_12, x_21, xlogx(k22));
+  if (sc != sc) nanrow[it.t0 + r] = 1;
   score[it.dst[r] + (k - it.off[r])] = uint64_t(__double_as_longlong(sc));
 }
 // Work units of pass 1: the items (64 consecutive rows x one block; queue q = block % 8 holds its blocks' items in
@@ -981,7 +982,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
                                                   const int64_t *__restrict__ obs, int32_t exact,
                                                   const int64_t *__restrict__ ubase, const int32_t *__restrict__ umap,
                                                   unsigned long long *__restrict__ qctr, uint64_t *__restrict__ score,
-                                                  int32_t exp) {
+                                                  int32_t *__restrict__ nanrow, int32_t exp) {
 #pragma clang fp contract(off)
   __shared__ RsItem items[4];
   __shared__ double xt[2 * kRsXT];
@@ -1096,6 +1097,9 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
                                                              h[u].x_or2, 0.0, it.rt[r][3], h[u].x_rs1,
                                                              (exp & 2) ? double(k22) : xlogx(k22))));
             }
+            if ((bits & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (bits & 0xFFFFFFFFFFFFFull) != 0 &&
+                bits != kRsZero)
+              nanrow[it.t0 + r] = 1;  // (a NaN score: the row's heap pass cannot be split, k_rs_heap)
             if (!(exp & 8) || bits == 0x1234ull) score[it.dst[r] + (k - it.off[r])] = bits;
           }
           const uint64_t sm = __ballot(slow);
@@ -1114,7 +1118,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             nq -= 64;
-            rs_score_slow(it, nq + lane, true, xt, k11t, trow, tcol, observed, exact, score);
+            rs_score_slow(it, nq + lane, true, xt, k11t, trow, tcol, observed, exact, score, nanrow);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
           }
@@ -1128,7 +1132,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      rs_score_slow(it, lane, lane < nq, xt, k11t, trow, tcol, observed, exact, score);
+      rs_score_slow(it, lane, lane < nq, xt, k11t, trow, tcol, observed, exact, score, nanrow);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
@@ -1146,79 +1150,187 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
 #define COOC_R5_WAVES 4
 #endif
 constexpr int kR5Waves = COOC_R5_WAVES, kR5Slots = COOC_R5_SLOTS, kR5L = COOC_R5_L;
-struct R5Slot {
-  uint32_t col[64];
+struct R5Slot {  // a step's scores (the heap holds entry indices: the columns are read for the k kept, at the end)
   uint32_t slo[64];
   uint32_t shi[64];
 };
+// Rows longer than kRsLong entries whose scores hold no NaN are cut into segments of kRsSeg entries, one wave each:
+// a segment feeds a heap of its own from empty and keeps, in order, every entry that heap could take (at most
+// kRsCand; more: the row is replayed whole).  An entry a full segment heap refuses (score <= its root) is refused by
+// the row's heap too, whose root is the k-th largest score of a superset of the entries before it (a total order:
+// no NaN); refused entries change nothing, so the row's heap fed only the kept entries, in order, ends exactly as
+// fed every entry.  The wave that finishes a row's last segment replays the kept entries into the row's heap.
+constexpr int64_t kRsLong = 65536;
+constexpr int32_t kRsSeg = 16384, kRsCand = 2048;
+__global__ void k_rs_seg_count(int64_t n_rows, CsrRows src, const int32_t *__restrict__ nanrow, int64_t long_thr,
+                               int32_t seg_len, int32_t *__restrict__ nseg) {
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t > n_rows) return;
+  if (t == n_rows) {
+    nseg[t] = 0;
+    return;
+  }
+  const int64_t n = src.size(int32_t(t));
+  nseg[t] = (n > long_thr && !nanrow[t]) ? int32_t((n + seg_len - 1) / seg_len) : 0;
+}
+
+// Streams entries [i0, i1) of a row through the wave's ring into its heap (hv, hs, size, least); kSeg: also records
+// the entries offered (a superset of those taken) as segment-relative u16 indices in cand[0, kRsCand), *nc counting
+// them all.
+template <bool kSeg>
+__device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint64_t *__restrict__ score, int64_t rb, int64_t sb,
+                                 int64_t i0, int64_t i1, int32_t topk, int32_t *hv, double *hs, int32_t &size,
+                                 double &least, int32_t no_nan_exit, uint16_t *__restrict__ cand, int32_t cand_cap,
+                                 int32_t &nc) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t n = i1 - i0;
+  const int64_t nsteps = (n + 63) >> 6;
+  for (int64_t j = -kR5L; j < nsteps; j++) {
+    {  // step j + L (clamped to the range's last entry past its end: every step issues 2 DMAs)
+      const int64_t jl = j + kR5L;
+      const int64_t e = i0 + min(jl * 64 + lane, n - 1);
+      R5Slot &sl = rg[jl & (kR5Slots - 1)];
+      const uint32_t *sp = reinterpret_cast<const uint32_t *>(score + sb + e);
+      __builtin_amdgcn_global_load_lds(sp, R3_LDS(sl.slo), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(sp + 1, R3_LDS(sl.shi), 4, 0, 0);
+    }
+    if (j < 0) continue;
+    r3_wait_vm<2 * kR5L>();  // step j's DMAs (issued L steps ago) have landed
+    const R5Slot &sl = rg[j & (kR5Slots - 1)];
+    const bool in_row = j * 64 + lane < n;
+    const uint64_t bits = in_row ? (uint64_t(r3_rd32(&sl.shi[lane])) << 32) | uint64_t(r3_rd32(&sl.slo[lane]))
+                                 : kRsZero;
+    const int32_t c = bits != kRsZero ? int32_t(i0 + j * 64 + lane) : -1;  // the entry's index in the row
+    const double sc = __longlong_as_double(int64_t(bits));
+    uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
+    if (kSeg) {
+      if ((m >> lane) & 1ull) {
+        const int32_t q = nc + int32_t(__popcll(m & lt));
+        if (q < cand_cap) cand[q] = uint16_t(j * 64 + lane);
+      }
+      nc += int32_t(__popcll(m));
+    }
+    while (m) {  // in lane order: the reference's sequential offers
+      const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+      m &= m - 1;
+      const double s_l = __shfl(sc, l, 64);
+      const int32_t c_l = __shfl(c, l, 64);
+      if (size < topk) {
+        heap_add(hv, hs, size, c_l, s_l);
+      } else if (s_l > hs[1]) {
+        heap_update(hv, hs, size, c_l, s_l);
+      }
+      least = hs[1];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
+  }
+  r3_wait_vm<0>();  // (the ring's last DMAs: the next range reuses the slots)
+}
+
+// pass 2: units [0, n_seg) are the long rows' segments, then one unit per row (a long row's own unit is skipped);
+// one wave per unit, units taken 4 at a time.  A row streams its scores through a kR5Slots-slot LDS-DMA ring (2 DMAs
+// per step of 64 entries issued kR5L steps ahead; counted waits as in k_rescore3) into the heap in column order (the
+// sequential loop of ItemRowRescorer...java:199-223), ending at a full heap with a NaN root.  The heap orders by
+// score alone (IntDoublePriorityQueue.java:132-205), so it holds entry indices and the k kept columns are read at
+// the end: 8 B streamed per entry, not 12.
 __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRows src,
                                                           const int64_t *__restrict__ sbase,
                                                           const uint64_t *__restrict__ score,
                                                           unsigned long long *__restrict__ row_ctr, int32_t topk,
                                                           int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
                                                           double *__restrict__ out_score, int32_t no_nan_exit,
-                                                          int64_t exp_skip) {
+                                                          int64_t exp_skip, const int64_t *__restrict__ segp,
+                                                          uint16_t *__restrict__ cand, int32_t *__restrict__ ncand,
+                                                          int32_t *__restrict__ segdone, int32_t seg_len,
+                                                          int32_t cand_cap) {
   __shared__ R5Slot ring[kR5Waves][kR5Slots];
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + kR5Waves * (topk + 1)) + int64_t(wave) * (topk + 1);
   R5Slot *rg = ring[wave];
-  int64_t t_next = 0, t_end = 0;
+  const int64_t n_seg = segp[n_rows], n_units = n_seg + n_rows;
+  int64_t u_next = 0, u_end = 0;
   for (;;) {
-    if (t_next == t_end) {
-      t_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 4ull)) : 0ll, 0, 64);
-      t_end = t_next + 4;
+    if (u_next == u_end) {
+      u_next = __shfl(lane == 0 ? int64_t(atomicAdd(row_ctr, 4ull)) : 0ll, 0, 64);
+      u_end = u_next + 4;
     }
-    const int64_t t = t_next++;
-    if (t >= n_rows) break;
-    const int64_t n = (exp_skip > 0 && src.size(int32_t(t)) > exp_skip) ? 0 : src.size(int32_t(t));  // (timing experiment)
-    int32_t size = 0;
+    const int64_t u = u_next++;
+    if (u >= n_units) break;
+    int32_t size = 0, nc = 0;
     double least = 0.0;
-    if (n > 0) {
-      const int64_t rb = src.base(int32_t(t)), sb = sbase[t];
-      const int64_t nsteps = (n + 63) >> 6;
-      for (int64_t j = -kR5L; j < nsteps; j++) {
-        {  // step j + L (clamped to the row's last entry past its end: every step issues 3 DMAs)
-          const int64_t jl = j + kR5L;
-          const int64_t e = min(jl * 64 + lane, n - 1);
-          R5Slot &sl = rg[jl & (kR5Slots - 1)];
-          const uint32_t *sp = reinterpret_cast<const uint32_t *>(score + sb + e);
-          __builtin_amdgcn_global_load_lds(src.col + rb + e, R3_LDS(sl.col), 4, 0, 0);
-          __builtin_amdgcn_global_load_lds(sp, R3_LDS(sl.slo), 4, 0, 0);
-          __builtin_amdgcn_global_load_lds(sp + 1, R3_LDS(sl.shi), 4, 0, 0);
-        }
-        if (j < 0) continue;
-        r3_wait_vm<3 * kR5L>();  // step j's DMAs (issued L steps ago) have landed
-        const R5Slot &sl = rg[j & (kR5Slots - 1)];
-        const bool in_row = j * 64 + lane < n;
-        const uint64_t bits = in_row ? (uint64_t(r3_rd32(&sl.shi[lane])) << 32) | uint64_t(r3_rd32(&sl.slo[lane]))
-                                     : kRsZero;
-        const int32_t c = bits != kRsZero ? int32_t(r3_rd32(&sl.col[lane])) : -1;
-        const double sc = __longlong_as_double(int64_t(bits));
-        uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
-        while (m) {  // in lane order: the reference's sequential offers
-          const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
-          m &= m - 1;
-          const double s_l = __shfl(sc, l, 64);
-          const int32_t c_l = __shfl(c, l, 64);
-          if (size < topk) {
-            heap_add(hv, hs, size, c_l, s_l);
-          } else if (s_l > hs[1]) {
-            heap_update(hv, hs, size, c_l, s_l);
-          }
-          least = hs[1];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
+    int64_t t;
+    if (u < n_seg) {  // a segment: its own heap, its offered entries kept
+      int64_t lo = 0, hi = n_rows;  // t: the last row with segp[t] <= u
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (segp[mid] <= u) lo = mid; else hi = mid;
       }
-      r3_wait_vm<0>();  // (the ring's last DMAs: the next row reuses the slots)
+      t = lo;
+      const int64_t n = src.size(int32_t(t)), rb = src.base(int32_t(t)), sb = sbase[t];
+      const int64_t s0 = segp[t], ns = segp[t + 1] - s0, i0 = (u - s0) * seg_len;
+      rs_stream<true>(rg, src, score, rb, sb, i0, min(n, i0 + seg_len), topk, hv, hs, size, least, 1,
+                      cand + u * kRsCand, cand_cap, nc);
+      if (lane == 0) ncand[u] = nc;
+      __threadfence();  // (the kept entries and their count, before the row's segment count)
+      const int32_t done = __shfl(lane == 0 ? atomicAdd(segdone + t, 1) : 0, 0, 64);
+      if (done != ns - 1) continue;
+      __threadfence();  // the last segment of the row: every segment's kept entries are visible
+      size = 0;
+      least = 0.0;
+      bool whole = false;
+      for (int64_t q = 0; q < ns; q++) whole |= ncand[s0 + q] > cand_cap;
+      if (whole) {
+        rs_stream<false>(rg, src, score, rb, sb, 0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0, nc);
+      } else {
+        for (int64_t q = 0; q < ns; q++) {
+          const int32_t cq = ncand[s0 + q];
+          for (int32_t j0 = 0; j0 < cq; j0 += 64) {
+            int32_t c = -1;
+            double sc = 0.0;
+            if (j0 + lane < cq) {
+              const int64_t i = q * seg_len + cand[(s0 + q) * kRsCand + j0 + lane];
+              c = int32_t(i);
+              sc = __longlong_as_double(int64_t(score[sb + i]));
+            }
+            uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
+            while (m) {
+              const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+              m &= m - 1;
+              const double s_l = __shfl(sc, l, 64);
+              const int32_t c_l = __shfl(c, l, 64);
+              if (size < topk) {
+                heap_add(hv, hs, size, c_l, s_l);
+              } else if (s_l > hs[1]) {
+                heap_update(hv, hs, size, c_l, s_l);
+              }
+              least = hs[1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+    } else {  // a row
+      t = u - n_seg;
+      const int64_t n0 = src.size(int32_t(t));
+      if (segp[t + 1] > segp[t]) continue;  // (its segments serve it)
+      const int64_t n = (exp_skip > 0 && n0 > exp_skip) ? 0 : n0;  // (timing experiment)
+      if (n > 0)
+        rs_stream<false>(rg, src, score, src.base(int32_t(t)), sbase[t], 0, n, topk, hv, hs, size, least, no_nan_exit,
+                         nullptr, 0, nc);
     }
     out_size[t] = size;
-    for (int32_t i = lane; i < size; i += 64) {
-      out_val[t * topk + i] = hv[i + 1];
-      out_score[t * topk + i] = hs[i + 1];
+    if (size > 0) {
+      const int64_t rb = src.base(int32_t(t));
+      for (int32_t i = lane; i < size; i += 64) {
+        out_val[t * topk + i] = src.col[rb + hv[i + 1]];
+        out_score[t * topk + i] = hs[i + 1];
+      }
     }
   }
 }
@@ -1629,7 +1741,16 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   const size_t o_ubase = al(o_units + sizeof(int32_t) * size_t(n_items_ + 1));
   const size_t o_ustate = al(o_ubase + sizeof(int64_t) * size_t(n_items_ + 1));
   const size_t o_umap = al(o_ustate + sizeof(unsigned long long) * size_t(scan_state_words(n_items_ + 1) + 1));
-  const size_t o_score = al(o_umap + sizeof(int32_t) * size_t(n_items_ + std::max<int64_t>(nnz, 0) / kRsP + 1));
+  const int64_t seg_min = getenv("COOC_RS_SPLIT_SEG") ? std::min<int64_t>(kRsSeg, std::max(64, atoi(getenv("COOC_RS_SPLIT_SEG")))) : kRsSeg;
+  const int64_t long_min = getenv("COOC_RS_SPLIT_LONG") ? std::max<int64_t>(1, atoll(getenv("COOC_RS_SPLIT_LONG"))) : kRsLong;
+  const int64_t n_seg_max = std::max<int64_t>(nnz, 0) / seg_min + std::max<int64_t>(nnz, 0) / long_min + 1;
+  const size_t o_nanrow = al(o_umap + sizeof(int32_t) * size_t(n_items_ + std::max<int64_t>(nnz, 0) / kRsP + 1));
+  const size_t o_nseg = al(o_nanrow + sizeof(int32_t) * size_t(M));  // (nanrow, then segdone: zeroed together)
+  const size_t o_segdone = al(o_nseg + sizeof(int32_t) * size_t(M + 1));
+  const size_t o_segp = al(o_segdone + sizeof(int32_t) * size_t(M));
+  const size_t o_ncand = al(o_segp + sizeof(int64_t) * size_t(M + 1));
+  const size_t o_cand = al(o_ncand + sizeof(int32_t) * size_t(n_seg_max));
+  const size_t o_score = al(o_cand + sizeof(uint16_t) * size_t(n_seg_max) * kRsCand);
   COOC_TRY(terms.reserve(o_score + sizeof(uint64_t) * size_t(std::max<int64_t>(nnz, 1))));
   char *base = static_cast<char *>(terms.p);
   auto *ctr = reinterpret_cast<unsigned long long *>(base + o_ctr);  // [0, 8) pass-1 queues, [8] pass-2 rows
@@ -1644,7 +1765,15 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   auto *ustate = reinterpret_cast<unsigned long long *>(base + o_ustate);
   auto *umap = reinterpret_cast<int32_t *>(base + o_umap);
   auto *tcol = reinterpret_cast<double *>(base + o_tcol);
+  auto *nanrow = reinterpret_cast<int32_t *>(base + o_nanrow);
+  auto *nseg = reinterpret_cast<int32_t *>(base + o_nseg);
+  auto *segdone = reinterpret_cast<int32_t *>(base + o_segdone);
+  auto *segp = reinterpret_cast<int64_t *>(base + o_segp);
+  auto *ncand = reinterpret_cast<int32_t *>(base + o_ncand);
+  auto *cand = reinterpret_cast<uint16_t *>(base + o_cand);
   COOC_HIP_TRY(hipMemsetAsync(ctr, 0, 256, s));
+  COOC_HIP_TRY(hipMemsetAsync(nanrow, 0, sizeof(int32_t) * size_t(std::max(M, 1)), s));
+  COOC_HIP_TRY(hipMemsetAsync(segdone, 0, sizeof(int32_t) * size_t(std::max(M, 1)), s));
   k_col_terms<<<blocks_for(M, 256), 256, 0, s>>>(M, grs, obs, exact ? 1 : 0, terms.as<ColTerms>());
   k_k11_terms<<<256, 256, 0, s>>>(obs, exact ? 1 : 0, k11t);
   COOC_HIP_TRY(hipGetLastError());
@@ -1671,8 +1800,23 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   int per_cu1 = 1;  // (a persistent grid: the work comes from the queues)
   COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, k_rs_score, 256, 0));
   k_rs_score<<<unsigned(n_cu) * unsigned(std::max(1, per_cu1)), 256, 0, s>>>(M, src, bp, sbase, grs, terms.as<ColTerms>(), k11t, trow, tcol, obs, exact ? 1 : 0,
-                                                 ubase, umap, ctr, score, getenv("COOC_RS_EXP") ? atoi(getenv("COOC_RS_EXP")) : 0);
+                                                 ubase, umap, ctr, score, nanrow,
+                                                 getenv("COOC_RS_EXP") ? atoi(getenv("COOC_RS_EXP")) : 0);
   COOC_HIP_TRY(hipGetLastError());
+  // the long rows' segments (COOC_RS_SPLIT=0: none) and their prefix
+  // (test knobs: COOC_RS_SPLIT_LONG / _SEG / _CAP shrink the thresholds so small logs take the split path)
+  const bool split = !(getenv("COOC_RS_SPLIT") && getenv("COOC_RS_SPLIT")[0] == '0');
+  const int64_t long_thr = getenv("COOC_RS_SPLIT_LONG") ? std::max<int64_t>(1, atoll(getenv("COOC_RS_SPLIT_LONG"))) : kRsLong;
+  const int32_t seg_len = getenv("COOC_RS_SPLIT_SEG") ? std::min(kRsSeg, std::max(64, atoi(getenv("COOC_RS_SPLIT_SEG")))) : kRsSeg;
+  const int32_t cand_cap = getenv("COOC_RS_SPLIT_CAP") ? std::min(kRsCand, std::max(1, atoi(getenv("COOC_RS_SPLIT_CAP")))) : kRsCand;
+  if (split) {
+    k_rs_seg_count<<<unsigned((int64_t(M) + 1 + 255) / 256), 256, 0, s>>>(M, src, nanrow, long_thr, seg_len, nseg);
+  } else {
+    COOC_HIP_TRY(hipMemsetAsync(nseg, 0, sizeof(int32_t) * size_t(M + 1), s));
+  }
+  COOC_HIP_TRY(hipMemsetAsync(ustate + scan_state_words(int64_t(M) + 1), 0, sizeof(int64_t), s));
+  COOC_TRY(launch_scan<false>(ScanI32{nseg}, segp, int64_t(M) + 1, ustate,
+                              reinterpret_cast<int64_t *>(ustate + scan_state_words(int64_t(M) + 1)), s));
   const char *nx = getenv("COOC_RS_NO_NAN_EXIT");
   const int32_t no_nan_exit = (nx && nx[0] == '1') ? 1 : 0;
   const size_t lds = sizeof(double) * kR5Waves * size_t(topk + 1) + sizeof(int32_t) * kR5Waves * size_t(topk + 1);
@@ -1681,7 +1825,8 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   const int64_t want = (int64_t(M) + kR5Waves - 1) / kR5Waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * std::max(1, per_cu))));
   k_rs_heap<<<grid, 64 * kR5Waves, lds, s>>>(M, src, sbase, score, ctr + 8, topk, out_size, out_val, out_score,
-                                             no_nan_exit, getenv("COOC_RS_HEAP_SKIP") ? atoll(getenv("COOC_RS_HEAP_SKIP")) : 0);
+                                             no_nan_exit, getenv("COOC_RS_HEAP_SKIP") ? atoll(getenv("COOC_RS_HEAP_SKIP")) : 0,
+                                             segp, cand, ncand, segdone, seg_len, cand_cap);
   COOC_HIP_TRY(hipGetLastError());
   return Status::Ok();
 }
@@ -1699,7 +1844,7 @@ Status launch_rescore_batch(hipStream_t s, int32_t M, const int64_t *row_base, c
     return launch_rescore_rows(s, nullptr, obs3 + 2, M, DenseRows{dense, M}, M, rowsum, obs3, exact, topk, terms,
                                out_size, out_val, out_score);
   // the two passes for whole-log row sums (numeric heaps), k_rescore3 otherwise; COOC_RS_TWO_PASS=1 / 0 forces
-  static const int tp_env = getenv("COOC_RS_TWO_PASS") ? atoi(getenv("COOC_RS_TWO_PASS")) : -1;
+  const int tp_env = getenv("COOC_RS_TWO_PASS") ? atoi(getenv("COOC_RS_TWO_PASS")) : -1;  // (read per call: tests)
   const bool two_pass = (tp_env < 0 ? whole_log : tp_env != 0) && !unordered && nnz >= 0 && topk <= 1024;
   if (two_pass)
     return launch_rescore_two_pass(s, M, CsrRows{row_base, row_nnz, col, cnt}, rank_of, rowsum, obs3, exact, topk, nnz,
