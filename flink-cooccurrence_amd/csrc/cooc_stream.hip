@@ -1033,14 +1033,16 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
       if (len > 0) {
         const int32_t a = int32_t(t);
         const int64_t rs_a = rs_row_sum(grs, a, exact);
-        const RowTerms R(observed, rs_a);
+        // RowTerms from the tables (the same xlogx of the same integers): x(rs_a) = trow[a][0].x, x(rs_a - 1) =
+        // trow[a][1].x, x(observed + 2 - rs_a) = trow[a][1].y, x(observed + 2) = the k11 table at k11 = 1
+        const double *tr = trow + int64_t(a) * kRsTK * 2;
         it.src[lane] = src.base(a) + e0;
         it.dst[lane] = sbase[t] + e0;
         it.rs[lane] = rs_a;
-        it.rt[lane][0] = R.x_a;
-        it.rt[lane][1] = R.x_all1;
-        it.rt[lane][2] = R.x_r1;
-        it.rt[lane][3] = R.x_a1;
+        it.rt[lane][0] = tr[0];
+        it.rt[lane][1] = k11t[1 + 32768 + 65536];
+        it.rt[lane][2] = tr[3];
+        it.rt[lane][3] = tr[2];
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
