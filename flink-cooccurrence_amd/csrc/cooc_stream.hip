@@ -814,6 +814,17 @@ __global__ __launch_bounds__(64 * kR3Waves) void k_rescore3(
 // path for whole-log row sums, whose heaps are numeric (the C5 owner unit: 2.7% NaN roots); k_rescore3 keeps the
 // local-row-sum case, whose roots are NaN almost everywhere and whose rows end after one step.
 constexpr int kRsB = 64;                                  // column blocks
+// Pass 1 stores, per entry, not its score but an upper bound of it: the score rounded up to f32 (4 B).  Pass 2
+// offers the heap an entry only when the bound is above the heap's root (or the heap is not full) and recomputes
+// that entry's exact score then (LogLikelihood.java:41-57 over the same integers: the same bits); an entry whose
+// bound is <= the root has a score <= the root and the reference would not take it (score > getLeastScore(),
+// ItemRowRescorer...java:218-222).  About 1% of the entries are recomputed; 4 B per entry are written and read
+// instead of 8.  A NaN score is stored as a quiet NaN (its bound compares false: recomputed); a zero count as
+// kRsZero32.
+constexpr uint32_t kRsZero32 = 0x7F80DEADu;               // (a signalling NaN: no rounding result has these bits)
+__device__ inline uint32_t rs_bound(double sc) {
+  return sc != sc ? 0x7FC00000u : __float_as_uint(__double2float_ru(sc));
+}
 constexpr uint64_t kRsZero = 0x7FF0000000000DEAull;      // pass 1's mark of a zero count (a signalling NaN: no
                                                           // arithmetic result has these bits)
 __device__ inline int32_t rs_blk(const int32_t *__restrict__ rank_of, int32_t c, int32_t bw) {
@@ -905,7 +916,7 @@ __device__ inline int rs_item_row(const RsItem &it, int32_t k) {
 __device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const double *xt,
                                      const double *__restrict__ k11t, const double *__restrict__ trow,
                                      const double *__restrict__ tcol, int64_t observed, int32_t exact,
-                                     uint64_t *__restrict__ score, int32_t *__restrict__ nanrow) {
+                                     uint32_t *__restrict__ score, int32_t *__restrict__ nanrow) {
 #pragma clang fp contract(off)
   if (!on) return;
   const int32_t k = it.qk[j];
@@ -939,7 +950,7 @@ __device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const dou
   }
   const double sc = llr_terms(x_all, it.rt[r][0], x_2122, it.qxrs[j], x_1222, x_11, x_12, x_21, xlogx(k22));
   if (sc != sc) nanrow[it.t0 + r] = 1;
-  score[it.dst[r] + (k - it.off[r])] = uint64_t(__double_as_longlong(sc));
+  score[it.dst[r] + (k - it.off[r])] = rs_bound(sc);
 }
 // Work units of pass 1: the items (64 consecutive rows x one block; queue q = block % 8 holds its blocks' items in
 // block order, so item g = q per_q + (b / 8) n_chunks + chunk) cut into pieces of at most kRsP entries, so that
@@ -981,7 +992,7 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
                                                   const double *__restrict__ trow, const double *__restrict__ tcol,
                                                   const int64_t *__restrict__ obs, int32_t exact,
                                                   const int64_t *__restrict__ ubase, const int32_t *__restrict__ umap,
-                                                  unsigned long long *__restrict__ qctr, uint64_t *__restrict__ score,
+                                                  unsigned long long *__restrict__ qctr, uint32_t *__restrict__ score,
                                                   int32_t *__restrict__ nanrow, int32_t exp) {
 #pragma clang fp contract(off)
   __shared__ RsItem items[4];
@@ -1091,18 +1102,16 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
           const bool valid = k < ke;
           const bool slow = valid && vA[u] != 0u && k11 != 1;
           if (valid && !slow) {
-            uint64_t bits = kRsZero;
+            uint32_t bits = kRsZero32;
             if (vA[u] != 0u) {  // ItemRowRescorer...java:203-205,230-240 (xlogx(1) = 0)
               const int64_t rs_a = it.rs[r];
               const int64_t k22 = observed + k11 - (rs_a - k11) - (h[u].rs - k11);
-              bits = uint64_t(__double_as_longlong(llr_terms(it.rt[r][1], it.rt[r][0], it.rt[r][2], h[u].x_rs,
-                                                             h[u].x_or2, 0.0, it.rt[r][3], h[u].x_rs1,
-                                                             (exp & 2) ? double(k22) : xlogx(k22))));
+              const double sc = llr_terms(it.rt[r][1], it.rt[r][0], it.rt[r][2], h[u].x_rs, h[u].x_or2, 0.0,
+                                          it.rt[r][3], h[u].x_rs1, (exp & 2) ? double(k22) : xlogx(k22));
+              if (sc != sc) nanrow[it.t0 + r] = 1;  // (a NaN score: the row's heap pass cannot be split, k_rs_heap)
+              bits = rs_bound(sc);
             }
-            if ((bits & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (bits & 0xFFFFFFFFFFFFFull) != 0 &&
-                bits != kRsZero)
-              nanrow[it.t0 + r] = 1;  // (a NaN score: the row's heap pass cannot be split, k_rs_heap)
-            if (!(exp & 8) || bits == 0x1234ull) score[it.dst[r] + (k - it.off[r])] = bits;
+            if (!(exp & 8) || bits == 0x1234u) score[it.dst[r] + (k - it.off[r])] = bits;
           }
           const uint64_t sm = __ballot(slow);
           if (slow) {
@@ -1152,9 +1161,8 @@ __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, c
 #define COOC_R5_WAVES 4
 #endif
 constexpr int kR5Waves = COOC_R5_WAVES, kR5Slots = COOC_R5_SLOTS, kR5L = COOC_R5_L;
-struct R5Slot {  // a step's scores (the heap holds entry indices: the columns are read for the k kept, at the end)
-  uint32_t slo[64];
-  uint32_t shi[64];
+struct R5Slot {  // a step's score bounds (the heap holds entry indices: the columns are read for the k kept, at the end)
+  uint32_t ub[64];
 };
 // Rows longer than kRsLong entries whose scores hold no NaN are cut into segments of kRsSeg entries, one wave each:
 // a segment feeds a heap of its own from empty and keeps, in order, every entry that heap could take (at most
@@ -1176,36 +1184,72 @@ __global__ void k_rs_seg_count(int64_t n_rows, CsrRows src, const int32_t *__res
   nseg[t] = (n > long_thr && !nanrow[t]) ? int32_t((n + seg_len - 1) / seg_len) : 0;
 }
 
-// Streams entries [i0, i1) of a row through the wave's ring into its heap (hv, hs, size, least); kSeg: also records
-// the entries offered (a superset of those taken) as segment-relative u16 indices in cand[0, kRsCand), *nc counting
-// them all.
+// The exact score of entry i of row a (pass 2's recomputation): LogLikelihood.java:41-57 over k11 (the entry's
+// count or its int16 view), k12 = rs_a - k11, k21 = rs_b - k11, k22 = observed + k11 - k12 - k21
+// (ItemRowRescorer...java:230-240) -- the integers pass 1 used, so the same bits.
+struct RsExact {
+  const int64_t *grs;
+  int64_t observed;
+  int32_t exact;
+  __device__ double operator()(CsrRows src, int64_t rb, int64_t i, int64_t rs_a) const {
+#pragma clang fp contract(off)
+    const int32_t c = src.col[rb + i];
+    const uint32_t v = src.cnt[rb + i];
+    const int64_t k11 = exact ? int64_t(v) : int64_t(int16_t(uint16_t(v)));
+    const int64_t rs_b = rs_row_sum(grs, c, exact);
+    const int64_t k12 = rs_a - k11, k21 = rs_b - k11;
+    return llr(k11, k12, k21, observed + k11 - k12 - k21);
+  }
+};
+
+// Feeds one step's offers (lanes with c >= 0, exact scores sc) to the heap in lane order; returns the offer mask.
+__device__ inline uint64_t rs_feed(bool cand, int32_t c, double sc, int32_t topk, int32_t *hv, double *hs,
+                                   int32_t &size, double &least) {
+  const uint64_t m0 = __ballot(cand && (size < topk || sc > least));
+  uint64_t m = m0;
+  while (m) {  // in lane order: the reference's sequential offers
+    const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
+    m &= m - 1;
+    const double s_l = __shfl(sc, l, 64);
+    const int32_t c_l = __shfl(c, l, 64);
+    if (size < topk) {
+      heap_add(hv, hs, size, c_l, s_l);
+    } else if (s_l > hs[1]) {
+      heap_update(hv, hs, size, c_l, s_l);
+    }
+    least = hs[1];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return m0;
+}
+
+// Streams entries [i0, i1) of a row's score bounds through the wave's ring into its heap (hv, hs, size, least);
+// kSeg: also records the entries offered (a superset of those taken) as segment-relative u16 indices in
+// cand[0, cand_cap), *nc counting them all.
 template <bool kSeg>
-__device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint64_t *__restrict__ score, int64_t rb, int64_t sb,
-                                 int64_t i0, int64_t i1, int32_t topk, int32_t *hv, double *hs, int32_t &size,
-                                 double &least, int32_t no_nan_exit, uint16_t *__restrict__ cand, int32_t cand_cap,
-                                 int32_t &nc) {
+__device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint32_t *__restrict__ score, RsExact ex, int64_t rs_a,
+                                 int64_t rb, int64_t sb, int64_t i0, int64_t i1, int32_t topk, int32_t *hv, double *hs,
+                                 int32_t &size, double &least, int32_t no_nan_exit, uint16_t *__restrict__ cand,
+                                 int32_t cand_cap, int32_t &nc) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const int64_t n = i1 - i0;
   const int64_t nsteps = (n + 63) >> 6;
   for (int64_t j = -kR5L; j < nsteps; j++) {
-    {  // step j + L (clamped to the range's last entry past its end: every step issues 2 DMAs)
+    {  // step j + L (clamped to the range's last entry past its end: every step issues 1 DMA)
       const int64_t jl = j + kR5L;
       const int64_t e = i0 + min(jl * 64 + lane, n - 1);
-      R5Slot &sl = rg[jl & (kR5Slots - 1)];
-      const uint32_t *sp = reinterpret_cast<const uint32_t *>(score + sb + e);
-      __builtin_amdgcn_global_load_lds(sp, R3_LDS(sl.slo), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds(sp + 1, R3_LDS(sl.shi), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(score + sb + e, R3_LDS(rg[jl & (kR5Slots - 1)].ub), 4, 0, 0);
     }
     if (j < 0) continue;
-    r3_wait_vm<2 * kR5L>();  // step j's DMAs (issued L steps ago) have landed
-    const R5Slot &sl = rg[j & (kR5Slots - 1)];
-    const bool in_row = j * 64 + lane < n;
-    const uint64_t bits = in_row ? (uint64_t(r3_rd32(&sl.shi[lane])) << 32) | uint64_t(r3_rd32(&sl.slo[lane]))
-                                 : kRsZero;
-    const int32_t c = bits != kRsZero ? int32_t(i0 + j * 64 + lane) : -1;  // the entry's index in the row
-    const double sc = __longlong_as_double(int64_t(bits));
-    uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
+    r3_wait_vm<kR5L>();  // step j's DMA (issued L steps ago) has landed
+    const int64_t i = i0 + j * 64 + lane;
+    const uint32_t ub = j * 64 + lane < n ? r3_rd32(&rg[j & (kR5Slots - 1)].ub[lane]) : kRsZero32;
+    // an offer only if the bound is above the root (or the heap is not full): then the exact score
+    const bool offer = ub != kRsZero32 && (size < topk || !(double(__uint_as_float(ub)) <= least));
+    const double sc = offer ? ex(src, rb, i, rs_a) : 0.0;
+    const uint64_t m = rs_feed(offer, int32_t(i), sc, topk, hv, hs, size, least);
     if (kSeg) {
       if ((m >> lane) & 1ull) {
         const int32_t q = nc + int32_t(__popcll(m & lt));
@@ -1213,34 +1257,22 @@ __device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint64_t *__rest
       }
       nc += int32_t(__popcll(m));
     }
-    while (m) {  // in lane order: the reference's sequential offers
-      const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
-      m &= m - 1;
-      const double s_l = __shfl(sc, l, 64);
-      const int32_t c_l = __shfl(c, l, 64);
-      if (size < topk) {
-        heap_add(hv, hs, size, c_l, s_l);
-      } else if (s_l > hs[1]) {
-        heap_update(hv, hs, size, c_l, s_l);
-      }
-      least = hs[1];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
   }
   r3_wait_vm<0>();  // (the ring's last DMAs: the next range reuses the slots)
 }
 
 // pass 2: units [0, n_seg) are the long rows' segments, then one unit per row (a long row's own unit is skipped);
-// one wave per unit, units taken 4 at a time.  A row streams its scores through a kR5Slots-slot LDS-DMA ring (2 DMAs
-// per step of 64 entries issued kR5L steps ahead; counted waits as in k_rescore3) into the heap in column order (the
-// sequential loop of ItemRowRescorer...java:199-223), ending at a full heap with a NaN root.  The heap orders by
-// score alone (IntDoublePriorityQueue.java:132-205), so it holds entry indices and the k kept columns are read at
-// the end: 8 B streamed per entry, not 12.
+// one wave per unit, units taken 4 at a time.  A row streams its score bounds through a kR5Slots-slot LDS-DMA ring
+// (one DMA per step of 64 entries issued kR5L steps ahead; counted waits as in k_rescore3) into the heap in column
+// order (the sequential loop of ItemRowRescorer...java:199-223), ending at a full heap with a NaN root.  The heap
+// orders by score alone (IntDoublePriorityQueue.java:132-205), so it holds entry indices and the k kept columns
+// are read at the end.
 __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRows src,
                                                           const int64_t *__restrict__ sbase,
-                                                          const uint64_t *__restrict__ score,
+                                                          const uint32_t *__restrict__ score,
+                                                          const int64_t *__restrict__ grs,
+                                                          const int64_t *__restrict__ obs, int32_t exact,
                                                           unsigned long long *__restrict__ row_ctr, int32_t topk,
                                                           int32_t *__restrict__ out_size, int32_t *__restrict__ out_val,
                                                           double *__restrict__ out_score, int32_t no_nan_exit,
@@ -1254,6 +1286,7 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + kR5Waves * (topk + 1)) + int64_t(wave) * (topk + 1);
   R5Slot *rg = ring[wave];
+  const RsExact ex{grs, exact ? obs[1] : obs[0], exact};
   const int64_t n_seg = segp[n_rows], n_units = n_seg + n_rows;
   int64_t u_next = 0, u_end = 0;
   for (;;) {
@@ -1274,8 +1307,9 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       }
       t = lo;
       const int64_t n = src.size(int32_t(t)), rb = src.base(int32_t(t)), sb = sbase[t];
+      const int64_t rs_a = rs_row_sum(ex.grs, int32_t(t), ex.exact);
       const int64_t s0 = segp[t], ns = segp[t + 1] - s0, i0 = (u - s0) * seg_len;
-      rs_stream<true>(rg, src, score, rb, sb, i0, min(n, i0 + seg_len), topk, hv, hs, size, least, 1,
+      rs_stream<true>(rg, src, score, ex, rs_a, rb, sb, i0, min(n, i0 + seg_len), topk, hv, hs, size, least, 1,
                       cand + u * kRsCand, cand_cap, nc);
       if (lane == 0) ncand[u] = nc;
       __threadfence();  // (the kept entries and their count, before the row's segment count)
@@ -1287,33 +1321,16 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       bool whole = false;
       for (int64_t q = 0; q < ns; q++) whole |= ncand[s0 + q] > cand_cap;
       if (whole) {
-        rs_stream<false>(rg, src, score, rb, sb, 0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0, nc);
+        rs_stream<false>(rg, src, score, ex, rs_a, rb, sb, 0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0,
+                         nc);
       } else {
         for (int64_t q = 0; q < ns; q++) {
           const int32_t cq = ncand[s0 + q];
           for (int32_t j0 = 0; j0 < cq; j0 += 64) {
-            int32_t c = -1;
-            double sc = 0.0;
-            if (j0 + lane < cq) {
-              const int64_t i = q * seg_len + cand[(s0 + q) * kRsCand + j0 + lane];
-              c = int32_t(i);
-              sc = __longlong_as_double(int64_t(score[sb + i]));
-            }
-            uint64_t m = __ballot(c >= 0 && (size < topk || sc > least));
-            while (m) {
-              const int l = __ffsll(static_cast<unsigned long long>(m)) - 1;
-              m &= m - 1;
-              const double s_l = __shfl(sc, l, 64);
-              const int32_t c_l = __shfl(c, l, 64);
-              if (size < topk) {
-                heap_add(hv, hs, size, c_l, s_l);
-              } else if (s_l > hs[1]) {
-                heap_update(hv, hs, size, c_l, s_l);
-              }
-              least = hs[1];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            const bool on = j0 + lane < cq;
+            const int64_t i = on ? q * seg_len + cand[(s0 + q) * kRsCand + j0 + lane] : 0;
+            const double sc = on ? ex(src, rb, i, rs_a) : 0.0;
+            rs_feed(on, int32_t(i), sc, topk, hv, hs, size, least);
           }
         }
       }
@@ -1323,8 +1340,8 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       if (segp[t + 1] > segp[t]) continue;  // (its segments serve it)
       const int64_t n = (exp_skip > 0 && n0 > exp_skip) ? 0 : n0;  // (timing experiment)
       if (n > 0)
-        rs_stream<false>(rg, src, score, src.base(int32_t(t)), sbase[t], 0, n, topk, hv, hs, size, least, no_nan_exit,
-                         nullptr, 0, nc);
+        rs_stream<false>(rg, src, score, ex, rs_row_sum(ex.grs, int32_t(t), ex.exact), src.base(int32_t(t)), sbase[t],
+                         0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0, nc);
     }
     out_size[t] = size;
     if (size > 0) {
@@ -1753,14 +1770,14 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   const size_t o_ncand = al(o_segp + sizeof(int64_t) * size_t(M + 1));
   const size_t o_cand = al(o_ncand + sizeof(int32_t) * size_t(n_seg_max));
   const size_t o_score = al(o_cand + sizeof(uint16_t) * size_t(n_seg_max) * kRsCand);
-  COOC_TRY(terms.reserve(o_score + sizeof(uint64_t) * size_t(std::max<int64_t>(nnz, 1))));
+  COOC_TRY(terms.reserve(o_score + sizeof(uint32_t) * size_t(std::max<int64_t>(nnz, 1))));
   char *base = static_cast<char *>(terms.p);
   auto *ctr = reinterpret_cast<unsigned long long *>(base + o_ctr);  // [0, 8) pass-1 queues, [8] pass-2 rows
   auto *k11t = reinterpret_cast<double *>(base + o_k11);
   auto *state = reinterpret_cast<unsigned long long *>(base + o_state);
   auto *sbase = reinterpret_cast<int64_t *>(base + o_sbase);
   auto *bp = reinterpret_cast<int32_t *>(base + o_bp);
-  auto *score = reinterpret_cast<uint64_t *>(base + o_score);
+  auto *score = reinterpret_cast<uint32_t *>(base + o_score);
   auto *trow = reinterpret_cast<double *>(base + o_trow);
   auto *units = reinterpret_cast<int32_t *>(base + o_units);
   auto *ubase = reinterpret_cast<int64_t *>(base + o_ubase);
@@ -1826,7 +1843,8 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   COOC_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rs_heap, 64 * kR5Waves, lds));
   const int64_t want = (int64_t(M) + kR5Waves - 1) / kR5Waves;
   const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * std::max(1, per_cu))));
-  k_rs_heap<<<grid, 64 * kR5Waves, lds, s>>>(M, src, sbase, score, ctr + 8, topk, out_size, out_val, out_score,
+  k_rs_heap<<<grid, 64 * kR5Waves, lds, s>>>(M, src, sbase, score, grs, obs, exact ? 1 : 0, ctr + 8, topk,
+                                             out_size, out_val, out_score,
                                              no_nan_exit, getenv("COOC_RS_HEAP_SKIP") ? atoll(getenv("COOC_RS_HEAP_SKIP")) : 0,
                                              segp, cand, ncand, segdone, seg_len, cand_cap);
   COOC_HIP_TRY(hipGetLastError());
