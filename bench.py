@@ -615,9 +615,10 @@ def main():
             "valu_busy": pmc_rs.get("valu_busy"), "limiter": limiter(pmc_rs, t_rs, tk),
             "pmc_source_digest": pmc_rs.get("source_digest") or pmc_rs.get("stale_source_digest"),
             "pmc_stale": rs_stale,
-            # what the two passes move by design: pass 1 reads every entry (8 B) and writes its score (8 B), pass 2
-            # reads the column and score (12 B) of the entries it feeds (rows end at a NaN root)
-            "two_pass_bytes_model": (16.0 * D + 12.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M)
+            # what the two passes move by design: pass 1 reads every entry (8 B) and writes its score's f32 bound
+            # (4 B), pass 2 reads the bounds (4 B) of the entries it walks (rows end at a NaN root); the ~1% it
+            # rescores exactly are not counted
+            "two_pass_bytes_model": (12.0 * D + 4.0 * D_rs + 20.0 * M + M * (4.0 + 12.0 * args.topk) + 32.0 * M)
             if two_pass else None,
             "note": "B = 8D_read + 20M + M(4 + 12k) + 32M per launch (entries read: rows behind a NaN heap root "
                     "end early; row headers and sums, heaps, 32-B column terms), over the HIP-event time of the "
