@@ -806,11 +806,12 @@ __global__ __launch_bounds__(64 * kR3Waves) void k_rescore3(
 // column block -- kRsB blocks of the row order's columns (ascending rank_of[col], or col), block b's work queued on
 // counter b % 8 in block order and taken first by the workgroups with blockIdx % 8 == b % 8 (one XCD under the
 // round-robin placement; speed only, any workgroup may take any item), so at any time an XCD gathers from the terms
-// of about one block (~0.5 MB) -- and writes every score (8 B) to a dense array beside the entries; pass 2
-// (k_rs_heap) streams each row's columns and scores in order through an LDS-DMA ring and feeds the heap exactly as
-// k_rescore3 does (the sequential loop of ItemRowRescorer...java:199-223; NaN roots end the row).  The scores are
-// k_rescore3's bit for bit: the same formulas over the same integers (the row-only and count-only terms through
-// xlogx or the k11 tables of the same argument).  Pass 1 scores every entry (no NaN-root exit), so this is the
+// of about one block (~0.5 MB) -- and writes every score's f32 upper bound (4 B) to a dense array beside the
+// entries; pass 2 (k_rs_heap) streams each row's bounds in order through an LDS-DMA ring, recomputes the exact
+// score of the entries whose bound beats the heap's root, and feeds those to the heap exactly as k_rescore3 does
+// (the sequential loop of ItemRowRescorer...java:199-223; NaN roots end the row).  The scores are k_rescore3's bit
+// for bit: the same formulas over the same integers (the row-only and count-only terms through xlogx or the k11
+// tables of the same argument).  Pass 1 scores every entry (no NaN-root exit), so this is the
 // path for whole-log row sums, whose heaps are numeric (the C5 owner unit: 2.7% NaN roots); k_rescore3 keeps the
 // local-row-sum case, whose roots are NaN almost everywhere and whose rows end after one step.
 constexpr int kRsB = 64;                                  // column blocks
@@ -825,8 +826,6 @@ constexpr uint32_t kRsZero32 = 0x7F80DEADu;               // (a signalling NaN: 
 __device__ inline uint32_t rs_bound(double sc) {
   return sc != sc ? 0x7FC00000u : __float_as_uint(__double2float_ru(sc));
 }
-constexpr uint64_t kRsZero = 0x7FF0000000000DEAull;      // pass 1's mark of a zero count (a signalling NaN: no
-                                                          // arithmetic result has these bits)
 __device__ inline int32_t rs_blk(const int32_t *__restrict__ rank_of, int32_t c, int32_t bw) {
   return min(kRsB - 1, (rank_of ? rank_of[c] : c) / bw);
 }
