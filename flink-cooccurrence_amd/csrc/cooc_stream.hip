@@ -834,7 +834,9 @@ __device__ inline int32_t rs_blk(const int32_t *__restrict__ rank_of, int32_t c,
 // per row, lane b binary-searching bound b over the row's block ids (about log2(n) probes per bound instead of a
 // rank lookup per entry)
 __global__ __launch_bounds__(256) void k_rs_bounds(int64_t n_rows, CsrRows src, const int32_t *__restrict__ rank_of,
-                                                   int32_t bw, int32_t *__restrict__ bp) {
+                                                   int32_t bw, int32_t *__restrict__ bp, int64_t per_q,
+                                                   int32_t *__restrict__ item_len) {
+  static_assert(kRsB == 64, "one bound per lane");
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   for (int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; t < n_rows; t += n_waves) {
@@ -851,6 +853,11 @@ __global__ __launch_bounds__(256) void k_rs_bounds(int64_t n_rows, CsrRows src, 
     }
     o[lane] = lo;
     if (lane == 0) o[kRsB] = max(n, 0);
+    // the row's share of its work items' entries (item g = (b % 8) per_q + (b / 8) n_chunks + t / 64)
+    const int32_t above = __shfl_down(lo, 1, 64);  // (every lane takes part in the shuffle)
+    const int32_t next = lane < 63 ? above : max(n, 0);
+    if (next > lo)
+      atomicAdd(item_len + int64_t(lane & 7) * per_q + int64_t(lane >> 3) * ((n_rows + 63) >> 6) + (t >> 6), next - lo);
   }
 }
 
@@ -954,35 +961,22 @@ __device__ inline void rs_score_slow(const RsItem &it, int j, bool on, const dou
 // Work units of pass 1: the items (64 consecutive rows x one block; queue q = block % 8 holds its blocks' items in
 // block order, so item g = q per_q + (b / 8) n_chunks + chunk) cut into pieces of at most kRsP entries, so that
 // no wave is left alone with the hot rows' items (the Zipf head: ~1e5 entries per item).  units[g] = the item's
-// pieces (units[n] = 0: ubase[n], the exclusive prefix, is the total); umap[u] = the item of unit u.
+// pieces (item_len[g]: the item's entries, summed by k_rs_bounds; item_len[n] = 0, so ubase[n], the exclusive
+// prefix of the pieces, is the total); umap[u] = the item of unit u.
 #ifndef COOC_RS_P
 #define COOC_RS_P 4096  // (A/B builds)
 #endif
 constexpr int32_t kRsP = COOC_RS_P;
-__global__ __launch_bounds__(256) void k_rs_items(int64_t n_rows, const int32_t *__restrict__ bp, int64_t per_q,
-                                                  int32_t *__restrict__ units) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n_chunks = (n_rows + 63) >> 6;
-  const int64_t n = per_q * 8;
-  const int64_t g = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  if (g > n) return;
-  if (g == n) {
-    if (lane == 0) units[n] = 0;
-    return;
-  }
-  const int64_t i = g % per_q;
-  const int b = int(g / per_q) + 8 * int(i / n_chunks);
-  const int64_t t = ((i % n_chunks) << 6) + lane;
-  int32_t len = t < n_rows ? bp[t * (kRsB + 1) + b + 1] - bp[t * (kRsB + 1) + b] : 0;
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) len += __shfl_xor(len, d, 64);
-  if (lane == 0) units[g] = (len + kRsP - 1) / kRsP;
-}
-__global__ void k_rs_unit_map(int64_t n, const int32_t *__restrict__ units, const int64_t *__restrict__ ubase,
+struct ScanUnits {  // the pieces of item g, from its entry count (k_rs_bounds)
+  const int32_t *len;
+  __device__ int64_t operator()(int64_t g) const { return (int64_t(len[g]) + kRsP - 1) / kRsP; }
+};
+__global__ void k_rs_unit_map(int64_t n, const int32_t *__restrict__ item_len, const int64_t *__restrict__ ubase,
                               int32_t *__restrict__ umap) {
   const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (g >= n) return;
-  for (int32_t p = 0; p < units[g]; p++) umap[ubase[g] + p] = int32_t(g);
+  const int64_t np = ScanUnits{item_len}(g);
+  for (int64_t p = 0; p < np; p++) umap[ubase[g] + p] = int32_t(g);
 }
 
 __global__ __launch_bounds__(256) void k_rs_score(int64_t n_rows, CsrRows src, const int32_t *__restrict__ bp,
@@ -1807,12 +1801,14 @@ Status launch_rescore_two_pass(hipStream_t s, int32_t M, CsrRows src, const int3
   const int32_t bw = int32_t((int64_t(M) + kRsB - 1) / kRsB);
   k_rs_tables<<<unsigned((int64_t(M) * kRsTK + 255) / 256), 256, 0, s>>>(M, src.row_nnz, grs, obs, exact ? 1 : 0, trow,
                                                                           tcol);
-  k_rs_bounds<<<unsigned(std::min<int64_t>((int64_t(M) + 3) / 4, int64_t(n_cu) * 8)), 256, 0, s>>>(M, src, rank_of, bw, bp);
-  // the work units (k_rs_items, a scan, k_rs_unit_map): at most n_items + nnz / kRsP of them
+  // the work units (the items' entries summed by k_rs_bounds, a scan of their pieces, k_rs_unit_map): at most
+  // n_items + nnz / kRsP of them
   const int64_t n_chunks = (int64_t(M) + 63) >> 6, per_q = n_chunks * (kRsB / 8), n_items = per_q * 8;
-  k_rs_items<<<unsigned((n_items + 1 + 3) / 4), 256, 0, s>>>(M, bp, per_q, units);
+  COOC_HIP_TRY(hipMemsetAsync(units, 0, sizeof(int32_t) * size_t(n_items + 1), s));
+  k_rs_bounds<<<unsigned(std::min<int64_t>((int64_t(M) + 3) / 4, int64_t(n_cu) * 8)), 256, 0, s>>>(M, src, rank_of, bw, bp,
+                                                                                                 per_q, units);
   COOC_HIP_TRY(hipMemsetAsync(ustate + scan_state_words(n_items + 1), 0, sizeof(int64_t), s));
-  COOC_TRY(launch_scan<false>(ScanI32{units}, ubase, n_items + 1, ustate,
+  COOC_TRY(launch_scan<false>(ScanUnits{units}, ubase, n_items + 1, ustate,
                               reinterpret_cast<int64_t *>(ustate + scan_state_words(n_items + 1)), s));
   k_rs_unit_map<<<unsigned((n_items + 255) / 256), 256, 0, s>>>(n_items, units, ubase, umap);
   int per_cu1 = 1;  // (a persistent grid: the work comes from the queues)
