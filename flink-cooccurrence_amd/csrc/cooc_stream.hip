@@ -1221,14 +1221,30 @@ __device__ inline uint64_t rs_feed(bool cand, int32_t c, double sc, int32_t topk
 // kSeg: also records the entries offered (a superset of those taken) as segment-relative u16 indices in
 // cand[0, cand_cap), *nc counting them all.
 template <bool kSeg>
-__device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint32_t *__restrict__ score, RsExact ex, int64_t rs_a,
-                                 int64_t rb, int64_t sb, int64_t i0, int64_t i1, int32_t topk, int32_t *hv, double *hs,
-                                 int32_t &size, double &least, int32_t no_nan_exit, uint16_t *__restrict__ cand,
-                                 int32_t cand_cap, int32_t &nc) {
+__device__ inline void rs_stream(R5Slot *rg, int32_t *qb, CsrRows src, const uint32_t *__restrict__ score, RsExact ex,
+                                 int64_t rs_a, int64_t rb, int64_t sb, int64_t i0, int64_t i1, int32_t topk,
+                                 int32_t *hv, double *hs, int32_t &size, double &least, int32_t no_nan_exit,
+                                 uint16_t *__restrict__ cand, int32_t cand_cap, int32_t &nc) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const int64_t n = i1 - i0;
   const int64_t nsteps = (n + 63) >> 6;
+  // Entries whose bound beats the root (as of the last feed: a superset of the offers) queue in qb in order; 64 at
+  // a time they are rescored exactly (full lanes, one drain of the ring per 64 instead of per step) and fed.
+  int32_t nq = 0;
+  auto flush = [&](int32_t cnt) {
+    const bool on = lane < cnt;
+    const int32_t ii = on ? qb[lane] : 0;
+    const double sc = on ? ex(src, rb, ii, rs_a) : 0.0;
+    const uint64_t m = rs_feed(on, ii, sc, topk, hv, hs, size, least);
+    if (kSeg) {
+      if ((m >> lane) & 1ull) {
+        const int32_t q = nc + int32_t(__popcll(m & lt));
+        if (q < cand_cap) cand[q] = uint16_t(ii - i0);
+      }
+      nc += int32_t(__popcll(m));
+    }
+  };
   for (int64_t j = -kR5L; j < nsteps; j++) {
     {  // step j + L (clamped to the range's last entry past its end: every step issues 1 DMA)
       const int64_t jl = j + kR5L;
@@ -1239,20 +1255,30 @@ __device__ inline void rs_stream(R5Slot *rg, CsrRows src, const uint32_t *__rest
     r3_wait_vm<kR5L>();  // step j's DMA (issued L steps ago) has landed
     const int64_t i = i0 + j * 64 + lane;
     const uint32_t ub = j * 64 + lane < n ? r3_rd32(&rg[j & (kR5Slots - 1)].ub[lane]) : kRsZero32;
-    // an offer only if the bound is above the root (or the heap is not full): then the exact score
+    // a possible offer only if the bound is above the root (or the heap is not full)
     const bool offer = ub != kRsZero32 && (size < topk || !(double(__uint_as_float(ub)) <= least));
-    const double sc = offer ? ex(src, rb, i, rs_a) : 0.0;
-    const uint64_t m = rs_feed(offer, int32_t(i), sc, topk, hv, hs, size, least);
-    if (kSeg) {
-      if ((m >> lane) & 1ull) {
-        const int32_t q = nc + int32_t(__popcll(m & lt));
-        if (q < cand_cap) cand[q] = uint16_t(j * 64 + lane);
-      }
-      nc += int32_t(__popcll(m));
+    const uint64_t b = __ballot(offer);
+    if (offer) qb[nq + int32_t(__popcll(b & lt))] = int32_t(i);
+    nq += int32_t(__popcll(b));
+    if (nq >= 64) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      flush(64);
+      const int32_t rest = lane + 64 < nq ? qb[lane + 64] : 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane + 64 < nq) qb[lane] = rest;
+      nq -= 64;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // (a full heap with a NaN root takes nothing more: the queued entries after it would be refused too)
+      if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
     }
-    if (!no_nan_exit && size == topk && __builtin_isnan(least)) break;
   }
   r3_wait_vm<0>();  // (the ring's last DMAs: the next range reuses the slots)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (nq > 0 && !(!no_nan_exit && size == topk && __builtin_isnan(least))) flush(nq);
 }
 
 // pass 2: units [0, n_seg) are the long rows' segments, then one unit per row (a long row's own unit is skipped);
@@ -1274,11 +1300,13 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
                                                           int32_t *__restrict__ segdone, int32_t seg_len,
                                                           int32_t cand_cap) {
   __shared__ R5Slot ring[kR5Waves][kR5Slots];
+  __shared__ int32_t qbuf[kR5Waves][128];
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double *hs = smem + int64_t(wave) * (topk + 1);
   int32_t *hv = reinterpret_cast<int32_t *>(smem + kR5Waves * (topk + 1)) + int64_t(wave) * (topk + 1);
   R5Slot *rg = ring[wave];
+  int32_t *qb = qbuf[wave];
   const RsExact ex{grs, exact ? obs[1] : obs[0], exact};
   const int64_t n_seg = segp[n_rows], n_units = n_seg + n_rows;
   int64_t u_next = 0, u_end = 0;
@@ -1302,7 +1330,7 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       const int64_t n = src.size(int32_t(t)), rb = src.base(int32_t(t)), sb = sbase[t];
       const int64_t rs_a = rs_row_sum(ex.grs, int32_t(t), ex.exact);
       const int64_t s0 = segp[t], ns = segp[t + 1] - s0, i0 = (u - s0) * seg_len;
-      rs_stream<true>(rg, src, score, ex, rs_a, rb, sb, i0, min(n, i0 + seg_len), topk, hv, hs, size, least, 1,
+      rs_stream<true>(rg, qb, src, score, ex, rs_a, rb, sb, i0, min(n, i0 + seg_len), topk, hv, hs, size, least, 1,
                       cand + u * kRsCand, cand_cap, nc);
       if (lane == 0) ncand[u] = nc;
       __threadfence();  // (the kept entries and their count, before the row's segment count)
@@ -1314,7 +1342,7 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       bool whole = false;
       for (int64_t q = 0; q < ns; q++) whole |= ncand[s0 + q] > cand_cap;
       if (whole) {
-        rs_stream<false>(rg, src, score, ex, rs_a, rb, sb, 0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0,
+        rs_stream<false>(rg, qb, src, score, ex, rs_a, rb, sb, 0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0,
                          nc);
       } else {
         for (int64_t q = 0; q < ns; q++) {
@@ -1333,7 +1361,7 @@ __global__ __launch_bounds__(64 * kR5Waves) void k_rs_heap(int64_t n_rows, CsrRo
       if (segp[t + 1] > segp[t]) continue;  // (its segments serve it)
       const int64_t n = (exp_skip > 0 && n0 > exp_skip) ? 0 : n0;  // (timing experiment)
       if (n > 0)
-        rs_stream<false>(rg, src, score, ex, rs_row_sum(ex.grs, int32_t(t), ex.exact), src.base(int32_t(t)), sbase[t],
+        rs_stream<false>(rg, qb, src, score, ex, rs_row_sum(ex.grs, int32_t(t), ex.exact), src.base(int32_t(t)), sbase[t],
                          0, n, topk, hv, hs, size, least, no_nan_exit, nullptr, 0, nc);
     }
     out_size[t] = size;
